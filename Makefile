@@ -1,0 +1,23 @@
+# libpcx.so: the MI355X (gfx950) kernels behind the C ABI in include/pcx.h.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+CXXFLAGS = -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Iinclude -Wall -Wno-unused-result \
+           -munsafe-fp-atomics
+SRC = $(wildcard phoneme_contrast_amd/csrc/*.hip)
+OBJ = $(patsubst phoneme_contrast_amd/csrc/%.hip,build/%.o,$(SRC))
+HDR = $(wildcard phoneme_contrast_amd/csrc/*.h) include/pcx.h
+LIB = phoneme_contrast_amd/libpcx.so
+
+all: $(LIB)
+
+build/%.o: phoneme_contrast_amd/csrc/%.hip $(HDR)
+	@mkdir -p build
+	$(HIPCC) $(CXXFLAGS) -c $< -o $@
+
+$(LIB): $(OBJ)
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJ)
+
+clean:
+	rm -rf build $(LIB)
+
+.PHONY: all clean

@@ -1,0 +1,74 @@
+/*
+ * libpcx — MI355X (gfx950) native kernels for the phoneme-contrast train step.
+ *
+ * C ABI only: plain pointers, sizes and a hipStream_t.  Every entry point is asynchronous on
+ * the given stream, never allocates or frees device memory (the caller passes workspaces sized
+ * by the matching *_workspace_bytes query), never synchronises the device, and returns
+ * PCX_OK or a negative error code; pcx_last_error() gives the message of the last failure on the
+ * calling thread.
+ *
+ * Reference interfaces replaced (paths relative to the reference checkout):
+ *   pcx_supcon_*      SupervisedContrastiveLoss.forward + its autograd backward
+ *                     (src/training/losses.py:41-86); NTXentLoss labelled branch
+ *                     (losses.py:101-151) is the same call with base_temperature = temperature.
+ *   pcx_net_*         PhonemeNet.forward (src/models/phoneme_cnn.py:98-126) and
+ *                     PhonemeNetDeep.forward (phoneme_cnn.py:274-304) with their autograd
+ *                     backward, train (batch-stat BatchNorm, Dropout2d) and eval mode.
+ *   pcx_adam_step     torch.optim.Adam.step with coupled weight decay as configured at
+ *                     scripts/train.py:129-133.
+ */
+#ifndef PCX_H_
+#define PCX_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PCX_OK 0
+#define PCX_EINVAL (-1)   /* bad argument / unsupported configuration */
+#define PCX_ESHAPE (-2)   /* tensor shape does not match the plan     */
+#define PCX_EHIP (-3)     /* HIP runtime error (launch failure, ...)  */
+#define PCX_EWORKSPACE (-5) /* workspace smaller than *_workspace_bytes */
+
+#define PCX_REDUCTION_MEAN 0
+#define PCX_REDUCTION_SUM 1
+#define PCX_REDUCTION_NONE 2
+
+/* library version (major*10000 + minor*100 + patch) */
+int pcx_version(void);
+/* copies the last error message of this thread into buf (NUL-terminated); returns its length */
+int pcx_last_error(char* buf, size_t n);
+
+/* ------------------------------------------------------------------ SupCon / NT-Xent loss
+ * features [B,D] fp32 row-major (assumed L2-normalised), labels [B] int64 or NULL,
+ * mask [B,B] fp32 row-major or NULL (exactly one of labels/mask must be given).
+ * Forward writes loss_out ([1] for mean/sum, [B] for none) and rowstats [B*4] (kept by the
+ * caller for the backward).  Backward writes dfeatures [B,D] = d(sum_i w_i loss_i)/dF where
+ * w_i comes from grad_out ([1] for mean/sum, [B] for none). */
+size_t pcx_supcon_workspace_bytes(int64_t B, int64_t D);
+int pcx_supcon_forward(const float* features, const int64_t* labels, const float* mask,
+                       int64_t B, int64_t D, float temperature, float base_temperature,
+                       int reduction, float* loss_out, float* rowstats,
+                       void* workspace, size_t workspace_bytes, hipStream_t stream);
+int pcx_supcon_backward(const float* features, const int64_t* labels, const float* mask,
+                        int64_t B, int64_t D, float temperature, float base_temperature,
+                        int reduction, const float* grad_out, const float* rowstats,
+                        float* dfeatures, void* workspace, size_t workspace_bytes,
+                        hipStream_t stream);
+
+/* ------------------------------------------------------------------ Adam (flat buffers)
+ * p, g, m, v: n fp32 each.  Coupled L2 (g += wd*p), bias correction with 1-based `step`.
+ * grad_scale multiplies g first (1/world_size after an all-reduce SUM). */
+int pcx_adam_step(float* p, const float* g, float* m, float* v, int64_t n, int64_t step,
+                  float lr, float beta1, float beta2, float eps, float weight_decay,
+                  float grad_scale, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PCX_H_ */

@@ -1,0 +1,67 @@
+// Shared device/host helpers for libpcx (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "pcx.h"
+
+namespace pcx {
+
+// ---------------------------------------------------------------- error state (host)
+void set_error(const char* fmt, ...);
+int hip_status(hipError_t e, const char* what);
+
+#define PCX_CHECK_ARG(cond, ...)                  \
+    do {                                          \
+        if (!(cond)) {                            \
+            ::pcx::set_error(__VA_ARGS__);        \
+            return PCX_EINVAL;                    \
+        }                                         \
+    } while (0)
+
+#define PCX_LAUNCH_CHECK(what)                                            \
+    do {                                                                  \
+        hipError_t _e = hipGetLastError();                                \
+        if (_e != hipSuccess) return ::pcx::hip_status(_e, what);         \
+    } while (0)
+
+// ---------------------------------------------------------------- device helpers
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int WAVE = 64;
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// D = A(32x2) * B(2x32) + C, exact f32 (v_mfma_f32_32x32x2_f32).
+// lane l supplies A[i=l&31][k=l>>5] and B[k=l>>5][j=l&31];
+// C/D register r of lane l holds (row (r&3)+8*(r>>2)+4*(l>>5), col l&31).
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// row of accumulator register r for lane half h (32x32 C/D layout)
+__device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+// combine lanes l and l^32 (the two row-halves of a 32x32 accumulator column)
+__device__ __forceinline__ float half_sum(float v) { return v + __shfl_xor(v, 32, 64); }
+__device__ __forceinline__ float half_max(float v) { return fmaxf(v, __shfl_xor(v, 32, 64)); }
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+
+inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+}  // namespace pcx

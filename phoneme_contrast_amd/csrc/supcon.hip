@@ -1,0 +1,350 @@
+// Supervised-contrastive loss (SupCon) forward + closed-form backward on fp32 MFMA.
+//
+// Replaces SupervisedContrastiveLoss.forward (reference src/training/losses.py:41-86) and the
+// autograd graph behind it.  S = F F^T is never materialised: every kernel recomputes its
+// 32x32 tiles of S with v_mfma_f32_32x32x2_f32 (exact f32) from the L2-resident features.
+//
+// The tile is computed TRANSPOSED, C'[j][i] = S_ij with A = F_j, B = F_i, so each lane owns one
+// anchor row i (its MFMA column) and 16 candidate columns j in its accumulator registers:
+// the per-anchor reductions (max, sum-exp, positive sums) are in-lane plus one half swap, and
+// the same registers are directly the A operand of the gradient product dF_i = sum_j H_ij F_j.
+//
+// Numerics follow the reference exactly: row max over ALL j (diagonal included, detached),
+// den_i = sum_{j != i} exp(S_ij/T - m_i) + 1e-6, rows without positives divide by 1 and still
+// count in the mean, loss scaled by T / base_T.
+#include "pcx_common.h"
+
+namespace pcx {
+namespace {
+
+constexpr int TILE = 32;
+constexpr int WAVES = 4;
+
+struct RowPart {  // online log-sum-exp partial for one anchor row
+    float m, s, pos, msum;
+};
+
+__device__ __forceinline__ RowPart merge(RowPart a, RowPart b) {
+    RowPart r;
+    r.m = fmaxf(a.m, b.m);
+    float ea = (a.m == -INFINITY) ? 0.f : expf(a.m - r.m);
+    float eb = (b.m == -INFINITY) ? 0.f : expf(b.m - r.m);
+    r.s = a.s * ea + b.s * eb;
+    r.pos = a.pos + b.pos;
+    r.msum = a.msum + b.msum;
+    return r;
+}
+
+// 32x32 tile C'[j][i] = sum_k F[rj][k] F[ri][k] for this lane's rows rj (A side) and ri (B side).
+// Lane half h supplies features k = 8s + 4h + t at MFMA step (s, t); both operands are streamed
+// from the (L2-resident) feature matrix as float4, 4 MFMAs per load pair.
+template <int D>
+__device__ __forceinline__ f32x16 tile_s(const float* __restrict__ F, int64_t rj, int64_t ri,
+                                         int64_t B, int h) {
+    f32x16 acc = {0.f};
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* pa = F + rj * D + 4 * h;
+    const float* pb = F + ri * D + 4 * h;
+    const bool va = rj < B, vb = ri < B;
+#pragma unroll 4
+    for (int s = 0; s < D / 8; ++s) {
+        float4 a = va ? ld4(pa + 8 * s) : z;
+        float4 b = vb ? ld4(pb + 8 * s) : z;
+        acc = mfma32(a.x, b.x, acc);
+        acc = mfma32(a.y, b.y, acc);
+        acc = mfma32(a.z, b.z, acc);
+        acc = mfma32(a.w, b.w, acc);
+    }
+    return acc;
+}
+
+__device__ __forceinline__ float pos_weight(const int64_t* __restrict__ labels,
+                                            const float* __restrict__ mask, int64_t B, int64_t i,
+                                            int64_t j, int64_t li) {
+    if (labels) return (labels[j] == li) ? 1.f : 0.f;
+    return mask[i * B + j];
+}
+
+// ---------------------------------------------------------------- forward: row partials
+template <int D>
+__global__ __launch_bounds__(256) void supcon_rows_partial(
+    const float* __restrict__ F, const int64_t* __restrict__ labels, const float* __restrict__ mask,
+    int64_t B, float inv_t, int jblk_per_split, RowPart* __restrict__ part) {
+    const int lane = lane_id(), wave = threadIdx.x >> 6, h = lane >> 5;
+    const int64_t i = (int64_t)blockIdx.x * TILE + (lane & 31);
+    const int64_t nj = (B + TILE - 1) / TILE;
+    const int64_t li = (labels && i < B) ? labels[i] : 0;
+
+    RowPart p = {-INFINITY, 0.f, 0.f, 0.f};
+    const int64_t jb0 = (int64_t)blockIdx.y * jblk_per_split;
+    const int64_t jb1 = min(nj, jb0 + jblk_per_split);
+    for (int64_t jb = jb0 + wave; jb < jb1; jb += WAVES) {
+        f32x16 acc = tile_s<D>(F, jb * TILE + (lane & 31), i, B, h);
+        if (i < B) {
+            float mb = -INFINITY;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                int64_t j = jb * TILE + acc_row(r, h);
+                if (j < B) mb = fmaxf(mb, acc[r] * inv_t);
+            }
+            float mn = fmaxf(p.m, mb);
+            float s = (p.m == -INFINITY) ? 0.f : p.s * expf(p.m - mn);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                int64_t j = jb * TILE + acc_row(r, h);
+                if (j < B && j != i) {
+                    float v = acc[r] * inv_t;
+                    s += expf(v - mn);
+                    float w = pos_weight(labels, mask, B, i, j, li);
+                    p.pos += w * v;
+                    p.msum += w;
+                }
+            }
+            p.m = mn;
+            p.s = s;
+        }
+    }
+    // merge the two row-halves of each column, then the 4 waves
+    RowPart o;
+    o.m = __shfl_xor(p.m, 32, 64);
+    o.s = __shfl_xor(p.s, 32, 64);
+    o.pos = __shfl_xor(p.pos, 32, 64);
+    o.msum = __shfl_xor(p.msum, 32, 64);
+    p = merge(p, o);
+    __shared__ RowPart red[WAVES][TILE];
+    if (h == 0) red[wave][lane] = p;
+    __syncthreads();
+    if (threadIdx.x < TILE) {
+        RowPart q = red[0][threadIdx.x];
+#pragma unroll
+        for (int w = 1; w < WAVES; ++w) q = merge(q, red[w][threadIdx.x]);
+        int64_t row = (int64_t)blockIdx.x * TILE + threadIdx.x;
+        if (row < B) part[(int64_t)blockIdx.y * B + row] = q;
+    }
+}
+
+// ---------------------------------------------------------------- forward: finalize
+// rowstats[i] = {m_i, den_i, msum_i, loss_i}; loss_out reduced per `reduction`.
+__global__ __launch_bounds__(256) void supcon_rows_finalize(const RowPart* __restrict__ part,
+                                                             int nsplit, int64_t B, float t_over_bt,
+                                                             int reduction, float4* __restrict__ rowstats,
+                                                             float* __restrict__ loss_out) {
+    __shared__ float red[256];
+    float acc = 0.f;
+    for (int64_t i = threadIdx.x; i < B; i += blockDim.x) {
+        RowPart q = part[i];
+        for (int sp = 1; sp < nsplit; ++sp) q = merge(q, part[(int64_t)sp * B + i]);
+        float den = q.s + 1e-6f;
+        float P = (q.msum == 0.f) ? 1.f : q.msum;
+        float mlpp = (q.pos - q.msum * q.m - q.msum * logf(den)) / P;
+        float li = -t_over_bt * mlpp;
+        rowstats[i] = make_float4(q.m, den, q.msum, li);
+        if (reduction == PCX_REDUCTION_NONE) loss_out[i] = li;
+        acc += li;
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && reduction != PCX_REDUCTION_NONE)
+        loss_out[0] = (reduction == PCX_REDUCTION_MEAN) ? red[0] / (float)B : red[0];
+}
+
+// ---------------------------------------------------------------- backward: row coefficients
+// G_ij = a_i M_ij - b_i exp(S_ij/T - m_i), a_i = -w_i/(base_T P_i), b_i = a_i msum_i / den_i
+__global__ void supcon_coef(const float4* __restrict__ rowstats, const float* __restrict__ grad_out,
+                            int64_t B, float inv_bt, int reduction, float4* __restrict__ coef) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B) return;
+    float4 st = rowstats[i];
+    float w = (reduction == PCX_REDUCTION_NONE) ? grad_out[i]
+              : (reduction == PCX_REDUCTION_MEAN ? grad_out[0] / (float)B : grad_out[0]);
+    float P = (st.z == 0.f) ? 1.f : st.z;
+    float a = -w * inv_bt / P;
+    coef[i] = make_float4(a, a * st.z / st.y, st.x, 0.f);
+}
+
+// ---------------------------------------------------------------- backward: dF partials
+template <int D>
+__global__ __launch_bounds__(256) void supcon_grad_partial(
+    const float* __restrict__ F, const int64_t* __restrict__ labels, const float* __restrict__ mask,
+    const float4* __restrict__ coef, int64_t B, float inv_t, int jblk_per_split,
+    float* __restrict__ part) {
+    constexpr int NQ = D / 32;  // 32-wide feature sub-tiles of dF
+    const int lane = lane_id(), wave = threadIdx.x >> 6, h = lane >> 5;
+    const int64_t i = (int64_t)blockIdx.x * TILE + (lane & 31);
+    const int64_t nj = (B + TILE - 1) / TILE;
+    const bool ivalid = i < B;
+    const int64_t li = (labels && ivalid) ? labels[i] : 0;
+    const float4 ci = ivalid ? coef[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+
+    f32x16 acc[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) acc[q] = f32x16{0.f};
+
+    const int64_t jb0 = (int64_t)blockIdx.y * jblk_per_split;
+    const int64_t jb1 = min(nj, jb0 + jblk_per_split);
+    for (int64_t jb = jb0 + wave; jb < jb1; jb += WAVES) {
+        f32x16 s = tile_s<D>(F, jb * TILE + (lane & 31), i, B, h);
+        float hv[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            int64_t j = jb * TILE + acc_row(r, h);
+            float v = 0.f;
+            if (ivalid && j < B && j != i) {
+                float4 cj = coef[j];
+                float zs = s[r] * inv_t;
+                float mij = pos_weight(labels, mask, B, i, j, li);
+                float mji = labels ? mij : mask[j * B + i];
+                v = ci.x * mij + cj.x * mji - ci.y * expf(zs - ci.z) - cj.y * expf(zs - cj.z);
+            }
+            hv[r] = v;
+        }
+        // dF_i += sum_j H_ij F_j : A = H (lane = anchor i, k = j of register r), B = F_j rows
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            int64_t j = jb * TILE + acc_row(r, h);
+            const float* fj = F + j * D + (lane & 31);
+            bool jv = j < B;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                float b = jv ? fj[32 * q] : 0.f;
+                acc[q] = mfma32(hv[r], b, acc[q]);
+            }
+        }
+    }
+    // reduce the 4 waves through LDS: out tile rows = anchors (acc_row), cols = features
+    __shared__ float red[TILE][D + 1];
+    for (int w = 0; w < WAVES; ++w) {
+        if (wave == w) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    float* dst = &red[acc_row(r, h)][32 * q + (lane & 31)];
+                    *dst = (w == 0) ? acc[q][r] : *dst + acc[q][r];
+                }
+        }
+        __syncthreads();
+    }
+    for (int e = threadIdx.x; e < TILE * D; e += blockDim.x) {
+        int rr = e / D, cc = e % D;
+        int64_t row = (int64_t)blockIdx.x * TILE + rr;
+        if (row < B) part[((int64_t)blockIdx.y * B + row) * D + cc] = red[rr][cc];
+    }
+}
+
+__global__ void sum_splits(const float* __restrict__ part, int nsplit, int64_t n,
+                           float* __restrict__ out) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    float a = part[e];
+    for (int s = 1; s < nsplit; ++s) a += part[(int64_t)s * n + e];
+    out[e] = a;
+}
+
+struct Geo {
+    int nib, nsplit, per;
+};
+
+Geo geometry(int64_t B) {
+    Geo g;
+    g.nib = ceil_div(B, TILE);
+    int64_t nj = g.nib;
+    int64_t want = nj / (WAVES * 4);  // aim for >= 4 j-blocks per wave
+    g.nsplit = (int)(want < 1 ? 1 : (want > 16 ? 16 : want));
+    g.per = ceil_div(nj, g.nsplit);
+    g.nsplit = ceil_div(nj, g.per);
+    return g;
+}
+
+int check_common(const float* F, const int64_t* labels, const float* mask, int64_t B, int64_t D,
+                 float temperature, float base_temperature, int reduction) {
+    PCX_CHECK_ARG(F != nullptr, "supcon: features is NULL");
+    PCX_CHECK_ARG((labels != nullptr) != (mask != nullptr), "supcon: give exactly one of labels/mask");
+    PCX_CHECK_ARG(B > 1, "Batch size must be greater than 1 for contrastive loss");
+    PCX_CHECK_ARG(D == 64 || D == 128 || D == 256, "supcon: embedding dim %lld unsupported (64/128/256)",
+                  (long long)D);
+    PCX_CHECK_ARG(temperature > 0.f && base_temperature > 0.f, "supcon: temperatures must be > 0");
+    PCX_CHECK_ARG(reduction >= 0 && reduction <= 2, "supcon: bad reduction %d", reduction);
+    PCX_CHECK_ARG(((uintptr_t)F & 15) == 0, "supcon: features must be 16-byte aligned");
+    return PCX_OK;
+}
+
+}  // namespace
+}  // namespace pcx
+
+using namespace pcx;
+
+extern "C" size_t pcx_supcon_workspace_bytes(int64_t B, int64_t D) {
+    if (B < 2) return 0;
+    Geo g = geometry(B);
+    size_t fwd = (size_t)g.nsplit * B * sizeof(RowPart);
+    size_t bwd = (size_t)g.nsplit * B * D * sizeof(float) + (size_t)B * sizeof(float4);
+    size_t n = fwd > bwd ? fwd : bwd;
+    return (n + 255) / 256 * 256;
+}
+
+extern "C" int pcx_supcon_forward(const float* F, const int64_t* labels, const float* mask, int64_t B,
+                                  int64_t D, float temperature, float base_temperature, int reduction,
+                                  float* loss_out, float* rowstats, void* ws, size_t ws_bytes,
+                                  hipStream_t stream) {
+    int rc = check_common(F, labels, mask, B, D, temperature, base_temperature, reduction);
+    if (rc) return rc;
+    PCX_CHECK_ARG(loss_out && rowstats, "supcon: NULL output");
+    if (ws_bytes < pcx_supcon_workspace_bytes(B, D)) {
+        set_error("supcon: workspace too small");
+        return PCX_EWORKSPACE;
+    }
+    Geo g = geometry(B);
+    RowPart* part = static_cast<RowPart*>(ws);
+    dim3 grid(g.nib, g.nsplit);
+    float inv_t = 1.0f / temperature;
+    if (D == 64)
+        supcon_rows_partial<64><<<grid, 256, 0, stream>>>(F, labels, mask, B, inv_t, g.per, part);
+    else if (D == 128)
+        supcon_rows_partial<128><<<grid, 256, 0, stream>>>(F, labels, mask, B, inv_t, g.per, part);
+    else
+        supcon_rows_partial<256><<<grid, 256, 0, stream>>>(F, labels, mask, B, inv_t, g.per, part);
+    PCX_LAUNCH_CHECK("supcon_rows_partial");
+    supcon_rows_finalize<<<1, 256, 0, stream>>>(part, g.nsplit, B, temperature / base_temperature,
+                                                 reduction, reinterpret_cast<float4*>(rowstats),
+                                                 loss_out);
+    PCX_LAUNCH_CHECK("supcon_rows_finalize");
+    return PCX_OK;
+}
+
+extern "C" int pcx_supcon_backward(const float* F, const int64_t* labels, const float* mask, int64_t B,
+                                   int64_t D, float temperature, float base_temperature, int reduction,
+                                   const float* grad_out, const float* rowstats, float* dF, void* ws,
+                                   size_t ws_bytes, hipStream_t stream) {
+    int rc = check_common(F, labels, mask, B, D, temperature, base_temperature, reduction);
+    if (rc) return rc;
+    PCX_CHECK_ARG(grad_out && rowstats && dF, "supcon: NULL argument");
+    if (ws_bytes < pcx_supcon_workspace_bytes(B, D)) {
+        set_error("supcon: workspace too small");
+        return PCX_EWORKSPACE;
+    }
+    Geo g = geometry(B);
+    float* part = static_cast<float*>(ws);
+    float4* coef = reinterpret_cast<float4*>(part + (size_t)g.nsplit * B * D);
+    supcon_coef<<<ceil_div(B, 256), 256, 0, stream>>>(reinterpret_cast<const float4*>(rowstats),
+                                                       grad_out, B, 1.0f / base_temperature,
+                                                       reduction, coef);
+    PCX_LAUNCH_CHECK("supcon_coef");
+    dim3 grid(g.nib, g.nsplit);
+    float inv_t = 1.0f / temperature;
+    if (D == 64)
+        supcon_grad_partial<64><<<grid, 256, 0, stream>>>(F, labels, mask, coef, B, inv_t, g.per, part);
+    else if (D == 128)
+        supcon_grad_partial<128><<<grid, 256, 0, stream>>>(F, labels, mask, coef, B, inv_t, g.per, part);
+    else
+        supcon_grad_partial<256><<<grid, 256, 0, stream>>>(F, labels, mask, coef, B, inv_t, g.per, part);
+    PCX_LAUNCH_CHECK("supcon_grad_partial");
+    int64_t n = B * D;
+    sum_splits<<<ceil_div(n, 256), 256, 0, stream>>>(part, g.nsplit, n, dF);
+    PCX_LAUNCH_CHECK("sum_splits");
+    return PCX_OK;
+}
