@@ -68,6 +68,48 @@ int pcx_adam_step(float* p, const float* g, float* m, float* v, int64_t n, int64
                   float lr, float beta1, float beta2, float eps, float weight_decay,
                   float grad_scale, hipStream_t stream);
 
+
+/* ------------------------------------------------------------------ whole-network plans
+ * A plan fixes the network configuration and the input shape [B, 1, F, T]; it owns no device
+ * memory.  Parameters are passed as an array of device pointers in the reference's
+ * model.named_parameters() order, gradients in the same order; bn_stats holds
+ * {running_mean, running_var} of every BatchNorm in state_dict order (2 pointers per BN) and
+ * bn_counts their num_batches_tracked (int64).  dropout[i] is a [B][C_i] keep-scale mask
+ * (0 or 1/(1-p)) per nn.Dropout2d in forward order, or NULL (no dropout).  The forward leaves
+ * the activations the backward needs inside `workspace`, so forward and backward of one step
+ * must share it. */
+#define PCX_NET_CNN_SMALL 0  /* "phoneme_cnn"      PhonemeNet     */
+#define PCX_NET_CNN_DEEP 1   /* "phoneme_cnn_deep" PhonemeNetDeep */
+
+typedef struct pcx_net_config {
+    int kind;
+    int in_channels;      /* must be 1 */
+    int embedding_dim;
+    int use_attention;
+    int hidden_dims[4];   /* deep only */
+    int use_residual;     /* deep only */
+} pcx_net_config;
+
+void* pcx_net_create(const pcx_net_config* cfg, int64_t B, int64_t F, int64_t T);
+void pcx_net_destroy(void* plan);
+size_t pcx_net_workspace_bytes(const void* plan);
+int pcx_net_info(const void* plan, int* nparams, int* nbn, int* ndrop, int* drop_channels);
+/* byte range of a named intermediate inside the workspace (introspection / tests) */
+int pcx_net_region(const void* plan, const char* name, size_t* offset, size_t* bytes);
+int pcx_net_forward(const void* plan, const float* const* params, float* const* bn_stats,
+                    int64_t* const* bn_counts, const float* x, const float* const* dropout,
+                    int train, float* emb, void* workspace, size_t workspace_bytes,
+                    hipStream_t stream);
+int pcx_net_backward(const void* plan, const float* const* params, const float* x,
+                     const float* const* dropout, const float* emb, const float* d_emb,
+                     float* const* grads, void* workspace, size_t workspace_bytes,
+                     hipStream_t stream);
+
+/* Dropout2d keep-scale masks: out[i] = (u_i >= p) ? 1/(1-p) : 0 with u_i a counter-based
+ * uniform draw from (seed, offset + i).  Not bit-compatible with torch's CPU generator. */
+int pcx_dropout_masks(float* out, int64_t n, float p, uint64_t seed, uint64_t offset,
+                      hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

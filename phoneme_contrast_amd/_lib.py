@@ -29,6 +29,19 @@ c_int = ctypes.c_int
 c_float = ctypes.c_float
 c_size = ctypes.c_size_t
 
+
+
+class NetConfig(ctypes.Structure):
+    """pcx_net_config (include/pcx.h)."""
+    _fields_ = [("kind", ctypes.c_int), ("in_channels", ctypes.c_int),
+                ("embedding_dim", ctypes.c_int), ("use_attention", ctypes.c_int),
+                ("hidden_dims", ctypes.c_int * 4), ("use_residual", ctypes.c_int)]
+
+
+_pp = ctypes.POINTER(ctypes.c_void_p)
+_pi = ctypes.POINTER(ctypes.c_int)
+_ps = ctypes.POINTER(ctypes.c_size_t)
+
 # name -> (restype, argtypes); mirrors include/pcx.h
 SIGNATURES = {
     "pcx_version": (c_int, []),
@@ -40,6 +53,17 @@ SIGNATURES = {
                                     c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_size, c_void_p]),
     "pcx_adam_step": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_i64, c_float,
                               c_float, c_float, c_float, c_float, c_float, c_void_p]),
+    "pcx_net_create": (c_void_p, [ctypes.POINTER(NetConfig), c_i64, c_i64, c_i64]),
+    "pcx_net_destroy": (None, [c_void_p]),
+    "pcx_net_workspace_bytes": (c_size, [c_void_p]),
+    "pcx_net_info": (c_int, [c_void_p, _pi, _pi, _pi, _pi]),
+    "pcx_net_region": (c_int, [c_void_p, ctypes.c_char_p, _ps, _ps]),
+    "pcx_net_forward": (c_int, [c_void_p, _pp, _pp, _pp, c_void_p, _pp, c_int, c_void_p, c_void_p,
+                                c_size, c_void_p]),
+    "pcx_net_backward": (c_int, [c_void_p, _pp, c_void_p, _pp, c_void_p, c_void_p, _pp, c_void_p,
+                                 c_size, c_void_p]),
+    "pcx_dropout_masks": (c_int, [c_void_p, c_i64, c_float, ctypes.c_uint64, ctypes.c_uint64,
+                                  c_void_p]),
 }
 
 

@@ -32,3 +32,30 @@ extern "C" int pcx_last_error(char* buf, size_t n) {
     }
     return (int)len;
 }
+
+namespace {
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__global__ void dropout_mask_kernel(float* out, int64_t n, float p, float keep, uint64_t seed, uint64_t off) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t r = splitmix64(seed ^ splitmix64(off + (uint64_t)i));
+    float u = (float)(r >> 40) * (1.0f / 16777216.0f);
+    out[i] = (u >= p) ? keep : 0.f;
+}
+}  // namespace
+
+extern "C" int pcx_dropout_masks(float* out, int64_t n, float p, uint64_t seed, uint64_t offset,
+                                 hipStream_t stream) {
+    using namespace pcx;
+    PCX_CHECK_ARG(out || n == 0, "dropout: NULL output");
+    PCX_CHECK_ARG(p >= 0.f && p < 1.f, "dropout probability has to be between 0 and 1, but got %f", p);
+    if (n == 0) return PCX_OK;
+    dropout_mask_kernel<<<ceil_div(n, 256), 256, 0, stream>>>(out, n, p, 1.f / (1.f - p), seed, offset);
+    PCX_LAUNCH_CHECK("dropout_mask_kernel");
+    return PCX_OK;
+}

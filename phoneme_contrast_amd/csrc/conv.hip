@@ -1,0 +1,720 @@
+// Convolution kernels of the phoneme CNN on CDNA4 (gfx950), fp32 throughout.
+//
+//  * conv3x3_kernel  — 3x3 / stride 1 / pad 1 conv as an implicit GEMM on v_mfma_f32_32x32x2_f32
+//                      (exact f32).  One kernel body serves the forward conv (reference
+//                      src/models/phoneme_cnn.py:39,47,50,58,61) and its data gradient (the same conv
+//                      on dy with flipped, transposed weights).  The BN/ReLU/MaxPool/Dropout2d that
+//                      sit between two convs (phoneme_cnn.py:37-43, 48-54, 59-64) are applied while
+//                      the input tile is staged into LDS (prologue); BN statistics, or the backward
+//                      of ReLU/MaxPool/Dropout plus the BN-backward sums, are fused into the
+//                      epilogue.  No activation tensor is materialised between a conv and its BN.
+//  * conv1_fwd_kernel — the Cin = 1 first conv (phoneme_cnn.py:36): direct, HBM-write-bound.
+//  * wgrad3x3_kernel / wgrad1_kernel — weight gradients, K = B*H*W split over slices.
+//
+// Tensor layout is the reference's planar NCHW.  MFMA orientation: A = weights (M = output
+// channels), B = input pixels (N = 32 consecutive flattened pixels per lane group), so each
+// accumulator register holds one channel for 32 consecutive pixels and the output stores are
+// 128-byte coalesced rows of a channel plane.
+#include "kernels.h"
+
+namespace pcx {
+namespace {
+
+constexpr int PADL = 4;  // left pad of an LDS row: data column 0 sits 16-byte aligned
+constexpr int CK = 8;    // input channels staged per K-chunk
+
+__device__ __forceinline__ int xcd_remap(int orig, int nb) {
+    // blocks b and b+8 share an XCD (observed round-robin dispatch): give each XCD a contiguous
+    // range of tiles so neighbouring tiles (which share halo rows) hit the same L2.  Bijective.
+    int q = nb >> 3, r = nb & 7, x = orig & 7;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (orig >> 3);
+}
+
+__device__ __forceinline__ float lanebcast(float v, int src) { return __shfl(v, src, 64); }
+
+__device__ __forceinline__ float sum32(float v) {  // reduce within each 32-lane half
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// ------------------------------------------------------------------ prologue (staging)
+template <int PRO>
+__device__ __forceinline__ float pro_elem(const ConvArgs& a, int c, int b, int hh, int w) {
+    if (PRO == PRO_RAW) {
+        return a.src[(((int64_t)b * a.cin + c) * a.H + hh) * a.W + w];
+    } else if (PRO == PRO_BNRELU) {
+        float4 cf = a.cf_in[c];
+        float v = a.src[(((int64_t)b * a.cin + c) * a.H + hh) * a.W + w];
+        return fmaxf(fmaf(v, cf.x, cf.y), 0.f);
+    } else if (PRO == PRO_BNRELU_POOL) {
+        float4 cf = a.cf_in[c];
+        const float* p = a.src + (((int64_t)b * a.cin + c) * a.srcH + 2 * hh) * a.srcW + 2 * w;
+        float m = fmaxf(fmaxf(fmaf(p[0], cf.x, cf.y), fmaf(p[1], cf.x, cf.y)),
+                        fmaxf(fmaf(p[a.srcW], cf.x, cf.y), fmaf(p[a.srcW + 1], cf.x, cf.y)));
+        m = fmaxf(m, 0.f);
+        return a.drop_in ? m * a.drop_in[(int64_t)b * a.cin + c] : m;
+    } else {  // PRO_BNBWD
+        float4 cf = a.cf_in[c];
+        int64_t o = (((int64_t)b * a.cin + c) * a.H + hh) * a.W + w;
+        return cf.x * (a.src[o] - cf.y - (a.src2[o] - cf.w) * cf.z);
+    }
+}
+
+template <int PRO>
+__device__ __forceinline__ float4 pro_quad(const ConvArgs& a, int c, int b, int hh, int w) {
+    // four consecutive conv-input columns w..w+3 (w % 4 == 0) of channel c, row hh of sample b
+    const bool full = (w + 3 < a.W) && ((a.W & 3) == 0) &&
+                      (PRO != PRO_BNRELU_POOL || (a.srcW & 3) == 0);
+    if (full) {
+        if (PRO == PRO_RAW || PRO == PRO_BNRELU) {
+            float4 v = ld4(a.src + (((int64_t)b * a.cin + c) * a.H + hh) * a.W + w);
+            if (PRO == PRO_BNRELU) {
+                float4 cf = a.cf_in[c];
+                v.x = fmaxf(fmaf(v.x, cf.x, cf.y), 0.f);
+                v.y = fmaxf(fmaf(v.y, cf.x, cf.y), 0.f);
+                v.z = fmaxf(fmaf(v.z, cf.x, cf.y), 0.f);
+                v.w = fmaxf(fmaf(v.w, cf.x, cf.y), 0.f);
+            }
+            return v;
+        } else if (PRO == PRO_BNRELU_POOL) {
+            float4 cf = a.cf_in[c];
+            const float* p = a.src + (((int64_t)b * a.cin + c) * a.srcH + 2 * hh) * a.srcW + 2 * w;
+            float4 t0 = ld4(p), t1 = ld4(p + 4), u0 = ld4(p + a.srcW), u1 = ld4(p + a.srcW + 4);
+            auto bn = [&](float v) { return fmaf(v, cf.x, cf.y); };
+            float4 r;
+            r.x = fmaxf(fmaxf(fmaxf(bn(t0.x), bn(t0.y)), fmaxf(bn(u0.x), bn(u0.y))), 0.f);
+            r.y = fmaxf(fmaxf(fmaxf(bn(t0.z), bn(t0.w)), fmaxf(bn(u0.z), bn(u0.w))), 0.f);
+            r.z = fmaxf(fmaxf(fmaxf(bn(t1.x), bn(t1.y)), fmaxf(bn(u1.x), bn(u1.y))), 0.f);
+            r.w = fmaxf(fmaxf(fmaxf(bn(t1.z), bn(t1.w)), fmaxf(bn(u1.z), bn(u1.w))), 0.f);
+            if (a.drop_in) {
+                float d = a.drop_in[(int64_t)b * a.cin + c];
+                r.x *= d; r.y *= d; r.z *= d; r.w *= d;
+            }
+            return r;
+        } else {
+            float4 cf = a.cf_in[c];
+            int64_t o = (((int64_t)b * a.cin + c) * a.H + hh) * a.W + w;
+            float4 dz = ld4(a.src + o), y = ld4(a.src2 + o);
+            float4 r;
+            r.x = cf.x * (dz.x - cf.y - (y.x - cf.w) * cf.z);
+            r.y = cf.x * (dz.y - cf.y - (y.y - cf.w) * cf.z);
+            r.z = cf.x * (dz.z - cf.y - (y.z - cf.w) * cf.z);
+            r.w = cf.x * (dz.w - cf.y - (y.w - cf.w) * cf.z);
+            return r;
+        }
+    }
+    float4 r;
+    r.x = (w + 0 < a.W) ? pro_elem<PRO>(a, c, b, hh, w + 0) : 0.f;
+    r.y = (w + 1 < a.W) ? pro_elem<PRO>(a, c, b, hh, w + 1) : 0.f;
+    r.z = (w + 2 < a.W) ? pro_elem<PRO>(a, c, b, hh, w + 2) : 0.f;
+    r.w = (w + 3 < a.W) ? pro_elem<PRO>(a, c, b, hh, w + 3) : 0.f;
+    return r;
+}
+
+// ------------------------------------------------------------------ 3x3 implicit GEMM
+template <int WM, int WN, int PRO, int EPI>
+__global__ __launch_bounds__(256) void conv3x3_kernel(ConvArgs a) {
+    constexpr int COUT_T = 32 * WM;
+    constexpr int BP = 4 * WN * 32;  // pixels per block
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int PLANE = a.NR * a.RS;
+    float* xs = smem;
+    float* wsm = smem + CK * PLANE;
+
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int ny = a.cout / COUT_T;
+    const int nb = gridDim.x;
+    const int flat = xcd_remap(blockIdx.x, nb);
+    const int tile = flat / ny;
+    const int n0 = (flat - tile * ny) * COUT_T;
+    const int64_t HW = (int64_t)a.H * a.W;
+    const int64_t Mtot = (int64_t)a.B * HW;
+    const int64_t m0 = (int64_t)tile * BP;
+    const int64_t row0 = m0 / a.W - 1;  // global row (b*H + h) of staged row 0
+    const int64_t nrows = (int64_t)a.B * a.H;
+
+    int pixoff[WN];
+    bool vup[WN], vdn[WN], valid[WN];
+    int pb[WN], pp[WN];
+#pragma unroll
+    for (int ni = 0; ni < WN; ++ni) {
+        int64_t m = m0 + (wave * WN + ni) * 32 + l32;
+        valid[ni] = m < Mtot;
+        int64_t mm = valid[ni] ? m : Mtot - 1;
+        int64_t gr = mm / a.W;
+        int w = (int)(mm - gr * a.W);
+        int b = (int)(gr / a.H);
+        int hr = (int)(gr - (int64_t)b * a.H);
+        pixoff[ni] = (int)(gr - row0) * a.RS + PADL + w;
+        vup[ni] = hr > 0;
+        vdn[ni] = hr < a.H - 1;
+        pb[ni] = b;
+        pp[ni] = hr * a.W + w;
+    }
+
+    f32x16 acc[WM][WN];
+#pragma unroll
+    for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < WN; ++ni) acc[mi][ni] = f32x16{0.f};
+
+    const int Q = a.RS >> 2;
+    for (int c0 = 0; c0 < a.cin; c0 += CK) {
+        __syncthreads();
+        // ---- stage CK input channels x NR rows (prologue applied), one row per wave
+        for (int row = wave; row < CK * a.NR; row += 4) {
+            int cl = row / a.NR;
+            int lr = row - cl * a.NR;
+            int64_t gr = row0 + lr;
+            bool rowok = gr >= 0 && gr < nrows;
+            int b = rowok ? (int)(gr / a.H) : 0;
+            int hh = rowok ? (int)(gr - (int64_t)b * a.H) : 0;
+            float* dst = xs + cl * PLANE + lr * a.RS;
+            for (int q = lane; q < Q; q += 64) {
+                int w = (q - 1) * 4;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (rowok && q >= 1 && w < a.W) v = pro_quad<PRO>(a, c0 + cl, b, hh, w);
+                st4(dst + 4 * q, v);
+            }
+        }
+        // ---- stage the weight chunk [9][CK][COUT_T]
+        constexpr int QW = COUT_T / 4;
+        for (int slot = tid; slot < 9 * CK * QW; slot += 256) {
+            int row = slot / QW, q = slot - row * QW;
+            int tap = row / CK, cc = row - tap * CK;
+            st4(wsm + row * COUT_T + 4 * q,
+                ld4(a.wpack + ((int64_t)(tap * a.cin + c0 + cc)) * a.cout + n0 + 4 * q));
+        }
+        __syncthreads();
+        // ---- 9 taps x CK/2 MFMA k-steps
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            const int dh = tap / 3 - 1, dw = tap % 3 - 1;
+            const int toff = dh * a.RS + dw;
+#pragma unroll
+            for (int s = 0; s < CK / 2; ++s) {
+                float av[WM], bv[WN];
+#pragma unroll
+                for (int mi = 0; mi < WM; ++mi)
+                    av[mi] = wsm[(tap * CK + 2 * s + h) * COUT_T + mi * 32 + l32];
+#pragma unroll
+                for (int ni = 0; ni < WN; ++ni) {
+                    float v = xs[(2 * s + h) * PLANE + pixoff[ni] + toff];
+                    if (dh < 0 && !vup[ni]) v = 0.f;
+                    if (dh > 0 && !vdn[ni]) v = 0.f;
+                    bv[ni] = v;
+                }
+#pragma unroll
+                for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+                    for (int ni = 0; ni < WN; ++ni) acc[mi][ni] = mfma32(av[mi], bv[ni], acc[mi][ni]);
+            }
+        }
+    }
+
+    // ------------------------------------------------------------------ epilogues
+    __syncthreads();  // LDS is reused for the cross-wave statistics below
+    float* red = smem;
+    const int cnt_w = (int)max((int64_t)0, min((int64_t)WN * 32, Mtot - (m0 + wave * WN * 32)));
+    if (EPI == EPI_FWD) {
+#pragma unroll
+        for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int chl = mi * 32 + acc_row(r, h);
+                const int ch = n0 + chl;
+                float K = lanebcast(acc[mi][0][r], h * 32);
+                float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+                for (int ni = 0; ni < WN; ++ni) {
+                    float v = acc[mi][ni][r];
+                    if (valid[ni]) {
+                        a.out[((int64_t)pb[ni] * a.cout + ch) * HW + pp[ni]] = v;
+                        float d = v - K;
+                        s1 += d;
+                        s2 = fmaf(d, d, s2);
+                    }
+                }
+                s1 = sum32(s1);
+                s2 = sum32(s2);
+                if (l32 == 0) {
+                    float n = (float)cnt_w;
+                    float mean = cnt_w ? K + s1 / n : 0.f;
+                    float m2 = cnt_w ? fmaxf(s2 - s1 * s1 / n, 0.f) : 0.f;
+                    float* d = red + (wave * COUT_T + chl) * 3;
+                    d[0] = n; d[1] = mean; d[2] = m2;
+                }
+            }
+        __syncthreads();
+        if (tid < COUT_T) {
+            float n = 0.f, mean = 0.f, m2 = 0.f;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const float* d = red + (w * COUT_T + tid) * 3;
+                if (d[0] > 0.f) {
+                    float nt = n + d[0];
+                    float delta = d[1] - mean;
+                    mean += delta * d[0] / nt;
+                    m2 += d[2] + delta * delta * n * d[0] / nt;
+                    n = nt;
+                }
+            }
+            a.part0[(int64_t)(n0 + tid) * a.nblk + tile] = n * mean;
+            a.part1[(int64_t)(n0 + tid) * a.nblk + tile] = m2;
+            if (tid == 0 && n0 == 0) a.partn[tile] = n;
+        }
+    } else {
+        // backward epilogues: sums of dz and dz*xhat per channel
+#pragma unroll
+        for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int chl = mi * 32 + acc_row(r, h);
+                const int ch = n0 + chl;
+                const float4 cf = a.cf_out[ch];
+                float sdz = 0.f, sdx = 0.f;
+#pragma unroll
+                for (int ni = 0; ni < WN; ++ni) {
+                    if (!valid[ni]) continue;
+                    const float g = acc[mi][ni][r];
+                    if (EPI == EPI_BWD_RELU) {
+                        int64_t o = ((int64_t)pb[ni] * a.cout + ch) * HW + pp[ni];
+                        float y = a.yprev[o];
+                        float dz = (fmaf(y, cf.x, cf.y) > 0.f) ? g : 0.f;
+                        a.out[o] = dz;
+                        sdz += dz;
+                        sdx = fmaf(dz, (y - cf.z) * cf.w, sdx);
+                    } else {  // EPI_BWD_POOL
+                        const int hp = pp[ni] / a.W, wp = pp[ni] - hp * a.W;
+                        float gd = a.drop_out ? g * a.drop_out[(int64_t)pb[ni] * a.cout + ch] : g;
+                        int64_t o = ((int64_t)pb[ni] * a.cout + ch) * a.Hs * a.Ws +
+                                    (int64_t)(2 * hp) * a.Ws + 2 * wp;
+                        float y0 = a.yprev[o], y1 = a.yprev[o + 1];
+                        float y2 = a.yprev[o + a.Ws], y3 = a.yprev[o + a.Ws + 1];
+                        float r0 = fmaxf(fmaf(y0, cf.x, cf.y), 0.f), r1 = fmaxf(fmaf(y1, cf.x, cf.y), 0.f);
+                        float r2 = fmaxf(fmaf(y2, cf.x, cf.y), 0.f), r3 = fmaxf(fmaf(y3, cf.x, cf.y), 0.f);
+                        // first maximum in window scan order, as torch's max_pool2d
+                        int arg = 0;
+                        float best = r0, ya = y0;
+                        if (r1 > best) { best = r1; arg = 1; ya = y1; }
+                        if (r2 > best) { best = r2; arg = 2; ya = y2; }
+                        if (r3 > best) { best = r3; arg = 3; ya = y3; }
+                        float d = best > 0.f ? gd : 0.f;
+                        a.out[o] = arg == 0 ? d : 0.f;
+                        a.out[o + 1] = arg == 1 ? d : 0.f;
+                        a.out[o + a.Ws] = arg == 2 ? d : 0.f;
+                        a.out[o + a.Ws + 1] = arg == 3 ? d : 0.f;
+                        sdz += d;
+                        sdx = fmaf(d, (ya - cf.z) * cf.w, sdx);
+                    }
+                }
+                sdz = sum32(sdz);
+                sdx = sum32(sdx);
+                if (l32 == 0) {
+                    float* d = red + (wave * COUT_T + chl) * 2;
+                    d[0] = sdz; d[1] = sdx;
+                }
+            }
+        __syncthreads();
+        if (tid < COUT_T) {
+            float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                s0 += red[(w * COUT_T + tid) * 2];
+                s1 += red[(w * COUT_T + tid) * 2 + 1];
+            }
+            a.part0[(int64_t)(n0 + tid) * a.nblk + tile] = s0;
+            a.part1[(int64_t)(n0 + tid) * a.nblk + tile] = s1;
+        }
+    }
+}
+
+template <int WM, int WN>
+int launch_tiles(int pro, int epi, const ConvArgs& a, dim3 grid, size_t smem, hipStream_t s) {
+#define PCX_CONV_CASE(P, E)                                                                      \
+    if (pro == P && epi == E) {                                                                 \
+        (void)hipFuncSetAttribute((const void*)conv3x3_kernel<WM, WN, P, E>,                          \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);            \
+        conv3x3_kernel<WM, WN, P, E><<<grid, 256, smem, s>>>(a);                                \
+        PCX_LAUNCH_CHECK("conv3x3_kernel");                                                     \
+        return PCX_OK;                                                                          \
+    }
+    PCX_CONV_CASE(PRO_RAW, EPI_FWD)
+    PCX_CONV_CASE(PRO_BNRELU, EPI_FWD)
+    PCX_CONV_CASE(PRO_BNRELU_POOL, EPI_FWD)
+    PCX_CONV_CASE(PRO_BNBWD, EPI_BWD_RELU)
+    PCX_CONV_CASE(PRO_BNBWD, EPI_BWD_POOL)
+#undef PCX_CONV_CASE
+    set_error("conv3x3: unsupported prologue/epilogue pair (%d, %d)", pro, epi);
+    return PCX_EINVAL;
+}
+
+void tile_shape(int cout, int* wm, int* wn) {
+    if (cout == 32) { *wm = 1; *wn = 4; }
+    else { *wm = 2; *wn = 2; }
+}
+
+// ------------------------------------------------------------------ Cin = 1 first conv
+constexpr int C1_CPW = 8;  // output channels per wave
+
+__global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Args a) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t HW = (int64_t)a.H * a.W;
+    const int64_t nrows = (int64_t)a.B * a.H;
+    const int64_t r0 = (int64_t)blockIdx.x * a.rows_per_blk;
+    const int64_t r1 = min(nrows, r0 + a.rows_per_blk);
+    for (int cg = wave * C1_CPW; cg < a.cout; cg += 4 * C1_CPW) {
+        float wt[C1_CPW][9];
+#pragma unroll
+        for (int j = 0; j < C1_CPW; ++j)
+#pragma unroll
+            for (int t = 0; t < 9; ++t) wt[j][t] = a.w[(cg + j) * 9 + t];
+        // shift for the one-pass variance: the output at the block's first pixel
+        float K[C1_CPW];
+        {
+            int b = (int)(r0 / a.H), hh = (int)(r0 - (int64_t)b * a.H);
+            float x9[9];
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                int y = hh + t / 3 - 1, x = t % 3 - 1;
+                x9[t] = (y >= 0 && y < a.H && x >= 0) ? a.x[(int64_t)b * HW + (int64_t)y * a.W + x] : 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < C1_CPW; ++j) {
+                float v = 0.f;
+#pragma unroll
+                for (int t = 0; t < 9; ++t) v = fmaf(wt[j][t], x9[t], v);
+                K[j] = v;
+            }
+        }
+        float s1[C1_CPW], s2[C1_CPW];
+#pragma unroll
+        for (int j = 0; j < C1_CPW; ++j) s1[j] = s2[j] = 0.f;
+        for (int64_t gr = r0; gr < r1; ++gr) {
+            const int b = (int)(gr / a.H), hh = (int)(gr - (int64_t)b * a.H);
+            const float* xb = a.x + (int64_t)b * HW;
+            for (int w = lane; w < a.W; w += 64) {
+                float x9[9];
+#pragma unroll
+                for (int t = 0; t < 9; ++t) {
+                    int y = hh + t / 3 - 1, x = w + t % 3 - 1;
+                    x9[t] = (y >= 0 && y < a.H && x >= 0 && x < a.W) ? xb[(int64_t)y * a.W + x] : 0.f;
+                }
+#pragma unroll
+                for (int j = 0; j < C1_CPW; ++j) {
+                    float v = 0.f;
+#pragma unroll
+                    for (int t = 0; t < 9; ++t) v = fmaf(wt[j][t], x9[t], v);
+                    a.out[((int64_t)b * a.cout + cg + j) * HW + (int64_t)hh * a.W + w] = v;
+                    float d = v - K[j];
+                    s1[j] += d;
+                    s2[j] = fmaf(d, d, s2[j]);
+                }
+            }
+        }
+        const float n = (float)((r1 - r0) * a.W);
+#pragma unroll
+        for (int j = 0; j < C1_CPW; ++j) {
+            float t1 = wave_sum(s1[j]), t2 = wave_sum(s2[j]);
+            if (lane == 0) {
+                a.part0[(int64_t)(cg + j) * a.nblk + blockIdx.x] = n * K[j] + t1;
+                a.part1[(int64_t)(cg + j) * a.nblk + blockIdx.x] = fmaxf(t2 - t1 * t1 / n, 0.f);
+            }
+        }
+        if (lane == 0 && cg == 0) a.partn[blockIdx.x] = n;
+    }
+}
+
+// ------------------------------------------------------------------ weight gradient 3x3
+template <int PRO>
+__device__ __forceinline__ float wg_pro(const WgradArgs& a, int c, int b, int hh, int w) {
+    if (PRO == PRO_RAW) {
+        return a.src[(((int64_t)b * a.cin + c) * a.H + hh) * a.W + w];
+    } else if (PRO == PRO_BNRELU) {
+        float4 cf = a.cf_x[c];
+        return fmaxf(fmaf(a.src[(((int64_t)b * a.cin + c) * a.H + hh) * a.W + w], cf.x, cf.y), 0.f);
+    } else {  // PRO_BNRELU_POOL
+        float4 cf = a.cf_x[c];
+        const float* p = a.src + (((int64_t)b * a.cin + c) * a.srcH + 2 * hh) * a.srcW + 2 * w;
+        float m = fmaxf(fmaxf(fmaf(p[0], cf.x, cf.y), fmaf(p[1], cf.x, cf.y)),
+                        fmaxf(fmaf(p[a.srcW], cf.x, cf.y), fmaf(p[a.srcW + 1], cf.x, cf.y)));
+        m = fmaxf(m, 0.f);
+        return a.drop ? m * a.drop[(int64_t)b * a.cin + c] : m;
+    }
+}
+
+template <int PRO>
+__global__ __launch_bounds__(256) void wgrad3x3_kernel(WgradArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int P = a.R * a.CW;           // dy positions per chunk
+    const int PS = P + 1;               // odd strides: conflict-free column reads
+    const int XS = a.CW + 2;
+    const int XP = (a.R + 2) * XS + 1;
+    float* dyt = smem;                  // [32][PS]
+    float* xt = smem + 32 * PS;         // [32][XP]
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int ncg = a.cin / 32;
+    const int mi = blockIdx.y / ncg, ci = blockIdx.y - mi * ncg;
+    const int n0 = mi * 32, c0 = ci * 32;
+
+    f32x16 acc[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[t] = f32x16{0.f};
+
+    const int ch0 = blockIdx.x * a.per_slice;
+    const int ch1 = min(a.nchunks, ch0 + a.per_slice);
+    for (int chunk = ch0; chunk < ch1; ++chunk) {
+        const int seg = chunk % a.nseg;
+        const int rb = (chunk / a.nseg) % a.nrb;
+        const int b = chunk / (a.nseg * a.nrb);
+        const int h0 = rb * a.R, w0 = seg * a.CW;
+        __syncthreads();
+        // dy rows: BN backward applied to (dz, y)
+        for (int row = wave; row < 32 * a.R; row += 4) {
+            int n = row / a.R, r = row - n * a.R;
+            int hh = h0 + r;
+            float4 cf = a.cf_dy[n0 + n];
+            int64_t base = (((int64_t)b * a.cout + n0 + n) * a.H + hh) * a.W;
+            float* dst = dyt + n * PS + r * a.CW;
+            for (int e = lane; e < a.CW; e += 64) {
+                int w = w0 + e;
+                float v = 0.f;
+                if (hh < a.H && w < a.W) {
+                    float dz = a.dz[base + w], y = a.y[base + w];
+                    v = cf.x * (dz - cf.y - (y - cf.w) * cf.z);
+                }
+                dst[e] = v;
+            }
+        }
+        // x rows h0-1 .. h0+R (zero outside the sample), columns w0-1 .. w0+CW
+        for (int row = wave; row < 32 * (a.R + 2); row += 4) {
+            int c = row / (a.R + 2), rr = row - c * (a.R + 2);
+            int hh = h0 - 1 + rr;
+            bool rowok = hh >= 0 && hh < a.H;
+            float* dst = xt + c * XP + rr * XS;
+            for (int e = lane; e < XS; e += 64) {
+                int w = w0 - 1 + e;
+                dst[e] = (rowok && w >= 0 && w < a.W) ? wg_pro<PRO>(a, c0 + c, b, hh, w) : 0.f;
+            }
+        }
+        __syncthreads();
+        for (int s = wave; s < P / 2; s += 4) {
+            const int p0 = 2 * s;
+            const int r = p0 / a.CW;
+            const int w = p0 - r * a.CW;
+            const float av = dyt[l32 * PS + p0 + h];
+            const float* xb = xt + l32 * XP + r * XS + w + h;
+#pragma unroll
+            for (int t = 0; t < 9; ++t) acc[t] = mfma32(av, xb[(t / 3) * XS + (t % 3)], acc[t]);
+        }
+    }
+    // reduce the 4 waves' K-split accumulators through LDS (deterministic order)
+    __syncthreads();
+    float* red = smem;  // [9][32][32]
+    for (int w = 0; w < 4; ++w) {
+        if (wave == w) {
+#pragma unroll
+            for (int t = 0; t < 9; ++t)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    float* d = red + (t * 32 + acc_row(r, h)) * 32 + l32;
+                    *d = (w == 0) ? acc[t][r] : *d + acc[t][r];
+                }
+        }
+        __syncthreads();
+    }
+    float* out = a.part + (int64_t)blockIdx.x * a.cout * a.cin * 9;
+    for (int e = tid; e < 32 * 32 * 9; e += 256) {
+        int i = e / 288, rem = e - i * 288, j = rem / 9, t = rem - j * 9;
+        out[((int64_t)(n0 + i) * a.cin + c0 + j) * 9 + t] = red[(t * 32 + i) * 32 + j];
+    }
+}
+
+// ------------------------------------------------------------------ weight gradient, Cin = 1
+__global__ __launch_bounds__(256) void wgrad1_kernel(Wgrad1Args a) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t HW = (int64_t)a.H * a.W;
+    const int64_t nrows = (int64_t)a.B * a.H;
+    const int64_t r0 = (int64_t)blockIdx.x * a.rows_per_slice;
+    const int64_t r1 = min(nrows, r0 + a.rows_per_slice);
+    for (int cg = wave * C1_CPW; cg < a.cout; cg += 4 * C1_CPW) {
+        float acc[C1_CPW][9];
+        float4 cf[C1_CPW];
+#pragma unroll
+        for (int j = 0; j < C1_CPW; ++j) {
+            cf[j] = a.cf_dy[cg + j];
+#pragma unroll
+            for (int t = 0; t < 9; ++t) acc[j][t] = 0.f;
+        }
+        for (int64_t gr = r0; gr < r1; ++gr) {
+            const int b = (int)(gr / a.H), hh = (int)(gr - (int64_t)b * a.H);
+            const float* xb = a.x + (int64_t)b * HW;
+            for (int w = lane; w < a.W; w += 64) {
+                float x9[9];
+#pragma unroll
+                for (int t = 0; t < 9; ++t) {
+                    int y = hh + t / 3 - 1, x = w + t % 3 - 1;
+                    x9[t] = (y >= 0 && y < a.H && x >= 0 && x < a.W) ? xb[(int64_t)y * a.W + x] : 0.f;
+                }
+#pragma unroll
+                for (int j = 0; j < C1_CPW; ++j) {
+                    int64_t o = ((int64_t)b * a.cout + cg + j) * HW + (int64_t)hh * a.W + w;
+                    float dy = cf[j].x * (a.dz[o] - cf[j].y - (a.y[o] - cf[j].w) * cf[j].z);
+#pragma unroll
+                    for (int t = 0; t < 9; ++t) acc[j][t] = fmaf(dy, x9[t], acc[j][t]);
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < C1_CPW; ++j)
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                float v = wave_sum(acc[j][t]);
+                if (lane == 0) a.part[((int64_t)blockIdx.x * a.cout + cg + j) * 9 + t] = v;
+            }
+    }
+}
+
+__global__ void sum_slices_kernel(const float* __restrict__ part, int nslice, int64_t n,
+                                  float* __restrict__ out) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    float s = 0.f;
+    for (int k = 0; k < nslice; ++k) s += part[(int64_t)k * n + e];
+    out[e] = s;
+}
+
+__global__ void pack_fwd_kernel(const float* __restrict__ w, float* __restrict__ wp, int cout, int cin) {
+    int e = blockIdx.x * blockDim.x + threadIdx.x;  // e over [cout][cin][9]
+    if (e >= cout * cin * 9) return;
+    int n = e / (cin * 9), rem = e - n * cin * 9, c = rem / 9, t = rem - c * 9;
+    wp[((int64_t)t * cin + c) * cout + n] = w[e];
+}
+
+__global__ void pack_dgrad_kernel(const float* __restrict__ w, float* __restrict__ wp, int cout, int cin) {
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= cout * cin * 9) return;
+    int n = e / (cin * 9), rem = e - n * cin * 9, c = rem / 9, t = rem - c * 9;
+    // dgrad GEMM: input channels = n (dy), output channels = c (dx), tap flipped
+    wp[((int64_t)(8 - t) * cout + n) * cin + c] = w[e];
+}
+
+}  // namespace
+
+// ====================================================================== host launchers
+size_t conv3x3_nblk(int B, int H, int W, int cout) {
+    int wm, wn;
+    tile_shape(cout, &wm, &wn);
+    int64_t M = (int64_t)B * H * W;
+    return (size_t)ceil_div(M, 4 * wn * 32);
+}
+
+int launch_conv3x3(int pro, int epi, ConvArgs a, hipStream_t s) {
+    PCX_CHECK_ARG(a.cin % CK == 0, "conv3x3: cin %d must be a multiple of %d", a.cin, CK);
+    PCX_CHECK_ARG(a.cout == 32 || a.cout % 64 == 0, "conv3x3: cout %d unsupported", a.cout);
+    PCX_CHECK_ARG(a.B > 0 && a.H > 0 && a.W > 0, "conv3x3: empty tensor");
+    int wm, wn;
+    tile_shape(a.cout, &wm, &wn);
+    const int bp = 4 * wn * 32, cout_t = 32 * wm;
+    const int64_t M = (int64_t)a.B * a.H * a.W;
+    const int ntile = ceil_div(M, bp);
+    PCX_CHECK_ARG(a.nblk == ntile, "conv3x3: partial buffer sized for %d tiles, need %d", a.nblk, ntile);
+    a.NR = (bp - 1 + a.W - 1) / a.W + 1 + 2;
+    a.RS = PADL + ((a.W + 1 + 3) / 4) * 4;
+    size_t smem = ((size_t)CK * a.NR * a.RS + 9 * CK * cout_t) * sizeof(float);
+    size_t red = (size_t)4 * cout_t * 3 * sizeof(float);
+    if (smem < red) smem = red;
+    PCX_CHECK_ARG(smem <= 160 * 1024, "conv3x3: W=%d needs %zu B of LDS", a.W, smem);
+    dim3 grid((unsigned)(ntile * (a.cout / cout_t)));
+    if (wm == 1 && wn == 4) return launch_tiles<1, 4>(pro, epi, a, grid, smem, s);
+    return launch_tiles<2, 2>(pro, epi, a, grid, smem, s);
+}
+
+int conv1_nblk(int B, int H, int* rows_per_blk) {
+    int64_t nrows = (int64_t)B * H;
+    int rpb = (int)std::max<int64_t>(1, nrows / 2048);
+    *rows_per_blk = rpb;
+    return ceil_div(nrows, rpb);
+}
+
+int launch_conv1_fwd(Conv1Args a, hipStream_t s) {
+    PCX_CHECK_ARG(a.cout % (4 * C1_CPW) == 0, "conv1: cout %d must be a multiple of 32", a.cout);
+    conv1_fwd_kernel<<<a.nblk, 256, 0, s>>>(a);
+    PCX_LAUNCH_CHECK("conv1_fwd_kernel");
+    return PCX_OK;
+}
+
+void wgrad3x3_geometry(int B, int H, int W, int cin, int cout, WgradArgs* a) {
+    int cw = W < 100 ? W : 100;
+    cw += cw & 1;
+    int R = std::max(1, 200 / cw);
+    R = std::min(R, H);
+    a->CW = cw;
+    a->R = R;
+    a->nseg = ceil_div(W, cw);
+    a->nrb = ceil_div(H, R);
+    a->nchunks = B * a->nrb * a->nseg;
+    int ngroups = (cout / 32) * (cin / 32);
+    int want = std::max(1, 2048 / ngroups);
+    want = std::min(want, a->nchunks);
+    a->per_slice = ceil_div(a->nchunks, want);
+    a->nslice = ceil_div(a->nchunks, a->per_slice);
+}
+
+int launch_wgrad3x3(int pro, WgradArgs a, hipStream_t s) {
+    PCX_CHECK_ARG(a.cin % 32 == 0 && a.cout % 32 == 0, "wgrad3x3: channels must be multiples of 32");
+    const int P = a.R * a.CW;
+    size_t smem = ((size_t)32 * (P + 1) + (size_t)32 * ((a.R + 2) * (a.CW + 2) + 1)) * sizeof(float);
+    size_t red = (size_t)9 * 32 * 32 * sizeof(float);
+    if (smem < red) smem = red;
+    PCX_CHECK_ARG(smem <= 160 * 1024, "wgrad3x3: LDS %zu too large", smem);
+    dim3 grid(a.nslice, (a.cout / 32) * (a.cin / 32));
+#define PCX_WG_CASE(P_)                                                                          \
+    if (pro == P_) {                                                                            \
+        (void)hipFuncSetAttribute((const void*)wgrad3x3_kernel<P_>,                                   \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);            \
+        wgrad3x3_kernel<P_><<<grid, 256, smem, s>>>(a);                                         \
+        PCX_LAUNCH_CHECK("wgrad3x3_kernel");                                                    \
+        return PCX_OK;                                                                          \
+    }
+    PCX_WG_CASE(PRO_RAW)
+    PCX_WG_CASE(PRO_BNRELU)
+    PCX_WG_CASE(PRO_BNRELU_POOL)
+#undef PCX_WG_CASE
+    set_error("wgrad3x3: unsupported prologue %d", pro);
+    return PCX_EINVAL;
+}
+
+int launch_wgrad1(Wgrad1Args a, hipStream_t s) {
+    PCX_CHECK_ARG(a.cout % (4 * C1_CPW) == 0, "wgrad1: cout must be a multiple of 32");
+    wgrad1_kernel<<<a.nslice, 256, 0, s>>>(a);
+    PCX_LAUNCH_CHECK("wgrad1_kernel");
+    return PCX_OK;
+}
+
+int launch_sum_slices(const float* part, int nslice, int64_t n, float* out, hipStream_t s) {
+    sum_slices_kernel<<<ceil_div(n, 256), 256, 0, s>>>(part, nslice, n, out);
+    PCX_LAUNCH_CHECK("sum_slices_kernel");
+    return PCX_OK;
+}
+
+int launch_pack_fwd(const float* w, float* wp, int cout, int cin, hipStream_t s) {
+    int n = cout * cin * 9;
+    pack_fwd_kernel<<<ceil_div(n, 256), 256, 0, s>>>(w, wp, cout, cin);
+    PCX_LAUNCH_CHECK("pack_fwd_kernel");
+    return PCX_OK;
+}
+
+int launch_pack_dgrad(const float* w, float* wp, int cout, int cin, hipStream_t s) {
+    int n = cout * cin * 9;
+    pack_dgrad_kernel<<<ceil_div(n, 256), 256, 0, s>>>(w, wp, cout, cin);
+    PCX_LAUNCH_CHECK("pack_dgrad_kernel");
+    return PCX_OK;
+}
+
+}  // namespace pcx

@@ -1,0 +1,385 @@
+// Embedding head of PhonemeNet / PhonemeNetDeep (reference src/models/phoneme_cnn.py):
+//   x = Dropout2d(ReLU(BN(y)))                       (fused: never materialised)
+//   a = sigmoid(conv1x1(x)), x' = x * a              SpatialAttention, :129-143
+//   pooled = mean_{h,w} x'                           AdaptiveAvgPool2d(1), :74,116-117
+//   e = normalize(BN1d(Linear(pooled)))             :75-77,119-124
+// and the backward of all of it.  These are small (per-sample) kernels; the trunk convs dominate.
+#include "kernels.h"
+
+namespace pcx {
+namespace {
+
+__device__ __forceinline__ float xval(float y, float4 cf, float d) { return d * fmaxf(fmaf(y, cf.x, cf.y), 0.f); }
+
+// one block per sample
+__global__ __launch_bounds__(256) void head_pool_fwd_kernel(HeadPoolArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* att = sm;                // [P]
+    float* swa = sm + a.P;          // [C]
+    float* sdr = swa + a.C;         // [C]
+    float4* scf = reinterpret_cast<float4*>(sdr + a.C + ((4 - ((a.P + 2 * a.C) & 3)) & 3));
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const float* yb = a.y + (int64_t)b * a.C * a.P;
+    for (int c = tid; c < a.C; c += blockDim.x) {
+        scf[c] = a.cf[c];
+        sdr[c] = a.drop ? a.drop[(int64_t)b * a.C + c] : 1.f;
+        swa[c] = a.wa ? a.wa[c] : 0.f;
+    }
+    __syncthreads();
+    const float ba = a.wa ? a.ba[0] : 0.f;
+    for (int p = tid; p < a.P; p += blockDim.x) {
+        float v = 1.f;
+        if (a.wa) {
+            float l = ba;
+            for (int c = 0; c < a.C; ++c) l = fmaf(swa[c], xval(yb[(int64_t)c * a.P + p], scf[c], sdr[c]), l);
+            v = 1.f / (1.f + expf(-l));
+            a.att[(int64_t)b * a.P + p] = v;
+        }
+        att[p] = v;
+    }
+    __syncthreads();
+    const float invp = 1.f / (float)a.P;
+    for (int c = wave; c < a.C; c += blockDim.x / 64) {
+        const float* yc = yb + (int64_t)c * a.P;
+        float4 cf = scf[c];
+        float d = sdr[c];
+        float s = 0.f;
+        for (int p = lane; p < a.P; p += 64) s = fmaf(xval(yc[p], cf, d), att[p], s);
+        s = wave_sum(s);
+        if (lane == 0) a.pooled[(int64_t)b * a.C + c] = s * invp;
+    }
+}
+
+__global__ __launch_bounds__(256) void head_pool_bwd_kernel(HeadPoolArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* att = sm;                // [P]
+    float* dl = sm + a.P;           // [P]
+    float* swa = dl + a.P;          // [C]
+    float* sdr = swa + a.C;         // [C]
+    float* sdp = sdr + a.C;         // [C]
+    float4* scf = reinterpret_cast<float4*>(sdp + a.C + ((4 - ((2 * a.P + 3 * a.C) & 3)) & 3));
+    __shared__ float red[4];
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const float* yb = a.y + (int64_t)b * a.C * a.P;
+    const float invp = 1.f / (float)a.P;
+    for (int c = tid; c < a.C; c += blockDim.x) {
+        scf[c] = a.cf[c];
+        sdr[c] = a.drop ? a.drop[(int64_t)b * a.C + c] : 1.f;
+        swa[c] = a.wa ? a.wa[c] : 0.f;
+        sdp[c] = a.dpooled[(int64_t)b * a.C + c] * invp;
+    }
+    __syncthreads();
+    float dls = 0.f;
+    for (int p = tid; p < a.P; p += blockDim.x) {
+        float at = 1.f, d = 0.f;
+        if (a.wa) {
+            at = a.att[(int64_t)b * a.P + p];
+            float s = 0.f;
+            for (int c = 0; c < a.C; ++c) s = fmaf(sdp[c], xval(yb[(int64_t)c * a.P + p], scf[c], sdr[c]), s);
+            d = s * at * (1.f - at);
+        }
+        att[p] = at;
+        dl[p] = d;
+        dls += d;
+    }
+    dls = wave_sum(dls);
+    if (lane == 0) red[wave] = dls;
+    __syncthreads();
+    if (tid == 0 && a.wa) a.p_dba[b] = red[0] + red[1] + red[2] + red[3];
+    for (int c = wave; c < a.C; c += blockDim.x / 64) {
+        const float* yc = yb + (int64_t)c * a.P;
+        float* dzc = a.dz + ((int64_t)b * a.C + c) * a.P;
+        const float4 cf = scf[c];
+        const float dr = sdr[c], g = sdp[c], wac = swa[c];
+        float sdz = 0.f, sdx = 0.f, sdw = 0.f;
+        for (int p = lane; p < a.P; p += 64) {
+            float y = yc[p];
+            float z = fmaf(y, cf.x, cf.y);
+            float dx = fmaf(g, att[p], dl[p] * wac);
+            float dz = z > 0.f ? dx * dr : 0.f;
+            dzc[p] = dz;
+            sdz += dz;
+            sdx = fmaf(dz, (y - cf.z) * cf.w, sdx);
+            sdw = fmaf(dl[p], dr * fmaxf(z, 0.f), sdw);
+        }
+        sdz = wave_sum(sdz);
+        sdx = wave_sum(sdx);
+        sdw = wave_sum(sdw);
+        if (lane == 0) {
+            a.p_dz[(int64_t)c * a.B + b] = sdz;
+            a.p_dzx[(int64_t)c * a.B + b] = sdx;
+            if (a.wa) a.p_dwa[(int64_t)c * a.B + b] = sdw;
+        }
+    }
+}
+
+// --------------------------------------------------------------- projection
+constexpr int PR = 16;  // rows per block
+
+// h = pooled @ W^T + bias ; one thread per output feature, 16 rows per block
+__global__ __launch_bounds__(256) void proj_fwd_kernel(ProjArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float sp[];  // [PR][K]
+    const int b0 = blockIdx.x * PR, tid = threadIdx.x;
+    const int nr = min(PR, a.B - b0);
+    for (int e = tid; e < nr * a.K; e += blockDim.x) sp[e] = a.pooled[(int64_t)b0 * a.K + e];
+    __syncthreads();
+    for (int d = tid; d < a.D; d += blockDim.x) {
+        float acc[PR];
+        const float bi = a.bias[d];
+#pragma unroll
+        for (int r = 0; r < PR; ++r) acc[r] = bi;
+        for (int k = 0; k < a.K; ++k) {
+            const float w = a.wt[(int64_t)k * a.D + d];
+#pragma unroll
+            for (int r = 0; r < PR; ++r) acc[r] = fmaf(sp[r * a.K + k], w, acc[r]);
+        }
+        for (int r = 0; r < nr; ++r) a.h[(int64_t)(b0 + r) * a.D + d] = acc[r];
+    }
+}
+
+__device__ __forceinline__ double bsum(double v, double* red) {
+    const int tid = threadIdx.x;
+    red[tid] = v;
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+        if (tid < o) red[tid] += red[tid + o];
+        __syncthreads();
+    }
+    double r = red[0];
+    __syncthreads();
+    return r;
+}
+
+// BatchNorm1d statistics over the batch, one block per feature (exact two-pass, float64)
+__global__ __launch_bounds__(256) void bn1d_fwd_kernel(ProjArgs a) {
+    __shared__ double red[256];
+    const int d = blockIdx.x;
+    const float g = a.gamma[d], be = a.beta[d];
+    if (!a.train) {
+        if (threadIdx.x == 0) {
+            float invstd = 1.f / sqrtf(a.rvar[d] + a.eps);
+            a.cf[d] = make_float4(g * invstd, be - a.rmean[d] * g * invstd, a.rmean[d], invstd);
+        }
+        return;
+    }
+    double s = 0.0;
+    for (int b = threadIdx.x; b < a.B; b += blockDim.x) s += (double)a.h[(int64_t)b * a.D + d];
+    const double mean = bsum(s, red) / a.B;
+    double q = 0.0;
+    for (int b = threadIdx.x; b < a.B; b += blockDim.x) {
+        double t = (double)a.h[(int64_t)b * a.D + d] - mean;
+        q += t * t;
+    }
+    q = bsum(q, red);
+    if (threadIdx.x == 0) {
+        double var = q / a.B;
+        double invstd = 1.0 / sqrt(var + (double)a.eps);
+        a.cf[d] = make_float4((float)(g * invstd), (float)(be - mean * g * invstd), (float)mean, (float)invstd);
+        double unb = a.B > 1 ? q / (a.B - 1) : q;
+        a.rmean[d] = (float)((1.0 - a.momentum) * a.rmean[d] + a.momentum * mean);
+        a.rvar[d] = (float)((1.0 - a.momentum) * a.rvar[d] + a.momentum * unb);
+        if (d == 0 && a.nbt) a.nbt[0] += 1;
+    }
+}
+
+// e = z / max(||z||, 1e-12), z = h*s + t ; one wave per row
+__global__ __launch_bounds__(256) void normalize_fwd_kernel(ProjArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= a.B) return;
+    float z[4];
+    float ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        int d = lane + 64 * k;
+        z[k] = 0.f;
+        if (d < a.D) {
+            float4 cf = a.cf[d];
+            z[k] = fmaf(a.h[b * a.D + d], cf.x, cf.y);
+            ss = fmaf(z[k], z[k], ss);
+        }
+    }
+    const float n = sqrtf(wave_sum(ss));
+    const float inv = 1.f / fmaxf(n, 1e-12f);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        int d = lane + 64 * k;
+        if (d < a.D) a.emb[b * a.D + d] = z[k] * inv;
+    }
+    if (lane == 0) a.norm[b] = n;
+}
+
+__global__ __launch_bounds__(256) void normalize_bwd_kernel(ProjArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= a.B) return;
+    float e[4], g[4];
+    float dot = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        int d = lane + 64 * k;
+        e[k] = g[k] = 0.f;
+        if (d < a.D) {
+            e[k] = a.emb[b * a.D + d];
+            g[k] = a.demb[b * a.D + d];
+            dot = fmaf(e[k], g[k], dot);
+        }
+    }
+    dot = wave_sum(dot);
+    const float n = a.norm[b];
+    const bool live = n > 1e-12f;
+    const float inv = 1.f / fmaxf(n, 1e-12f);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        int d = lane + 64 * k;
+        if (d < a.D) a.dzp[b * a.D + d] = live ? (g[k] - e[k] * dot) * inv : g[k] * inv;
+    }
+}
+
+__global__ __launch_bounds__(256) void bn1d_bwd_kernel(ProjArgs a) {
+    __shared__ double red[256];
+    const int d = blockIdx.x;
+    const float4 cf = a.cf[d];
+    double s0 = 0.0, s1 = 0.0;
+    for (int b = threadIdx.x; b < a.B; b += blockDim.x) {
+        double g = a.dzp[(int64_t)b * a.D + d];
+        s0 += g;
+        s1 += g * ((double)a.h[(int64_t)b * a.D + d] - cf.z) * cf.w;
+    }
+    s0 = bsum(s0, red);
+    s1 = bsum(s1, red);
+    if (threadIdx.x == 0) {
+        a.dbeta[d] = (float)s0;
+        a.dgamma[d] = (float)s1;
+        a.cfb[d] = make_float4(a.gamma[d] * cf.w, (float)(s0 / a.B), (float)(s1 / a.B) * cf.w, cf.z);
+    }
+}
+
+// dh = BN1d backward ; dpooled = dh @ W
+__global__ __launch_bounds__(256) void proj_bwd_data_kernel(ProjArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float sd[];  // [PR][D]
+    const int b0 = blockIdx.x * PR, tid = threadIdx.x;
+    const int nr = min(PR, a.B - b0);
+    for (int e = tid; e < PR * a.D; e += blockDim.x) {
+        int r = e / a.D, d = e - r * a.D;
+        float v = 0.f;
+        if (r < nr) {
+            int64_t o = (int64_t)(b0 + r) * a.D + d;
+            float4 c = a.cfb[d];
+            v = c.x * (a.dzp[o] - c.y - (a.h[o] - c.w) * c.z);
+            a.dh[o] = v;
+        }
+        sd[e] = v;
+    }
+    __syncthreads();
+    for (int k = tid; k < a.K; k += blockDim.x) {
+        float acc[PR];
+#pragma unroll
+        for (int r = 0; r < PR; ++r) acc[r] = 0.f;
+        for (int d = 0; d < a.D; ++d) {
+            const float w = a.w[(int64_t)d * a.K + k];
+#pragma unroll
+            for (int r = 0; r < PR; ++r) acc[r] = fmaf(sd[r * a.D + d], w, acc[r]);
+        }
+        for (int r = 0; r < nr; ++r) a.dpooled[(int64_t)(b0 + r) * a.K + k] = acc[r];
+    }
+}
+
+// dW[d][k] = sum_b dh[b][d] pooled[b][k] ; db[d] = sum_b dh[b][d] ; one block per d
+__global__ __launch_bounds__(256) void proj_bwd_weight_kernel(ProjArgs a) {
+    __shared__ double red[256];
+    const int d = blockIdx.x, tid = threadIdx.x;
+    for (int k = tid; k < a.K; k += blockDim.x) {
+        float s = 0.f;
+        for (int b = 0; b < a.B; ++b) s = fmaf(a.dh[(int64_t)b * a.D + d], a.pooled[(int64_t)b * a.K + k], s);
+        a.dw[(int64_t)d * a.K + k] = s;
+    }
+    double s = 0.0;
+    for (int b = tid; b < a.B; b += blockDim.x) s += (double)a.dh[(int64_t)b * a.D + d];
+    s = bsum(s, red);
+    if (tid == 0) a.db[d] = (float)s;
+}
+
+__global__ void transpose_kernel(const float* __restrict__ in, float* __restrict__ out, int rows, int cols) {
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= rows * cols) return;
+    int r = e / cols, c = e - r * cols;
+    out[(int64_t)c * rows + r] = in[e];
+}
+
+__global__ __launch_bounds__(256) void row_sum_kernel(const float* __restrict__ part, int64_t cols,
+                                                      float* __restrict__ out) {
+    __shared__ double red[256];
+    const float* p = part + (int64_t)blockIdx.x * cols;
+    double s = 0.0;
+    for (int64_t c = threadIdx.x; c < cols; c += blockDim.x) s += (double)p[c];
+    s = bsum(s, red);
+    if (threadIdx.x == 0) out[blockIdx.x] = (float)s;
+}
+
+size_t pool_smem(const HeadPoolArgs& a, bool bwd) {
+    size_t f = bwd ? (2 * (size_t)a.P + 3 * a.C) : ((size_t)a.P + 2 * a.C);
+    f = (f + 3) / 4 * 4;
+    return (f + 4 * (size_t)a.C) * sizeof(float);
+}
+
+}  // namespace
+
+int launch_head_pool_fwd(HeadPoolArgs a, hipStream_t s) {
+    size_t sm = pool_smem(a, false);
+    PCX_CHECK_ARG(sm <= 160 * 1024, "head: spatial size %d too large", a.P);
+    (void)hipFuncSetAttribute((const void*)head_pool_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    head_pool_fwd_kernel<<<a.B, 256, sm, s>>>(a);
+    PCX_LAUNCH_CHECK("head_pool_fwd_kernel");
+    return PCX_OK;
+}
+
+int launch_head_pool_bwd(HeadPoolArgs a, hipStream_t s) {
+    size_t sm = pool_smem(a, true);
+    PCX_CHECK_ARG(sm <= 160 * 1024, "head: spatial size %d too large", a.P);
+    (void)hipFuncSetAttribute((const void*)head_pool_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    head_pool_bwd_kernel<<<a.B, 256, sm, s>>>(a);
+    PCX_LAUNCH_CHECK("head_pool_bwd_kernel");
+    return PCX_OK;
+}
+
+int launch_proj_fwd(ProjArgs a, hipStream_t s) {
+    PCX_CHECK_ARG(a.D <= 256, "projection: embedding_dim %d > 256 unsupported", a.D);
+    size_t sm = (size_t)PR * a.K * sizeof(float);
+    (void)hipFuncSetAttribute((const void*)proj_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    proj_fwd_kernel<<<ceil_div(a.B, PR), 256, sm, s>>>(a);
+    PCX_LAUNCH_CHECK("proj_fwd_kernel");
+    bn1d_fwd_kernel<<<a.D, 256, 0, s>>>(a);
+    PCX_LAUNCH_CHECK("bn1d_fwd_kernel");
+    normalize_fwd_kernel<<<ceil_div(a.B, 4), 256, 0, s>>>(a);
+    PCX_LAUNCH_CHECK("normalize_fwd_kernel");
+    return PCX_OK;
+}
+
+int launch_proj_bwd(ProjArgs a, hipStream_t s) {
+    normalize_bwd_kernel<<<ceil_div(a.B, 4), 256, 0, s>>>(a);
+    PCX_LAUNCH_CHECK("normalize_bwd_kernel");
+    bn1d_bwd_kernel<<<a.D, 256, 0, s>>>(a);
+    PCX_LAUNCH_CHECK("bn1d_bwd_kernel");
+    size_t sm = (size_t)PR * a.D * sizeof(float);
+    (void)hipFuncSetAttribute((const void*)proj_bwd_data_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    proj_bwd_data_kernel<<<ceil_div(a.B, PR), 256, sm, s>>>(a);
+    PCX_LAUNCH_CHECK("proj_bwd_data_kernel");
+    proj_bwd_weight_kernel<<<a.D, 256, 0, s>>>(a);
+    PCX_LAUNCH_CHECK("proj_bwd_weight_kernel");
+    return PCX_OK;
+}
+
+int launch_transpose(const float* in, float* out, int rows, int cols, hipStream_t s) {
+    transpose_kernel<<<ceil_div((int64_t)rows * cols, 256), 256, 0, s>>>(in, out, rows, cols);
+    PCX_LAUNCH_CHECK("transpose_kernel");
+    return PCX_OK;
+}
+
+int launch_row_sum(const float* part, int rows, int64_t cols, float* out, hipStream_t s) {
+    row_sum_kernel<<<rows, 256, 0, s>>>(part, cols, out);
+    PCX_LAUNCH_CHECK("row_sum_kernel");
+    return PCX_OK;
+}
+
+}  // namespace pcx

@@ -1,0 +1,196 @@
+// Internal (C++) launch interface shared by the kernel files and the network orchestrator.
+// Not part of the C ABI.  All tensors are fp32, planar NCHW (the reference's own layout).
+#pragma once
+#include "pcx_common.h"
+
+namespace pcx {
+
+// ------------------------------------------------------------------ prologue / epilogue kinds
+// What a conv kernel applies to its input while staging it into LDS:
+enum Prologue {
+    PRO_RAW = 0,        // x = src
+    PRO_BNRELU = 1,     // x = max(0, src*s[c] + t[c])                        (cf = {s,t,.,.})
+    PRO_BNRELU_POOL = 2,// x = drop[b,c] * max_2x2 max(0, src*s + t), src at 2x resolution
+    PRO_BNBWD = 3,      // x = a*(dz - mb - (y - mean)*mgi)   src=dz, src2=y   (cf = {a,mb,mgi,mean})
+};
+// What a conv kernel does with its accumulator tile:
+enum Epilogue {
+    EPI_FWD = 0,        // store y, per-block BN statistics (sum, M2, count)
+    EPI_BWD_RELU = 1,   // dz = acc * [yprev*s+t > 0]; store dz; sums of dz and dz*xhat
+    EPI_BWD_POOL = 2,   // route acc (pooled res) through dropout, 2x2 argmax, ReLU to 2x res
+};
+
+// 3x3 / stride 1 / pad 1 convolution as an implicit GEMM on v_mfma_f32_32x32x2_f32.
+// Used for the forward pass (weights packed [9][cin][cout]) and for the data gradient
+// (dy in, dx out, weights packed flipped [9][cout_fwd][cin_fwd]).
+struct ConvArgs {
+    int B, H, W;          // conv resolution (input == output for stride 1, pad 1)
+    int cin, cout;        // GEMM channels (dgrad: cin = dy channels, cout = dx channels)
+    // prologue source
+    const float* src;
+    const float* src2;
+    const float4* cf_in;
+    const float* drop_in;
+    int srcH, srcW;
+    const float* wpack;   // [9][cin][cout]
+    // epilogue
+    float* out;
+    const float* yprev;
+    const float4* cf_out; // EPI_BWD_*: {s, t, mean, invstd} of the BN feeding the prologue
+    const float* drop_out;
+    int Hs, Ws;           // EPI_BWD_POOL: resolution of dz (2H or 2H+1, ...)
+    float* part0;         // [cout][nblk] statistics partials
+    float* part1;
+    float* partn;         // [nblk] element counts (EPI_FWD)
+    int nblk;
+    int NR, RS;           // staged rows / LDS row stride (host-computed)
+};
+
+int launch_conv3x3(int pro, int epi, ConvArgs a, hipStream_t s);
+size_t conv3x3_nblk(int B, int H, int W, int cout);
+
+// Cin = 1 convolution (first layer), 3x3 pad 1, with BN statistics.
+struct Conv1Args {
+    int B, H, W, cout;
+    const float* x;       // [B][1][H][W]
+    const float* w;       // [cout][1][3][3] (reference layout)
+    float* out;           // [B][cout][H][W]
+    float* part0;
+    float* part1;
+    float* partn;
+    int nblk, rows_per_blk;
+};
+int launch_conv1_fwd(Conv1Args a, hipStream_t s);
+int conv1_nblk(int B, int H, int* rows_per_blk);
+
+// Weight gradient of a 3x3 conv: dW[n][c][tap] = sum dy[n] * x[c](shifted), dy = BNBWD(dz, y),
+// x = prologue(src) exactly as in the forward conv.  Partials per slice, then summed.
+struct WgradArgs {
+    int B, H, W, cin, cout;
+    const float* dz;
+    const float* y;
+    const float4* cf_dy;  // {a, mb, mgi, mean}
+    const float* src;
+    const float4* cf_x;
+    const float* drop;
+    int srcH, srcW;
+    float* part;          // [nslice][cout][cin][9]
+    int R, CW, nseg, nrb, nchunks, per_slice, nslice;
+};
+int launch_wgrad3x3(int pro, WgradArgs a, hipStream_t s);
+void wgrad3x3_geometry(int B, int H, int W, int cin, int cout, WgradArgs* a);
+
+// first-layer (Cin = 1) weight gradient
+struct Wgrad1Args {
+    int B, H, W, cout;
+    const float* dz;
+    const float* y;
+    const float4* cf_dy;
+    const float* x;
+    float* part;          // [nslice][cout][9]
+    int nslice, rows_per_slice;
+};
+int launch_wgrad1(Wgrad1Args a, hipStream_t s);
+
+// sum `nslice` partial copies of an n-element array into out (deterministic order)
+int launch_sum_slices(const float* part, int nslice, int64_t n, float* out, hipStream_t s);
+
+// weight packing (reference layout [cout][cin][3][3])
+int launch_pack_fwd(const float* w, float* wp, int cout, int cin, hipStream_t s);   // -> [9][cin][cout]
+int launch_pack_dgrad(const float* w, float* wp, int cout, int cin, hipStream_t s); // -> [9][cout][cin] flipped
+
+// ------------------------------------------------------------------ batch norm finalisers
+struct BnFwdArgs {
+    int C, nblk;
+    const float* part0;   // sums   [C][nblk]
+    const float* part1;   // M2     [C][nblk]
+    const float* partn;   // counts [nblk]
+    const float* gamma;
+    const float* beta;
+    const float* bias;    // conv bias (excluded from the stored raw output) or NULL
+    float* rmean;
+    float* rvar;
+    int64_t* nbt;
+    float momentum, eps;
+    int train;
+    float4* cf;           // out {s, t, mean, invstd}
+};
+int launch_bn_fwd_finalize(BnFwdArgs a, hipStream_t s);
+
+struct BnBwdArgs {
+    int C, nblk;
+    double count;
+    const float* part0;   // sum dz
+    const float* part1;   // sum dz*xhat
+    const float* gamma;
+    const float4* cf_fwd; // {s, t, mean, invstd}
+    float* dgamma;
+    float* dbeta;
+    float4* cf;           // out {a, mb, mgi, mean}
+};
+int launch_bn_bwd_finalize(BnBwdArgs a, hipStream_t s);
+
+}  // namespace pcx
+
+namespace pcx {
+
+// ------------------------------------------------------------------ embedding head
+// SpatialAttention + AdaptiveAvgPool2d(1) (reference phoneme_cnn.py:113-117,129-143) applied to
+// x = drop * relu(y*s + t) (the last BN/ReLU/Dropout2d of the trunk, fused).
+struct HeadPoolArgs {
+    int B, C, P;
+    const float* y;        // [B][C][P] raw conv output
+    const float4* cf;      // {s, t, mean, invstd}
+    const float* drop;     // [B][C] or NULL
+    const float* wa;       // [C] attention 1x1 conv weight, NULL = no attention
+    const float* ba;       // [1]
+    float* pooled;         // [B][C]
+    float* att;            // [B][P] sigmoid map (saved for backward)
+    // backward
+    const float* dpooled;  // [B][C]
+    float* dz;             // [B][C][P]
+    float* p_dz;           // [C][B]
+    float* p_dzx;          // [C][B]
+    float* p_dwa;          // [C][B]
+    float* p_dba;          // [B]
+};
+int launch_head_pool_fwd(HeadPoolArgs a, hipStream_t s);
+int launch_head_pool_bwd(HeadPoolArgs a, hipStream_t s);
+
+// projection Linear(K -> D) + BatchNorm1d(D) + F.normalize (phoneme_cnn.py:75-77,119-124)
+struct ProjArgs {
+    int B, K, D;
+    const float* pooled;   // [B][K]
+    const float* w;        // [D][K] (reference layout)
+    const float* wt;       // [K][D] packed transpose
+    const float* bias;     // [D]
+    const float* gamma;
+    const float* beta;
+    float* rmean;
+    float* rvar;
+    int64_t* nbt;
+    float momentum, eps;
+    int train;
+    float* h;              // [B][D] linear output
+    float4* cf;            // [D] {s, t, mean, invstd}
+    float* emb;            // [B][D]
+    float* norm;           // [B]
+    // backward
+    const float* demb;     // [B][D]
+    float* dzp;            // [B][D]
+    float4* cfb;           // [D] {a, mb, mgi, mean}
+    float* dh;             // [B][D]
+    float* dpooled;        // [B][K]
+    float* dw;             // [D][K]
+    float* db;             // [D]
+    float* dgamma;
+    float* dbeta;
+};
+int launch_proj_fwd(ProjArgs a, hipStream_t s);
+int launch_proj_bwd(ProjArgs a, hipStream_t s);
+int launch_transpose(const float* in, float* out, int rows, int cols, hipStream_t s);
+
+// out[r] = sum_c part[r][c] (float64, fixed order)
+int launch_row_sum(const float* part, int rows, int64_t cols, float* out, hipStream_t s);
+
+}  // namespace pcx

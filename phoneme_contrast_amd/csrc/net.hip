@@ -1,0 +1,475 @@
+// Network plans: the whole PhonemeNet forward / backward as one C-ABI call each.
+//
+// A plan is an immutable host object (shapes, launch geometry, workspace carve-out).  The caller
+// owns every device buffer: parameters and gradients (reference state_dict order), BN running
+// statistics, dropout masks and one workspace of pcx_net_workspace_bytes().  The forward leaves
+// the raw conv outputs y1..y6 and the head state in the workspace; the backward consumes them.
+//
+// cnn_small (reference src/models/phoneme_cnn.py:10-126):
+//   y1 = conv1(x)                         z = BN(y), r = ReLU(z)     (BN/ReLU never stored)
+//   y2 = conv2(r1)          x3 = Dropout2d(MaxPool2(r2))   y3 = conv3(x3)
+//   y4 = conv4(r3)          x5 = Dropout2d(MaxPool2(r4))   y5 = conv5(x5)
+//   y6 = conv6(r5)          x6 = Dropout2d(r6) -> attention -> mean -> Linear -> BN1d -> normalize
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+
+namespace pcx {
+namespace {
+
+struct Region {
+    std::string name;
+    size_t off, bytes;
+};
+
+struct Layer {  // one 3x3 conv of the trunk (L = 1..6)
+    int cin, cout, H, W;   // conv resolution
+    int srcH, srcW;        // resolution of the tensor its prologue reads
+    bool pooled_in;        // prologue includes MaxPool2 + Dropout2d
+    int drop_idx;          // dropout layer feeding its input (pooled_in) or -1
+    size_t y, dz, cf, cfb, wp, wpd;  // workspace offsets
+    int nblk;              // forward statistics tiles
+    WgradArgs wg;          // weight-gradient geometry
+};
+
+struct Plan {
+    pcx_net_config cfg;
+    int B, F, T, D, C6, P6;
+    Layer L[7];
+    int conv1_nblk, conv1_rows;
+    int wg1_nslice, wg1_rows;
+    size_t stat_part, stat_bytes;   // shared scratch for BN partials
+    size_t wg_part, wg_bytes;       // shared scratch for weight-gradient partials
+    size_t pooled, att, h, cfp, cfpb, norm, dzp, dh, dpooled, wt, hp_dz, hp_dzx, hp_dwa, hp_dba;
+    size_t total;
+    std::vector<Region> regions;
+    int nparams, nbn, ndrop, drop_ch[4];
+
+    size_t carve(const char* name, size_t bytes) {
+        size_t off = total;
+        total += (bytes + 255) / 256 * 256;
+        regions.push_back({name, off, bytes});
+        return off;
+    }
+};
+
+inline int hip_status_ok(hipError_t e, const char* what) { return e == hipSuccess ? 0 : hip_status(e, what); }
+
+template <class T>
+T* at(void* ws, size_t off) {
+    return reinterpret_cast<T*>(static_cast<char*>(ws) + off);
+}
+
+// parameter indices (state_dict / named_parameters order) for cnn_small
+inline int p_conv_w(int L) { return 8 * ((L - 1) / 2) + 4 * ((L - 1) % 2); }
+inline int p_conv_b(int L) { return p_conv_w(L) + 1; }
+inline int p_bn_g(int L) { return p_conv_w(L) + 2; }
+inline int p_bn_b(int L) { return p_conv_w(L) + 3; }
+
+int build_small(Plan& p) {
+    const int B = p.B, H1 = p.F, W1 = p.T;
+    PCX_CHECK_ARG(H1 >= 4 && W1 >= 4, "PhonemeNet needs n_mfcc >= 4 and T >= 4 (got %d x %d)", H1, W1);
+    const int H3 = H1 / 2, W3 = W1 / 2, H5 = H3 / 2, W5 = W3 / 2;
+    struct { int cin, cout, H, W, srcH, srcW, pooled, drop; } spec[7] = {
+        {0, 0, 0, 0, 0, 0, 0, -1},
+        {1, 32, H1, W1, H1, W1, 0, -1},
+        {32, 32, H1, W1, H1, W1, 0, -1},
+        {32, 64, H3, W3, H1, W1, 1, 0},
+        {64, 64, H3, W3, H3, W3, 0, -1},
+        {64, 128, H5, W5, H3, W3, 1, 1},
+        {128, 128, H5, W5, H5, W5, 0, -1},
+    };
+    size_t stat = 0, wg = 0;
+    for (int l = 1; l <= 6; ++l) {
+        Layer& L = p.L[l];
+        L.cin = spec[l].cin; L.cout = spec[l].cout; L.H = spec[l].H; L.W = spec[l].W;
+        L.srcH = spec[l].srcH; L.srcW = spec[l].srcW; L.pooled_in = spec[l].pooled; L.drop_idx = spec[l].drop;
+        size_t n = (size_t)B * L.cout * L.H * L.W;
+        char nm[16];
+        snprintf(nm, sizeof nm, "y%d", l);
+        L.y = p.carve(nm, n * 4);
+        snprintf(nm, sizeof nm, "dz%d", l);
+        L.dz = p.carve(nm, n * 4);
+        snprintf(nm, sizeof nm, "cf%d", l);
+        L.cf = p.carve(nm, L.cout * 16);
+        snprintf(nm, sizeof nm, "cfb%d", l);
+        L.cfb = p.carve(nm, L.cout * 16);
+        if (l >= 2) {
+            L.wp = p.carve("wp", (size_t)9 * L.cin * L.cout * 4);
+            L.wpd = p.carve("wpd", (size_t)9 * L.cin * L.cout * 4);
+            L.nblk = (int)conv3x3_nblk(B, L.H, L.W, L.cout);
+            wgrad3x3_geometry(B, L.H, L.W, L.cin, L.cout, &L.wg);
+            wg = std::max(wg, (size_t)L.wg.nslice * L.cout * L.cin * 9);
+        } else {
+            L.nblk = conv1_nblk(B, L.H, &p.conv1_rows);
+            p.conv1_nblk = L.nblk;
+        }
+        stat = std::max(stat, (size_t)2 * L.cout * L.nblk + L.nblk);
+    }
+    // first-layer weight gradient slices
+    {
+        int64_t nrows = (int64_t)B * H1;
+        p.wg1_rows = (int)std::max<int64_t>(1, nrows / 1024);
+        p.wg1_nslice = ceil_div(nrows, p.wg1_rows);
+        wg = std::max(wg, (size_t)p.wg1_nslice * 32 * 9);
+    }
+    p.C6 = 128;
+    p.P6 = H5 * W5;
+    stat = std::max(stat, (size_t)2 * p.C6 * B);
+    p.stat_part = p.carve("stat_part", stat * 4);
+    p.wg_part = p.carve("wg_part", wg * 4);
+    const int D = p.D, K = p.C6;
+    p.pooled = p.carve("pooled", (size_t)B * K * 4);
+    p.att = p.carve("att", (size_t)B * p.P6 * 4);
+    p.h = p.carve("h", (size_t)B * D * 4);
+    p.cfp = p.carve("cfp", (size_t)D * 16);
+    p.cfpb = p.carve("cfpb", (size_t)D * 16);
+    p.norm = p.carve("norm", (size_t)B * 4);
+    p.dzp = p.carve("dzp", (size_t)B * D * 4);
+    p.dh = p.carve("dh", (size_t)B * D * 4);
+    p.dpooled = p.carve("dpooled", (size_t)B * K * 4);
+    p.wt = p.carve("wt", (size_t)K * D * 4);
+    p.hp_dz = p.carve("hp_dz", (size_t)K * B * 4);
+    p.hp_dzx = p.carve("hp_dzx", (size_t)K * B * 4);
+    p.hp_dwa = p.carve("hp_dwa", (size_t)K * B * 4);
+    p.hp_dba = p.carve("hp_dba", (size_t)B * 4);
+    p.nparams = p.cfg.use_attention ? 30 : 28;
+    p.nbn = 7;
+    p.ndrop = 3;
+    p.drop_ch[0] = 32; p.drop_ch[1] = 64; p.drop_ch[2] = 128;
+    return PCX_OK;
+}
+
+#define RC(x)                   \
+    do {                        \
+        int _rc = (x);          \
+        if (_rc) return _rc;    \
+    } while (0)
+
+int small_forward(const Plan& p, const float* const* P, float* const* bnstat, int64_t* const* nbt,
+                  const float* x, const float* const* drop, int train, float* emb, void* ws,
+                  hipStream_t s) {
+    const int B = p.B;
+    const float mom = 0.1f, eps = 1e-5f;
+    const float* dmask[3] = {nullptr, nullptr, nullptr};
+    if (train && drop)
+        for (int i = 0; i < 3; ++i) dmask[i] = drop[i];
+    float* part = at<float>(ws, p.stat_part);
+
+    auto finalize = [&](int l) {
+        const Layer& L = p.L[l];
+        BnFwdArgs f{};
+        f.C = L.cout;
+        f.nblk = L.nblk;
+        f.part0 = part;
+        f.part1 = part + (size_t)L.cout * L.nblk;
+        f.partn = part + (size_t)2 * L.cout * L.nblk;
+        f.gamma = P[p_bn_g(l)];
+        f.beta = P[p_bn_b(l)];
+        f.bias = P[p_conv_b(l)];
+        f.rmean = bnstat[2 * (l - 1)];
+        f.rvar = bnstat[2 * (l - 1) + 1];
+        f.nbt = nbt ? nbt[l - 1] : nullptr;
+        f.momentum = mom;
+        f.eps = eps;
+        f.train = train;
+        f.cf = at<float4>(ws, L.cf);
+        return launch_bn_fwd_finalize(f, s);
+    };
+
+    // layer 1: Cin = 1 direct conv
+    {
+        const Layer& L = p.L[1];
+        Conv1Args c{};
+        c.B = B; c.H = L.H; c.W = L.W; c.cout = L.cout;
+        c.x = x;
+        c.w = P[p_conv_w(1)];
+        c.out = at<float>(ws, L.y);
+        c.part0 = part;
+        c.part1 = part + (size_t)L.cout * L.nblk;
+        c.partn = part + (size_t)2 * L.cout * L.nblk;
+        c.nblk = L.nblk;
+        c.rows_per_blk = p.conv1_rows;
+        RC(launch_conv1_fwd(c, s));
+        RC(finalize(1));
+    }
+    for (int l = 2; l <= 6; ++l) {
+        const Layer& L = p.L[l];
+        const Layer& Lp = p.L[l - 1];
+        RC(launch_pack_fwd(P[p_conv_w(l)], at<float>(ws, L.wp), L.cout, L.cin, s));
+        ConvArgs c{};
+        c.B = B; c.H = L.H; c.W = L.W; c.cin = L.cin; c.cout = L.cout;
+        c.src = at<float>(ws, Lp.y);
+        c.cf_in = at<float4>(ws, Lp.cf);
+        c.drop_in = L.pooled_in ? dmask[L.drop_idx] : nullptr;
+        c.srcH = L.srcH; c.srcW = L.srcW;
+        c.wpack = at<float>(ws, L.wp);
+        c.out = at<float>(ws, L.y);
+        c.part0 = part;
+        c.part1 = part + (size_t)L.cout * L.nblk;
+        c.partn = part + (size_t)2 * L.cout * L.nblk;
+        c.nblk = L.nblk;
+        RC(launch_conv3x3(L.pooled_in ? PRO_BNRELU_POOL : PRO_BNRELU, EPI_FWD, c, s));
+        RC(finalize(l));
+    }
+    // head: attention + mean pool on x6 = Dropout2d(ReLU(BN6(y6)))
+    const int ia = 24, ip = p.cfg.use_attention ? 26 : 24;
+    {
+        HeadPoolArgs h{};
+        h.B = B; h.C = p.C6; h.P = p.P6;
+        h.y = at<float>(ws, p.L[6].y);
+        h.cf = at<float4>(ws, p.L[6].cf);
+        h.drop = dmask[2];
+        h.wa = p.cfg.use_attention ? P[ia] : nullptr;
+        h.ba = p.cfg.use_attention ? P[ia + 1] : nullptr;
+        h.pooled = at<float>(ws, p.pooled);
+        h.att = at<float>(ws, p.att);
+        RC(launch_head_pool_fwd(h, s));
+    }
+    {
+        RC(launch_transpose(P[ip], at<float>(ws, p.wt), p.D, p.C6, s));
+        ProjArgs j{};
+        j.B = B; j.K = p.C6; j.D = p.D;
+        j.pooled = at<float>(ws, p.pooled);
+        j.w = P[ip];
+        j.wt = at<float>(ws, p.wt);
+        j.bias = P[ip + 1];
+        j.gamma = P[ip + 2];
+        j.beta = P[ip + 3];
+        j.rmean = bnstat[12];
+        j.rvar = bnstat[13];
+        j.nbt = nbt ? nbt[6] : nullptr;
+        j.momentum = mom;
+        j.eps = eps;
+        j.train = train;
+        j.h = at<float>(ws, p.h);
+        j.cf = at<float4>(ws, p.cfp);
+        j.emb = emb;
+        j.norm = at<float>(ws, p.norm);
+        RC(launch_proj_fwd(j, s));
+    }
+    return PCX_OK;
+}
+
+int small_backward(const Plan& p, const float* const* P, const float* x, const float* const* drop,
+                   const float* emb, const float* demb, float* const* G, void* ws, hipStream_t s) {
+    const int B = p.B;
+    const float* dmask[3] = {nullptr, nullptr, nullptr};
+    if (drop)
+        for (int i = 0; i < 3; ++i) dmask[i] = drop[i];
+    float* part = at<float>(ws, p.stat_part);
+    float* wgp = at<float>(ws, p.wg_part);
+    const int ia = 24, ip = p.cfg.use_attention ? 26 : 24;
+
+    // projection / BN1d / normalize backward
+    {
+        ProjArgs j{};
+        j.B = B; j.K = p.C6; j.D = p.D;
+        j.pooled = at<float>(ws, p.pooled);
+        j.w = P[ip];
+        j.gamma = P[ip + 2];
+        j.h = at<float>(ws, p.h);
+        j.cf = at<float4>(ws, p.cfp);
+        j.emb = const_cast<float*>(emb);
+        j.norm = at<float>(ws, p.norm);
+        j.demb = demb;
+        j.dzp = at<float>(ws, p.dzp);
+        j.cfb = at<float4>(ws, p.cfpb);
+        j.dh = at<float>(ws, p.dh);
+        j.dpooled = at<float>(ws, p.dpooled);
+        j.dw = G[ip];
+        j.db = G[ip + 1];
+        j.dgamma = G[ip + 2];
+        j.dbeta = G[ip + 3];
+        RC(launch_proj_bwd(j, s));
+    }
+    // attention + pool + Dropout2d + ReLU backward -> dz6 and BN6 partials
+    {
+        HeadPoolArgs h{};
+        h.B = B; h.C = p.C6; h.P = p.P6;
+        h.y = at<float>(ws, p.L[6].y);
+        h.cf = at<float4>(ws, p.L[6].cf);
+        h.drop = dmask[2];
+        h.wa = p.cfg.use_attention ? P[ia] : nullptr;
+        h.ba = p.cfg.use_attention ? P[ia + 1] : nullptr;
+        h.att = at<float>(ws, p.att);
+        h.dpooled = at<float>(ws, p.dpooled);
+        h.dz = at<float>(ws, p.L[6].dz);
+        h.p_dz = part;
+        h.p_dzx = part + (size_t)p.C6 * B;
+        h.p_dwa = at<float>(ws, p.hp_dwa);
+        h.p_dba = at<float>(ws, p.hp_dba);
+        RC(launch_head_pool_bwd(h, s));
+        if (p.cfg.use_attention) {
+            RC(launch_row_sum(h.p_dwa, p.C6, B, G[ia], s));
+            RC(launch_row_sum(h.p_dba, 1, B, G[ia + 1], s));
+        }
+    }
+    auto bwd_finalize = [&](int l, int nblk, double count) {
+        const Layer& L = p.L[l];
+        BnBwdArgs f{};
+        f.C = L.cout;
+        f.nblk = nblk;
+        f.count = count;
+        f.part0 = part;
+        f.part1 = part + (size_t)L.cout * nblk;
+        f.gamma = P[p_bn_g(l)];
+        f.cf_fwd = at<float4>(ws, L.cf);
+        f.dgamma = G[p_bn_g(l)];
+        f.dbeta = G[p_bn_b(l)];
+        f.cf = at<float4>(ws, L.cfb);
+        return launch_bn_bwd_finalize(f, s);
+    };
+    RC(bwd_finalize(6, B, (double)B * p.P6));
+
+    for (int l = 6; l >= 2; --l) {
+        const Layer& L = p.L[l];
+        const Layer& Lp = p.L[l - 1];
+        // conv bias feeding a train-mode BN: exact gradient is zero (sum_b,h,w of BN-backward)
+        RC(hip_status_ok(hipMemsetAsync(G[p_conv_b(l)], 0, L.cout * 4, s), "memset bias grad"));
+        // ---- weight gradient
+        {
+            WgradArgs w = L.wg;
+            w.B = B; w.H = L.H; w.W = L.W; w.cin = L.cin; w.cout = L.cout;
+            w.dz = at<float>(ws, L.dz);
+            w.y = at<float>(ws, L.y);
+            w.cf_dy = at<float4>(ws, L.cfb);
+            w.src = at<float>(ws, Lp.y);
+            w.cf_x = at<float4>(ws, Lp.cf);
+            w.drop = L.pooled_in ? dmask[L.drop_idx] : nullptr;
+            w.srcH = L.srcH; w.srcW = L.srcW;
+            w.part = wgp;
+            RC(launch_wgrad3x3(L.pooled_in ? PRO_BNRELU_POOL : PRO_BNRELU, w, s));
+            RC(launch_sum_slices(wgp, w.nslice, (int64_t)L.cout * L.cin * 9, G[p_conv_w(l)], s));
+        }
+        // ---- data gradient -> dz of the previous BN (through ReLU / MaxPool / Dropout2d)
+        {
+            RC(launch_pack_dgrad(P[p_conv_w(l)], at<float>(ws, L.wpd), L.cout, L.cin, s));
+            float* dzp = at<float>(ws, Lp.dz);
+            if (L.pooled_in && ((L.srcH & 1) || (L.srcW & 1)))
+                RC(hip_status_ok(hipMemsetAsync(dzp, 0, (size_t)B * Lp.cout * L.srcH * L.srcW * 4, s),
+                                 "memset dz"));
+            ConvArgs c{};
+            c.B = B; c.H = L.H; c.W = L.W; c.cin = L.cout; c.cout = L.cin;
+            c.src = at<float>(ws, L.dz);
+            c.src2 = at<float>(ws, L.y);
+            c.cf_in = at<float4>(ws, L.cfb);
+            c.srcH = L.H; c.srcW = L.W;
+            c.wpack = at<float>(ws, L.wpd);
+            c.out = dzp;
+            c.yprev = at<float>(ws, Lp.y);
+            c.cf_out = at<float4>(ws, Lp.cf);
+            c.drop_out = L.pooled_in ? dmask[L.drop_idx] : nullptr;
+            c.Hs = L.srcH; c.Ws = L.srcW;
+            const int nblk = (int)conv3x3_nblk(B, L.H, L.W, L.cin);
+            c.part0 = part;
+            c.part1 = part + (size_t)L.cin * nblk;
+            c.nblk = nblk;
+            RC(launch_conv3x3(PRO_BNBWD, L.pooled_in ? EPI_BWD_POOL : EPI_BWD_RELU, c, s));
+            RC(bwd_finalize(l - 1, nblk, (double)B * Lp.H * Lp.W));
+        }
+    }
+    // layer 1 weight gradient (input has one channel)
+    {
+        const Layer& L = p.L[1];
+        RC(hip_status_ok(hipMemsetAsync(G[p_conv_b(1)], 0, L.cout * 4, s), "memset bias grad"));
+        Wgrad1Args w{};
+        w.B = B; w.H = L.H; w.W = L.W; w.cout = L.cout;
+        w.dz = at<float>(ws, L.dz);
+        w.y = at<float>(ws, L.y);
+        w.cf_dy = at<float4>(ws, L.cfb);
+        w.x = x;
+        w.part = wgp;
+        w.nslice = p.wg1_nslice;
+        w.rows_per_slice = p.wg1_rows;
+        RC(launch_wgrad1(w, s));
+        RC(launch_sum_slices(wgp, w.nslice, (int64_t)L.cout * 9, G[p_conv_w(1)], s));
+    }
+    return PCX_OK;
+}
+
+}  // namespace
+}  // namespace pcx
+
+// ====================================================================== C ABI
+using pcx::Plan;
+
+extern "C" void* pcx_net_create(const pcx_net_config* cfg, int64_t B, int64_t F, int64_t T) {
+    using namespace pcx;
+    if (!cfg) { set_error("pcx_net_create: NULL config"); return nullptr; }
+    if (cfg->in_channels != 1) { set_error("pcx_net_create: in_channels must be 1 (MFCC input)"); return nullptr; }
+    if (B < 1 || F < 1 || T < 1 || B * F * T > ((int64_t)1 << 40)) {
+        set_error("pcx_net_create: bad input shape [%lld,1,%lld,%lld]", (long long)B, (long long)F, (long long)T);
+        return nullptr;
+    }
+    if (cfg->embedding_dim < 1 || cfg->embedding_dim > 256) {
+        set_error("pcx_net_create: embedding_dim %d unsupported (1..256)", cfg->embedding_dim);
+        return nullptr;
+    }
+    Plan* p = new Plan();
+    p->cfg = *cfg;
+    p->B = (int)B; p->F = (int)F; p->T = (int)T; p->D = cfg->embedding_dim;
+    p->total = 0;
+    int rc = PCX_EINVAL;
+    if (cfg->kind == PCX_NET_CNN_SMALL) rc = build_small(*p);
+    else set_error("pcx_net_create: network kind %d not supported", cfg->kind);
+    if (rc) { delete p; return nullptr; }
+    return p;
+}
+
+extern "C" void pcx_net_destroy(void* plan) { delete static_cast<Plan*>(plan); }
+
+extern "C" size_t pcx_net_workspace_bytes(const void* plan) {
+    return plan ? static_cast<const Plan*>(plan)->total : 0;
+}
+
+extern "C" int pcx_net_info(const void* plan, int* nparams, int* nbn, int* ndrop, int* drop_channels) {
+    using namespace pcx;
+    PCX_CHECK_ARG(plan, "pcx_net_info: NULL plan");
+    const Plan* p = static_cast<const Plan*>(plan);
+    if (nparams) *nparams = p->nparams;
+    if (nbn) *nbn = p->nbn;
+    if (ndrop) *ndrop = p->ndrop;
+    if (drop_channels)
+        for (int i = 0; i < p->ndrop; ++i) drop_channels[i] = p->drop_ch[i];
+    return PCX_OK;
+}
+
+extern "C" int pcx_net_region(const void* plan, const char* name, size_t* offset, size_t* bytes) {
+    using namespace pcx;
+    PCX_CHECK_ARG(plan && name, "pcx_net_region: NULL argument");
+    const Plan* p = static_cast<const Plan*>(plan);
+    for (const auto& r : p->regions)
+        if (r.name == name) {
+            if (offset) *offset = r.off;
+            if (bytes) *bytes = r.bytes;
+            return PCX_OK;
+        }
+    set_error("pcx_net_region: no region '%s'", name);
+    return PCX_EINVAL;
+}
+
+extern "C" int pcx_net_forward(const void* plan, const float* const* params, float* const* bn_stats,
+                               int64_t* const* bn_counts, const float* x, const float* const* dropout,
+                               int train, float* emb, void* ws, size_t ws_bytes, hipStream_t stream) {
+    using namespace pcx;
+    PCX_CHECK_ARG(plan && params && bn_stats && x && emb && ws, "pcx_net_forward: NULL argument");
+    const Plan* p = static_cast<const Plan*>(plan);
+    if (ws_bytes < p->total) { set_error("pcx_net_forward: workspace too small"); return PCX_EWORKSPACE; }
+    if (train && p->B < 2) {
+        set_error("Expected more than 1 value per channel when training, got input size [1, %d]", p->D);
+        return PCX_EINVAL;
+    }
+    return small_forward(*p, params, bn_stats, bn_counts, x, dropout, train, emb, ws, stream);
+}
+
+extern "C" int pcx_net_backward(const void* plan, const float* const* params, const float* x,
+                                const float* const* dropout, const float* emb, const float* d_emb,
+                                float* const* grads, void* ws, size_t ws_bytes, hipStream_t stream) {
+    using namespace pcx;
+    PCX_CHECK_ARG(plan && params && x && emb && d_emb && grads && ws, "pcx_net_backward: NULL argument");
+    const Plan* p = static_cast<const Plan*>(plan);
+    if (ws_bytes < p->total) { set_error("pcx_net_backward: workspace too small"); return PCX_EWORKSPACE; }
+    return small_backward(*p, params, x, dropout, emb, d_emb, grads, ws, stream);
+}

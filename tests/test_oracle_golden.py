@@ -108,3 +108,25 @@ def test_eval_forward_matches_reference():
         e, _ = nm.forward(sd, d[f"b{B}/x"], train=False)
         assert np.abs(e - d[f"b{B}/emb"]).max() < 1e-5
         assert np.allclose(np.linalg.norm(e, axis=1), 1.0, atol=1e-6)
+
+
+@pytest.mark.parametrize("name", MODEL_CASES)
+def test_torch_port_matches_reference(name):
+    """The fp32 torch-CPU port (timed CPU baseline) reproduces the reference's fp32 step."""
+    import torch
+    from oracle import torch_port as tp
+    c = model_case(name)
+    sd = {k: torch.tensor(v) for k, v in c["state0"].items()}
+    for k in tp.param_names(sd):
+        sd[k].requires_grad_(True)
+    masks = [torch.tensor(m) for m in c["steps"][0]["masks"]]
+    e = tp.forward(sd, torch.tensor(c["x"]), True, masks)
+    loss = tp.supcon(e, torch.tensor(c["labels"]), c["temperature"], 0.07)
+    loss.backward()
+    assert np.abs(e.detach().numpy() - c["steps"][0]["emb"]).max() < 2e-6
+    assert abs(loss.item() - c["steps"][0]["loss"]) < 2e-5
+    got = {k: sd[k].grad.numpy() for k in tp.param_names(sd)}
+    errs = grad_errors(got, c["grads"])
+    errs64 = grad_errors(got, c["f64"]["grads"])
+    for k in errs:
+        assert min(errs[k][1], errs64[k][1]) < (2e-3 if errs[k][0] == "rel" else 1e-4), (k, errs[k])
