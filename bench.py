@@ -1,0 +1,269 @@
+#!/usr/bin/env python
+"""Benchmark of the north-star hot path: one contrastive train step of cnn_small at batch 4096
+per GPU (reference: ContrastiveTrainer._train_epoch, src/training/trainer.py:126-164), i.e.
+PhonemeNet forward + SupCon + backward + gradient all-reduce (N > 1) + Adam, on synthetic MFCC
+tensors [B, 1, 40, 200].
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Rank 0 prints ONE JSON line.  `value` = MFCC samples processed by all ranks / wall time of the K
+timed steps (max over ranks), inputs resident in HBM.  `roofline` is for the dominant kernel,
+timed live with HIP events on its stream inside the timed region; `cpu_baseline` is the
+float32 torch-CPU port of the reference step (oracle/torch_port.py) on a bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP32_PEAK_TFLOPS = 157.3     # MI355X vector == matrix fp32 (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0        # HBM3E spec
+METRIC = "MFCC-samples/sec per train step (cnn_small, batch 4096) at 1/2/4/8 MI355X"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+# ----------------------------------------------------------------------------- algorithmic cost
+def small_layers(B, F, T):
+    """(label suffix, cin, cout, H, W, src bytes/sample, pooled) for the six convs of cnn_small."""
+    H1, W1 = F, T
+    H3, W3 = H1 // 2, W1 // 2
+    H5, W5 = H3 // 2, W3 // 2
+    return [(1, 1, 32, H1, W1), (2, 32, 32, H1, W1), (3, 32, 64, H3, W3), (4, 64, 64, H3, W3),
+            (5, 64, 128, H5, W5), (6, 128, 128, H5, W5)]
+
+
+def kernel_costs(B, F, T, D=128):
+    """Algorithmic FLOPs and HBM bytes of ONE launch of each profiled kernel label.
+    FLOPs: 2*MACs of the dense contraction.  Bytes: each input tensor read once, each output
+    written once, fp32 (halo / prologue re-reads are not algorithmic)."""
+    L = {l: (ci, co, h, w) for l, ci, co, h, w in small_layers(B, F, T)}
+    src_res = {1: (F, T), 2: (F, T), 3: (F, T), 4: (F // 2, T // 2), 5: (F // 2, T // 2), 6: (F // 4, T // 4)}
+    out = {}
+    for l, (ci, co, h, w) in L.items():
+        macs = B * h * w * co * ci * 9
+        sh, sw = src_res[l]
+        y_out = 4 * B * co * h * w
+        x_in = 4 * B * ci * sh * sw
+        if l == 1:
+            out["conv1_fwd_L1"] = (2 * macs, 4 * B * F * T + y_out)
+            out["wgrad_L1"] = (2 * macs, 2 * y_out + 4 * B * F * T)
+            continue
+        out[f"conv_fwd_L{l}"] = (2 * macs, x_in + y_out)
+        # dgrad: reads dz_l and y_l, reads y_{l-1} (epilogue), writes dz_{l-1}
+        out[f"conv_dgrad_L{l}"] = (2 * macs, 2 * y_out + 2 * x_in)
+        # wgrad: reads dz_l, y_l and the forward input source
+        out[f"wgrad_L{l}"] = (2 * macs, 2 * y_out + x_in)
+    return out
+
+
+def step_cost(B, F, T, D=128):
+    """Algorithmic FLOPs and bytes of one whole train step."""
+    flops = 0
+    act_bytes = 4 * 2 * B * F * T  # input read twice
+    for l, ci, co, h, w in small_layers(B, F, T):
+        macs = B * h * w * co * ci * 9
+        flops += 2 * macs * (2 if l == 1 else 3)
+        act_bytes += 4 * 5 * B * co * h * w
+    flops += 4 * B * B * D + 3 * 2 * B * 128 * D
+    params = 304225
+    return flops, act_bytes + 40 * params + 12 * B * D
+
+
+# ----------------------------------------------------------------------------- CPU baseline
+def cpu_baseline(budget_s=12.0, B=64, T=200):
+    """float32 torch-CPU port of the reference train step (the reference cannot travel to the
+    GPU box), threads = cores - 2 as the reference's device helper sets (device.py:58-61)."""
+    from oracle import torch_port as tp
+    from phoneme_contrast_amd.models import PhonemeNet
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 2)
+    threads = max(1, min(share, os.cpu_count() or share) - 2)
+    torch.set_num_threads(threads)
+    torch.manual_seed(42)
+    sd = {k: v.clone() for k, v in PhonemeNet({"embedding_dim": 128, "dropout_rate": 0.1}).state_dict().items()}
+    tr = tp.CpuTrainer(sd, temperature=0.15)
+    g = torch.Generator().manual_seed(1234)
+    x = torch.randn(B, 1, 40, T, generator=g)
+    labels = torch.arange(B // 4).repeat_interleave(4)
+    masks = [(torch.rand(B, c, generator=g) >= 0.1).float() / 0.9 for c in (32, 64, 128)]
+    tr.step(x, labels, masks)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        tr.step(x, labels, masks)
+        n += 1
+        el = time.perf_counter() - t0
+        if (el > budget_s and n >= 2) or n >= 200:
+            break
+    return {"value": round(B * n / el, 2), "unit": "samples/s", "cores": threads, "kind": "port",
+            "sample": f"cnn_small train step (fwd+SupCon+bwd+Adam) B={B} T={T}, {n} steps in {el:.1f}s, "
+                      f"float32 torch-CPU restatement oracle/torch_port.py, {threads} threads"}
+
+
+def load_pmc(label):
+    """HBM bytes per launch of `label` from a committed rocprofv3 --pmc summary, or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(label, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+# ----------------------------------------------------------------------------- main
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=4096, help="per-GPU batch (views)")
+    ap.add_argument("--T", type=int, default=200)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    args = ap.parse_args()
+
+    from phoneme_contrast_amd import distributed as ddp
+    from phoneme_contrast_amd.losses import SupervisedContrastiveLoss
+    from phoneme_contrast_amd.models import model_registry
+    from phoneme_contrast_amd.optim import FusedAdam
+
+    rank, world, local = ddp.init_from_env()
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    B, F, T, D = args.batch, 40, args.T, 128
+
+    torch.manual_seed(42)
+    model = model_registry.create("phoneme_cnn", {"in_channels": 1, "embedding_dim": D,
+                                                  "use_attention": True, "dropout_rate": 0.1})
+    model = model.to(dev).train()
+    ddp.broadcast_module(model)
+    opt = FusedAdam(model.parameters(), lr=3e-4, weight_decay=1e-4)
+    loss_fn = SupervisedContrastiveLoss(temperature=0.15)
+    g = torch.Generator().manual_seed(1234 + rank)
+    x = torch.randn(B, 1, F, T, generator=g).to(dev)
+    labels = (torch.arange(B // 4).repeat_interleave(4) + rank * (B // 4)).to(dev)
+
+    def step():
+        e = model(x)
+        loss = loss_fn(e, labels)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        if world > 1:
+            flat = opt.flat_grad_views()
+            ddp.allreduce_flat(flat[0])
+            opt.step(flat_grads=flat, grad_scale=1.0 / world)
+        else:
+            opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        loss = step()
+    torch.cuda.synchronize()
+    log(f"rank {rank}: warm-up done, loss {loss.item():.4f}")
+
+    timing = not args.no_kernel_timing
+    if timing:
+        model.kernel_profile(True)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        el = t.item()
+    prof = model.kernel_profile_read() if timing else {}
+    model.kernel_profile(False)
+    final_loss = loss.item()
+
+    if rank != 0:
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
+
+    ms_step = 1000.0 * el / args.steps
+    value = world * B * args.steps / el
+    costs = kernel_costs(B, F, T, D)
+    roof = None
+    kernels = {}
+    if prof:
+        for lab, (tot, cnt) in sorted(prof.items(), key=lambda kv: -kv[1][0]):
+            kernels[lab] = {"avg_ms": round(tot / cnt, 4), "launches": cnt,
+                            "share": round(tot / (1000.0 * el), 4)}
+        dom = max((k for k in prof if k in costs), key=lambda k: prof[k][0])
+        tot, cnt = prof[dom]
+        avg_s = tot / cnt / 1000.0
+        fl, by = costs[dom]
+        ai = fl / by
+        if ai > FP32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9):
+            ach = fl / avg_s / 1e12
+            roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": FP32_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(ach / FP32_PEAK_TFLOPS, 4)}
+        else:
+            ach = by / avg_s / 1e9
+            roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4)}
+        roof["traffic"] = load_pmc(dom)
+        roof["algorithmic_flops_per_launch"] = fl
+        roof["algorithmic_bytes_per_launch"] = by
+        roof["avg_launch_ms"] = round(avg_s * 1000.0, 4)
+    sf, sb = step_cost(B, F, T, D)
+    step_roof = {"flops_per_step": sf, "bytes_per_step": sb,
+                 "mfma_fraction": round(sf / (el / args.steps) / (FP32_PEAK_TFLOPS * 1e12), 4),
+                 "hbm_fraction": round(sb / (el / args.steps) / (HBM_PEAK_GBS * 1e9), 4)}
+
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline()
+        except Exception as exc:  # pragma: no cover - reported, never fatal for the GPU number
+            cpu = {"error": repr(exc)}
+
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic N(0,1) MFCC [B,1,40,T], random-init cnn_small (seed 42)",
+        "config": {"workload": "cnn_small contrastive train step: fwd + SupCon(T=0.15) + bwd + "
+                               "grad all-reduce + Adam(lr 3e-4, wd 1e-4)",
+                   "per_gpu_batch": B, "global_batch": B * world, "n_mfcc": F, "T": T,
+                   "embedding_dim": D, "parallelism": f"dp{world}"},
+        "roofline": roof,
+        "step_roofline": step_roof,
+        "cpu_baseline": cpu,
+        "kernels": kernels,
+        "final_loss": round(final_loss, 5),
+    }
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -105,6 +105,14 @@ int pcx_net_backward(const void* plan, const float* const* params, const float* 
                      float* const* grads, void* workspace, size_t workspace_bytes,
                      hipStream_t stream);
 
+/* Per-launch timing of a plan's kernels with HIP events on the launch stream.
+ * pcx_net_profile(plan, 1) starts recording (and clears), pcx_net_profile_read() waits for the
+ * recorded events, returns the number of distinct kernel labels and fills '\n'-separated labels,
+ * total milliseconds and launch counts per label, then clears. */
+int pcx_net_profile(void* plan, int enable);
+int pcx_net_profile_read(void* plan, char* labels, size_t labels_len, float* total_ms,
+                         int* counts, int max_entries);
+
 /* Dropout2d keep-scale masks: out[i] = (u_i >= p) ? 1/(1-p) : 0 with u_i a counter-based
  * uniform draw from (seed, offset + i).  Not bit-compatible with torch's CPU generator. */
 int pcx_dropout_masks(float* out, int64_t n, float p, uint64_t seed, uint64_t offset,

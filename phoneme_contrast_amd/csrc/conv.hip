@@ -9,7 +9,7 @@
 //                      of ReLU/MaxPool/Dropout plus the BN-backward sums, are fused into the
 //                      epilogue.  No activation tensor is materialised between a conv and its BN.
 //  * conv1_fwd_kernel — the Cin = 1 first conv (phoneme_cnn.py:36): direct, HBM-write-bound.
-//  * wgrad3x3_kernel / wgrad1_kernel — weight gradients, K = B*H*W split over slices.
+//  * wgrad1_kernel — first-layer weight gradient (the 3x3 weight gradients live in wgrad.hip).
 //
 // Tensor layout is the reference's planar NCHW.  MFMA orientation: A = weights (M = output
 // channels), B = input pixels (N = 32 consecutive flattened pixels per lane group), so each
@@ -22,6 +22,14 @@ namespace {
 
 constexpr int PADL = 4;  // left pad of an LDS row: data column 0 sits 16-byte aligned
 constexpr int CK = 8;    // input channels staged per K-chunk
+
+__device__ __forceinline__ int fdiv(int n, int d, float inv) {  // n / d for 0 <= n < 2^22
+    int q = (int)((float)n * inv);
+    int r = n - q * d;
+    if (r < 0) --q;
+    else if (r >= d) ++q;
+    return q;
+}
 
 __device__ __forceinline__ int xcd_remap(int orig, int nb) {
     // blocks b and b+8 share an XCD (observed round-robin dispatch): give each XCD a contiguous
@@ -115,6 +123,7 @@ __device__ __forceinline__ float4 pro_quad(const ConvArgs& a, int c, int b, int 
 // ------------------------------------------------------------------ 3x3 implicit GEMM
 template <int WM, int WN, int PRO, int EPI>
 __global__ __launch_bounds__(256) void conv3x3_kernel(ConvArgs a) {
+    constexpr int SU = (PRO == PRO_BNRELU_POOL || PRO == PRO_BNBWD) ? 2 : 4;  // staging unroll
     constexpr int COUT_T = 32 * WM;
     constexpr int BP = 4 * WN * 32;  // pixels per block
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -160,27 +169,47 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvArgs a) {
 #pragma unroll
         for (int ni = 0; ni < WN; ++ni) acc[mi][ni] = f32x16{0.f};
 
+    // staged-row table: sample and row of every LDS row (b = -1 outside the batch)
+    __shared__ int2 rinfo[160];
+    for (int lr = tid; lr < a.NR; lr += 256) {
+        int64_t gr = row0 + lr;
+        bool ok = gr >= 0 && gr < nrows;
+        int b = ok ? (int)(gr / a.H) : -1;
+        rinfo[lr] = make_int2(b, ok ? (int)(gr - (int64_t)b * a.H) : 0);
+    }
     const int Q = a.RS >> 2;
+    const int QT = CK * a.NR * Q;
+    const float invQ = 1.f / Q, invNR = 1.f / a.NR;
+    const int wlast = ((a.W - 1) >> 2) << 2;  // start of the last data quad
     for (int c0 = 0; c0 < a.cin; c0 += CK) {
         __syncthreads();
-        // ---- stage CK input channels x NR rows (prologue applied), one row per wave
-        for (int row = wave; row < CK * a.NR; row += 4) {
-            int cl = row / a.NR;
-            int lr = row - cl * a.NR;
-            int64_t gr = row0 + lr;
-            bool rowok = gr >= 0 && gr < nrows;
-            int b = rowok ? (int)(gr / a.H) : 0;
-            int hh = rowok ? (int)(gr - (int64_t)b * a.H) : 0;
-            float* dst = xs + cl * PLANE + lr * a.RS;
-            for (int q = lane; q < Q; q += 64) {
-                int w = (q - 1) * 4;
-                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (rowok && q >= 1 && w < a.W) v = pro_quad<PRO>(a, c0 + cl, b, hh, w);
-                st4(dst + 4 * q, v);
+        // ---- stage CK input channels x NR rows (prologue applied); U quads in flight per thread
+        for (int e0 = tid; e0 < QT; e0 += 256 * SU) {
+            float4 v[SU];
+            int dst[SU];
+#pragma unroll
+            for (int u = 0; u < SU; ++u) {
+                const int e = e0 + u * 256;
+                const bool in = e < QT;
+                const int ee = in ? e : 0;
+                const int row = fdiv(ee, Q, invQ);
+                const int q = ee - row * Q;
+                const int cl = fdiv(row, a.NR, invNR);
+                const int lr = row - cl * a.NR;
+                const int2 ri = rinfo[lr];
+                const int w = (q - 1) * 4;
+                const bool ok = in && ri.x >= 0 && q >= 1 && w < a.W;
+                float4 t = pro_quad<PRO>(a, c0 + cl, max(ri.x, 0), ri.y, min(max(w, 0), wlast));
+                v[u] = ok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+                dst[u] = in ? cl * PLANE + lr * a.RS + 4 * q : -1;
             }
+#pragma unroll
+            for (int u = 0; u < SU; ++u)
+                if (dst[u] >= 0) st4(xs + dst[u], v[u]);
         }
         // ---- stage the weight chunk [9][CK][COUT_T]
         constexpr int QW = COUT_T / 4;
+#pragma unroll 4
         for (int slot = tid; slot < 9 * CK * QW; slot += 256) {
             int row = slot / QW, q = slot - row * QW;
             int tap = row / CK, cc = row - tap * CK;
@@ -428,112 +457,6 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Args a) {
     }
 }
 
-// ------------------------------------------------------------------ weight gradient 3x3
-template <int PRO>
-__device__ __forceinline__ float wg_pro(const WgradArgs& a, int c, int b, int hh, int w) {
-    if (PRO == PRO_RAW) {
-        return a.src[(((int64_t)b * a.cin + c) * a.H + hh) * a.W + w];
-    } else if (PRO == PRO_BNRELU) {
-        float4 cf = a.cf_x[c];
-        return fmaxf(fmaf(a.src[(((int64_t)b * a.cin + c) * a.H + hh) * a.W + w], cf.x, cf.y), 0.f);
-    } else {  // PRO_BNRELU_POOL
-        float4 cf = a.cf_x[c];
-        const float* p = a.src + (((int64_t)b * a.cin + c) * a.srcH + 2 * hh) * a.srcW + 2 * w;
-        float m = fmaxf(fmaxf(fmaf(p[0], cf.x, cf.y), fmaf(p[1], cf.x, cf.y)),
-                        fmaxf(fmaf(p[a.srcW], cf.x, cf.y), fmaf(p[a.srcW + 1], cf.x, cf.y)));
-        m = fmaxf(m, 0.f);
-        return a.drop ? m * a.drop[(int64_t)b * a.cin + c] : m;
-    }
-}
-
-template <int PRO>
-__global__ __launch_bounds__(256) void wgrad3x3_kernel(WgradArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int P = a.R * a.CW;           // dy positions per chunk
-    const int PS = P + 1;               // odd strides: conflict-free column reads
-    const int XS = a.CW + 2;
-    const int XP = (a.R + 2) * XS + 1;
-    float* dyt = smem;                  // [32][PS]
-    float* xt = smem + 32 * PS;         // [32][XP]
-    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int ncg = a.cin / 32;
-    const int mi = blockIdx.y / ncg, ci = blockIdx.y - mi * ncg;
-    const int n0 = mi * 32, c0 = ci * 32;
-
-    f32x16 acc[9];
-#pragma unroll
-    for (int t = 0; t < 9; ++t) acc[t] = f32x16{0.f};
-
-    const int ch0 = blockIdx.x * a.per_slice;
-    const int ch1 = min(a.nchunks, ch0 + a.per_slice);
-    for (int chunk = ch0; chunk < ch1; ++chunk) {
-        const int seg = chunk % a.nseg;
-        const int rb = (chunk / a.nseg) % a.nrb;
-        const int b = chunk / (a.nseg * a.nrb);
-        const int h0 = rb * a.R, w0 = seg * a.CW;
-        __syncthreads();
-        // dy rows: BN backward applied to (dz, y)
-        for (int row = wave; row < 32 * a.R; row += 4) {
-            int n = row / a.R, r = row - n * a.R;
-            int hh = h0 + r;
-            float4 cf = a.cf_dy[n0 + n];
-            int64_t base = (((int64_t)b * a.cout + n0 + n) * a.H + hh) * a.W;
-            float* dst = dyt + n * PS + r * a.CW;
-            for (int e = lane; e < a.CW; e += 64) {
-                int w = w0 + e;
-                float v = 0.f;
-                if (hh < a.H && w < a.W) {
-                    float dz = a.dz[base + w], y = a.y[base + w];
-                    v = cf.x * (dz - cf.y - (y - cf.w) * cf.z);
-                }
-                dst[e] = v;
-            }
-        }
-        // x rows h0-1 .. h0+R (zero outside the sample), columns w0-1 .. w0+CW
-        for (int row = wave; row < 32 * (a.R + 2); row += 4) {
-            int c = row / (a.R + 2), rr = row - c * (a.R + 2);
-            int hh = h0 - 1 + rr;
-            bool rowok = hh >= 0 && hh < a.H;
-            float* dst = xt + c * XP + rr * XS;
-            for (int e = lane; e < XS; e += 64) {
-                int w = w0 - 1 + e;
-                dst[e] = (rowok && w >= 0 && w < a.W) ? wg_pro<PRO>(a, c0 + c, b, hh, w) : 0.f;
-            }
-        }
-        __syncthreads();
-        for (int s = wave; s < P / 2; s += 4) {
-            const int p0 = 2 * s;
-            const int r = p0 / a.CW;
-            const int w = p0 - r * a.CW;
-            const float av = dyt[l32 * PS + p0 + h];
-            const float* xb = xt + l32 * XP + r * XS + w + h;
-#pragma unroll
-            for (int t = 0; t < 9; ++t) acc[t] = mfma32(av, xb[(t / 3) * XS + (t % 3)], acc[t]);
-        }
-    }
-    // reduce the 4 waves' K-split accumulators through LDS (deterministic order)
-    __syncthreads();
-    float* red = smem;  // [9][32][32]
-    for (int w = 0; w < 4; ++w) {
-        if (wave == w) {
-#pragma unroll
-            for (int t = 0; t < 9; ++t)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    float* d = red + (t * 32 + acc_row(r, h)) * 32 + l32;
-                    *d = (w == 0) ? acc[t][r] : *d + acc[t][r];
-                }
-        }
-        __syncthreads();
-    }
-    float* out = a.part + (int64_t)blockIdx.x * a.cout * a.cin * 9;
-    for (int e = tid; e < 32 * 32 * 9; e += 256) {
-        int i = e / 288, rem = e - i * 288, j = rem / 9, t = rem - j * 9;
-        out[((int64_t)(n0 + i) * a.cin + c0 + j) * 9 + t] = red[(t * 32 + i) * 32 + j];
-    }
-}
-
 // ------------------------------------------------------------------ weight gradient, Cin = 1
 __global__ __launch_bounds__(256) void wgrad1_kernel(Wgrad1Args a) {
     const int lane = threadIdx.x & 63;
@@ -629,7 +552,7 @@ int launch_conv3x3(int pro, int epi, ConvArgs a, hipStream_t s) {
     size_t smem = ((size_t)CK * a.NR * a.RS + 9 * CK * cout_t) * sizeof(float);
     size_t red = (size_t)4 * cout_t * 3 * sizeof(float);
     if (smem < red) smem = red;
-    PCX_CHECK_ARG(smem <= 160 * 1024, "conv3x3: W=%d needs %zu B of LDS", a.W, smem);
+    PCX_CHECK_ARG(smem <= 150 * 1024 && a.NR <= 160, "conv3x3: W=%d needs %zu B of LDS", a.W, smem);
     dim3 grid((unsigned)(ntile * (a.cout / cout_t)));
     if (wm == 1 && wn == 4) return launch_tiles<1, 4>(pro, epi, a, grid, smem, s);
     return launch_tiles<2, 2>(pro, epi, a, grid, smem, s);
@@ -647,47 +570,6 @@ int launch_conv1_fwd(Conv1Args a, hipStream_t s) {
     conv1_fwd_kernel<<<a.nblk, 256, 0, s>>>(a);
     PCX_LAUNCH_CHECK("conv1_fwd_kernel");
     return PCX_OK;
-}
-
-void wgrad3x3_geometry(int B, int H, int W, int cin, int cout, WgradArgs* a) {
-    int cw = W < 100 ? W : 100;
-    cw += cw & 1;
-    int R = std::max(1, 200 / cw);
-    R = std::min(R, H);
-    a->CW = cw;
-    a->R = R;
-    a->nseg = ceil_div(W, cw);
-    a->nrb = ceil_div(H, R);
-    a->nchunks = B * a->nrb * a->nseg;
-    int ngroups = (cout / 32) * (cin / 32);
-    int want = std::max(1, 2048 / ngroups);
-    want = std::min(want, a->nchunks);
-    a->per_slice = ceil_div(a->nchunks, want);
-    a->nslice = ceil_div(a->nchunks, a->per_slice);
-}
-
-int launch_wgrad3x3(int pro, WgradArgs a, hipStream_t s) {
-    PCX_CHECK_ARG(a.cin % 32 == 0 && a.cout % 32 == 0, "wgrad3x3: channels must be multiples of 32");
-    const int P = a.R * a.CW;
-    size_t smem = ((size_t)32 * (P + 1) + (size_t)32 * ((a.R + 2) * (a.CW + 2) + 1)) * sizeof(float);
-    size_t red = (size_t)9 * 32 * 32 * sizeof(float);
-    if (smem < red) smem = red;
-    PCX_CHECK_ARG(smem <= 160 * 1024, "wgrad3x3: LDS %zu too large", smem);
-    dim3 grid(a.nslice, (a.cout / 32) * (a.cin / 32));
-#define PCX_WG_CASE(P_)                                                                          \
-    if (pro == P_) {                                                                            \
-        (void)hipFuncSetAttribute((const void*)wgrad3x3_kernel<P_>,                                   \
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);            \
-        wgrad3x3_kernel<P_><<<grid, 256, smem, s>>>(a);                                         \
-        PCX_LAUNCH_CHECK("wgrad3x3_kernel");                                                    \
-        return PCX_OK;                                                                          \
-    }
-    PCX_WG_CASE(PRO_RAW)
-    PCX_WG_CASE(PRO_BNRELU)
-    PCX_WG_CASE(PRO_BNRELU_POOL)
-#undef PCX_WG_CASE
-    set_error("wgrad3x3: unsupported prologue %d", pro);
-    return PCX_EINVAL;
 }
 
 int launch_wgrad1(Wgrad1Args a, hipStream_t s) {

@@ -76,6 +76,7 @@ struct WgradArgs {
     int srcH, srcW;
     float* part;          // [nslice][cout][cin][9]
     int R, CW, nseg, nrb, nchunks, per_slice, nslice;
+    int MT, NPM, NPC;     // MFMA tile (16 or 32), tiles per block along cout / cin
 };
 int launch_wgrad3x3(int pro, WgradArgs a, hipStream_t s);
 void wgrad3x3_geometry(int B, int H, int W, int cin, int cout, WgradArgs* a);

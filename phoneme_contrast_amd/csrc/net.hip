@@ -23,6 +23,54 @@ struct Region {
     size_t off, bytes;
 };
 
+// Optional per-launch HIP-event timing (pcx_net_profile): lets bench.py time individual kernels
+// on the stream they run on, inside its timed region.
+struct Profiler {
+    bool on = false;
+    std::vector<hipEvent_t> pool;
+    size_t used = 0;
+    std::vector<std::string> labels;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> spans;
+    hipEvent_t get() {
+        if (used == pool.size()) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+            pool.push_back(e);
+        }
+        return pool[used++];
+    }
+    void clear() {
+        used = 0;
+        labels.clear();
+        spans.clear();
+    }
+    ~Profiler() {
+        for (auto e : pool) (void)hipEventDestroy(e);
+    }
+};
+
+struct Scope {
+    Profiler* p;
+    hipStream_t s;
+    hipEvent_t a = nullptr;
+    std::string label;
+    Scope(Profiler* prof, hipStream_t st, const char* lab, int layer = -1) : p(prof), s(st) {
+        if (!p->on) return;
+        label = lab;
+        if (layer >= 0) label += "_L" + std::to_string(layer);
+        a = p->get();
+        if (a) (void)hipEventRecord(a, s);
+    }
+    ~Scope() {
+        if (!p->on || !a) return;
+        hipEvent_t b = p->get();
+        if (!b) return;
+        (void)hipEventRecord(b, s);
+        p->labels.push_back(label);
+        p->spans.push_back({a, b});
+    }
+};
+
 struct Layer {  // one 3x3 conv of the trunk (L = 1..6)
     int cin, cout, H, W;   // conv resolution
     int srcH, srcW;        // resolution of the tensor its prologue reads
@@ -45,6 +93,7 @@ struct Plan {
     size_t total;
     std::vector<Region> regions;
     int nparams, nbn, ndrop, drop_ch[4];
+    mutable Profiler prof;
 
     size_t carve(const char* name, size_t bytes) {
         size_t off = total;
@@ -175,6 +224,7 @@ int small_forward(const Plan& p, const float* const* P, float* const* bnstat, in
         f.eps = eps;
         f.train = train;
         f.cf = at<float4>(ws, L.cf);
+        Scope sc(&p.prof, s, "bn_fwd_finalize");
         return launch_bn_fwd_finalize(f, s);
     };
 
@@ -191,7 +241,7 @@ int small_forward(const Plan& p, const float* const* P, float* const* bnstat, in
         c.partn = part + (size_t)2 * L.cout * L.nblk;
         c.nblk = L.nblk;
         c.rows_per_blk = p.conv1_rows;
-        RC(launch_conv1_fwd(c, s));
+        { Scope sc(&p.prof, s, "conv1_fwd", 1); RC(launch_conv1_fwd(c, s)); }
         RC(finalize(1));
     }
     for (int l = 2; l <= 6; ++l) {
@@ -210,7 +260,7 @@ int small_forward(const Plan& p, const float* const* P, float* const* bnstat, in
         c.part1 = part + (size_t)L.cout * L.nblk;
         c.partn = part + (size_t)2 * L.cout * L.nblk;
         c.nblk = L.nblk;
-        RC(launch_conv3x3(L.pooled_in ? PRO_BNRELU_POOL : PRO_BNRELU, EPI_FWD, c, s));
+        { Scope sc(&p.prof, s, "conv_fwd", l); RC(launch_conv3x3(L.pooled_in ? PRO_BNRELU_POOL : PRO_BNRELU, EPI_FWD, c, s)); }
         RC(finalize(l));
     }
     // head: attention + mean pool on x6 = Dropout2d(ReLU(BN6(y6)))
@@ -225,7 +275,7 @@ int small_forward(const Plan& p, const float* const* P, float* const* bnstat, in
         h.ba = p.cfg.use_attention ? P[ia + 1] : nullptr;
         h.pooled = at<float>(ws, p.pooled);
         h.att = at<float>(ws, p.att);
-        RC(launch_head_pool_fwd(h, s));
+        { Scope sc(&p.prof, s, "head_pool_fwd"); RC(launch_head_pool_fwd(h, s)); }
     }
     {
         RC(launch_transpose(P[ip], at<float>(ws, p.wt), p.D, p.C6, s));
@@ -247,7 +297,7 @@ int small_forward(const Plan& p, const float* const* P, float* const* bnstat, in
         j.cf = at<float4>(ws, p.cfp);
         j.emb = emb;
         j.norm = at<float>(ws, p.norm);
-        RC(launch_proj_fwd(j, s));
+        { Scope sc(&p.prof, s, "proj_fwd"); RC(launch_proj_fwd(j, s)); }
     }
     return PCX_OK;
 }
@@ -282,7 +332,7 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
         j.db = G[ip + 1];
         j.dgamma = G[ip + 2];
         j.dbeta = G[ip + 3];
-        RC(launch_proj_bwd(j, s));
+        { Scope sc(&p.prof, s, "proj_bwd"); RC(launch_proj_bwd(j, s)); }
     }
     // attention + pool + Dropout2d + ReLU backward -> dz6 and BN6 partials
     {
@@ -300,7 +350,7 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
         h.p_dzx = part + (size_t)p.C6 * B;
         h.p_dwa = at<float>(ws, p.hp_dwa);
         h.p_dba = at<float>(ws, p.hp_dba);
-        RC(launch_head_pool_bwd(h, s));
+        { Scope sc(&p.prof, s, "head_pool_bwd"); RC(launch_head_pool_bwd(h, s)); }
         if (p.cfg.use_attention) {
             RC(launch_row_sum(h.p_dwa, p.C6, B, G[ia], s));
             RC(launch_row_sum(h.p_dba, 1, B, G[ia + 1], s));
@@ -319,6 +369,7 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
         f.dgamma = G[p_bn_g(l)];
         f.dbeta = G[p_bn_b(l)];
         f.cf = at<float4>(ws, L.cfb);
+        Scope sc(&p.prof, s, "bn_bwd_finalize");
         return launch_bn_bwd_finalize(f, s);
     };
     RC(bwd_finalize(6, B, (double)B * p.P6));
@@ -340,8 +391,8 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
             w.drop = L.pooled_in ? dmask[L.drop_idx] : nullptr;
             w.srcH = L.srcH; w.srcW = L.srcW;
             w.part = wgp;
-            RC(launch_wgrad3x3(L.pooled_in ? PRO_BNRELU_POOL : PRO_BNRELU, w, s));
-            RC(launch_sum_slices(wgp, w.nslice, (int64_t)L.cout * L.cin * 9, G[p_conv_w(l)], s));
+            { Scope sc(&p.prof, s, "wgrad", l); RC(launch_wgrad3x3(L.pooled_in ? PRO_BNRELU_POOL : PRO_BNRELU, w, s)); }
+            { Scope sc(&p.prof, s, "wgrad_reduce", l); RC(launch_sum_slices(wgp, w.nslice, (int64_t)L.cout * L.cin * 9, G[p_conv_w(l)], s)); }
         }
         // ---- data gradient -> dz of the previous BN (through ReLU / MaxPool / Dropout2d)
         {
@@ -366,7 +417,7 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
             c.part0 = part;
             c.part1 = part + (size_t)L.cin * nblk;
             c.nblk = nblk;
-            RC(launch_conv3x3(PRO_BNBWD, L.pooled_in ? EPI_BWD_POOL : EPI_BWD_RELU, c, s));
+            { Scope sc(&p.prof, s, "conv_dgrad", l); RC(launch_conv3x3(PRO_BNBWD, L.pooled_in ? EPI_BWD_POOL : EPI_BWD_RELU, c, s)); }
             RC(bwd_finalize(l - 1, nblk, (double)B * Lp.H * Lp.W));
         }
     }
@@ -383,7 +434,7 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
         w.part = wgp;
         w.nslice = p.wg1_nslice;
         w.rows_per_slice = p.wg1_rows;
-        RC(launch_wgrad1(w, s));
+        { Scope sc(&p.prof, s, "wgrad", 1); RC(launch_wgrad1(w, s)); }
         RC(launch_sum_slices(wgp, w.nslice, (int64_t)L.cout * 9, G[p_conv_w(1)], s));
     }
     return PCX_OK;
@@ -472,4 +523,49 @@ extern "C" int pcx_net_backward(const void* plan, const float* const* params, co
     const Plan* p = static_cast<const Plan*>(plan);
     if (ws_bytes < p->total) { set_error("pcx_net_backward: workspace too small"); return PCX_EWORKSPACE; }
     return small_backward(*p, params, x, dropout, emb, d_emb, grads, ws, stream);
+}
+
+extern "C" int pcx_net_profile(void* plan, int enable) {
+    using namespace pcx;
+    PCX_CHECK_ARG(plan, "pcx_net_profile: NULL plan");
+    Plan* p = static_cast<Plan*>(plan);
+    p->prof.clear();
+    p->prof.on = enable != 0;
+    return PCX_OK;
+}
+
+extern "C" int pcx_net_profile_read(void* plan, char* labels, size_t labels_len, float* total_ms,
+                                    int* counts, int max_entries) {
+    using namespace pcx;
+    PCX_CHECK_ARG(plan, "pcx_net_profile_read: NULL plan");
+    Plan* p = static_cast<Plan*>(plan);
+    std::vector<std::string> names;
+    std::vector<double> tot;
+    std::vector<int> cnt;
+    for (size_t i = 0; i < p->prof.spans.size(); ++i) {
+        float ms = 0.f;
+        hipError_t e = hipEventSynchronize(p->prof.spans[i].second);
+        if (e != hipSuccess) return hip_status(e, "pcx_net_profile_read");
+        (void)hipEventElapsedTime(&ms, p->prof.spans[i].first, p->prof.spans[i].second);
+        size_t k = 0;
+        while (k < names.size() && names[k] != p->prof.labels[i]) ++k;
+        if (k == names.size()) { names.push_back(p->prof.labels[i]); tot.push_back(0.0); cnt.push_back(0); }
+        tot[k] += ms;
+        cnt[k] += 1;
+    }
+    std::string joined;
+    int n = 0;
+    for (size_t k = 0; k < names.size() && (int)k < max_entries; ++k, ++n) {
+        if (total_ms) total_ms[k] = (float)tot[k];
+        if (counts) counts[k] = cnt[k];
+        joined += names[k];
+        joined += '\n';
+    }
+    if (labels && labels_len) {
+        size_t c = std::min(joined.size(), labels_len - 1);
+        memcpy(labels, joined.data(), c);
+        labels[c] = 0;
+    }
+    p->prof.clear();
+    return n;
 }

@@ -139,10 +139,35 @@ class _NativeNet(BaseModel):
         p = self._plans.get(key)
         if p is None:
             p = _Plan(self._net_config(), B, F, T)
+            if getattr(self, "_profiling", False):
+                _lib.check(_lib.lib().pcx_net_profile(p.handle, 1), "pcx_net_profile")
             if p.nparams != len(list(self.parameters())):
                 raise RuntimeError("native plan / module parameter count mismatch")
             self._plans[key] = p
         return p
+
+    def kernel_profile(self, enable: bool = True):
+        """Start (or stop) per-launch HIP-event timing of the native kernels (all cached plans)."""
+        lib = _lib.lib()
+        self._profiling = bool(enable)
+        for p in self._plans.values():
+            _lib.check(lib.pcx_net_profile(p.handle, 1 if enable else 0), "pcx_net_profile")
+
+    def kernel_profile_read(self):
+        """{kernel label: (total_ms, launches)} since kernel_profile(True); waits for the events."""
+        lib = _lib.lib()
+        out = {}
+        for p in self._plans.values():
+            buf = ctypes.create_string_buffer(8192)
+            ms = (ctypes.c_float * 256)()
+            cnt = (ctypes.c_int * 256)()
+            n = lib.pcx_net_profile_read(p.handle, buf, 8192, ms, cnt, 256)
+            if n < 0:
+                _lib.check(n, "pcx_net_profile_read")
+            for i, lab in enumerate(buf.value.decode().split("\n")[:n]):
+                t, c = out.get(lab, (0.0, 0))
+                out[lab] = (t + ms[i], c + cnt[i])
+        return out
 
     def set_dropout_masks(self, masks: Optional[List[torch.Tensor]]):
         """Inject the Dropout2d keep-scale masks ([B, C] each, 0 or 1/(1-p)) used by the next
