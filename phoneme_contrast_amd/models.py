@@ -321,3 +321,73 @@ class PhonemeNet(_NativeNet):
         cfg.embedding_dim = self.embedding_dim
         cfg.use_attention = 1 if self.use_attention else 0
         return cfg
+
+
+class ResidualBlock(nn.Module):
+    """Residual block parameter holder (reference phoneme_cnn.py:146-184): conv3x3(stride) + BN +
+    ReLU, Dropout2d, conv3x3 + BN, shortcut = identity or conv1x1(stride) + BN, add, ReLU."""
+
+    def __init__(self, in_channels, out_channels, stride=1, dropout_rate=0.1):
+        super().__init__()
+        self.conv1 = nn.Conv2d(in_channels, out_channels, 3, stride=stride, padding=1)
+        self.bn1 = nn.BatchNorm2d(out_channels)
+        self.conv2 = nn.Conv2d(out_channels, out_channels, 3, padding=1)
+        self.bn2 = nn.BatchNorm2d(out_channels)
+        self.dropout = nn.Dropout2d(dropout_rate)
+        self.shortcut = nn.Sequential()
+        if stride != 1 or in_channels != out_channels:
+            self.shortcut = nn.Sequential(nn.Conv2d(in_channels, out_channels, 1, stride=stride),
+                                          nn.BatchNorm2d(out_channels))
+
+
+@model_registry.register("phoneme_cnn_deep")
+class PhonemeNetDeep(_NativeNet):
+    """cnn_deep (reference src/models/phoneme_cnn.py:187-304): 7x7 stem + MaxPool(3,2,1), four
+    ResidualBlocks (strides 1,2,2,2), SpatialAttention, pool, Linear+BatchNorm1d, normalize."""
+
+    _kind = 1
+
+    def __init__(self, config: dict):
+        super().__init__(config)
+        self.in_channels = config.get("in_channels", 1)
+        self.embedding_dim = config.get("embedding_dim", 128)
+        self.use_attention = config.get("use_attention", True)
+        self.dropout_rate = config.get("dropout_rate", 0.2)
+        self.hidden_dims = list(config.get("hidden_dims", [64, 128, 256, 512]))
+        self.use_residual = config.get("use_residual", True)
+        self._build_network()
+        self._initialize_weights()
+
+    def _build_network(self) -> None:
+        h = self.hidden_dims
+        self.init_conv = nn.Sequential(nn.Conv2d(self.in_channels, h[0], 7, stride=1, padding=3),
+                                       nn.BatchNorm2d(h[0]), nn.ReLU(inplace=True),
+                                       nn.MaxPool2d(3, stride=2, padding=1))
+        blocks, cin = [], h[0]
+        for i, cout in enumerate(h):
+            s = 1 if i == 0 else 2
+            if self.use_residual:
+                blocks.append(ResidualBlock(cin, cout, s, self.dropout_rate))
+            else:  # reference phoneme_cnn.py:230-243
+                blocks.append(nn.Sequential(
+                    nn.Conv2d(cin, cout, 3, stride=s, padding=1), nn.BatchNorm2d(cout), nn.ReLU(inplace=True),
+                    nn.Conv2d(cout, cout, 3, padding=1), nn.BatchNorm2d(cout), nn.ReLU(inplace=True),
+                    nn.Dropout2d(self.dropout_rate)))
+            cin = cout
+        self.conv_blocks = nn.Sequential(*blocks)
+        if self.use_attention:
+            self.attention = SpatialAttention(h[-1])
+        self.global_pool = nn.AdaptiveAvgPool2d(1)
+        self.projection = nn.Sequential(nn.Linear(h[-1], self.embedding_dim),
+                                        nn.BatchNorm1d(self.embedding_dim))
+
+    def _net_config(self):
+        cfg = _lib.NetConfig()
+        cfg.kind = self._kind
+        cfg.in_channels = self.in_channels
+        cfg.embedding_dim = self.embedding_dim
+        cfg.use_attention = 1 if self.use_attention else 0
+        for i, d in enumerate(self.hidden_dims[:4]):
+            cfg.hidden_dims[i] = d
+        cfg.use_residual = 1 if self.use_residual else 0
+        return cfg
