@@ -16,7 +16,7 @@
 namespace pcx {
 namespace {
 
-constexpr int U = 4;  // staging loads in flight per thread
+constexpr int U = 8;  // staging loads in flight per thread
 
 __device__ __forceinline__ int fdiv(int n, int d, float inv) {
     int q = (int)((float)n * inv);
@@ -80,7 +80,15 @@ __global__ __launch_bounds__(256) void wgrad3x3_kernel(WgradArgs a) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int ncb = a.cin / CB;
-    const int n0 = (blockIdx.y / ncb) * NB, c0 = (blockIdx.y % ncb) * CB;
+    const int ngroups = (a.cout / NB) * ncb;
+    // XCD-aware (slice, group) mapping: the groups of one slice read the same dy / x rows, so
+    // give them consecutive dispatch slots of the same XCD (blocks f and f+8 share an XCD).
+    const int f = blockIdx.x;
+    const int kk = f >> 3;
+    const int group = kk % ngroups;
+    const int slice = (kk / ngroups) * 8 + (f & 7);
+    if (slice >= a.nslice) return;
+    const int n0 = (group / ncb) * NB, c0 = (group % ncb) * CB;
     const int li = (MT == 32) ? (lane & 31) : (lane & 15);
     const int kg = (MT == 32) ? (lane >> 5) : (lane >> 4);
 
@@ -99,7 +107,7 @@ __global__ __launch_bounds__(256) void wgrad3x3_kernel(WgradArgs a) {
 
     const float invP = 1.f / P, invCW = 1.f / a.CW, invXR = 1.f / XR, invXS = 1.f / XS;
     const int ndy = NB * P, nx = CB * XR;
-    const int ch0 = blockIdx.x * a.per_slice;
+    const int ch0 = slice * a.per_slice;
     const int ch1 = min(a.nchunks, ch0 + a.per_slice);
     for (int chunk = ch0; chunk < ch1; ++chunk) {
         const int seg = chunk % a.nseg;
@@ -168,7 +176,7 @@ __global__ __launch_bounds__(256) void wgrad3x3_kernel(WgradArgs a) {
             if (w >= a.CW) { w = 0; ++r; }
         }
     }
-    float* out = a.part + (int64_t)blockIdx.x * a.cout * a.cin * 9;
+    float* out = a.part + (int64_t)slice * a.cout * a.cin * 9;
 #pragma unroll
     for (int k = 0; k < PW; ++k)
 #pragma unroll
@@ -195,22 +203,15 @@ void wgrad3x3_geometry(int B, int H, int W, int cin, int cout, WgradArgs* a) {
     a->MT = MT; a->NPM = NPM; a->NPC = NPC;
     const int NB = NPM * MT, CB = NPC * MT;
     const int KS = MT == 32 ? 2 : 4;
-    // chunk shape: minimise staged elements over the whole problem within ~76 KB of LDS
+    // chunk shape: whole rows (DRAM bursts stay >= 128 B; the halo rows of consecutive chunks of a
+    // slice are L2 hits), columns split only for very wide rows; as many rows as fit ~76 KB of LDS.
     const size_t lds_cap = 76 * 1024;
-    int bestR = 1, bestCW = KS;
-    double best = 1e300;
-    const int wmax = (W + 3) / 4 * 4;
-    for (int cw = 4; cw <= std::max(4, std::min(wmax, 128)); cw += 4) {
-        for (int R = 1; R <= std::min(H, 16); ++R) {
-            int P = R * cw;
-            size_t lds = ((size_t)NB * (P + 1) + (size_t)CB * ((R + 2) * (cw + 2) + 1)) * 4;
-            if (lds > lds_cap || P > 512) continue;
-            double nch = (double)((W + cw - 1) / cw) * ((H + R - 1) / R);
-            double staged = nch * ((double)NB * P + (double)CB * (R + 2) * (cw + 2));
-            double compute = nch * P * 0.5 * NB * CB / 64.0;  // position-MACs incl. padding waste
-            double cost = staged * 4.0 + compute;
-            if (cost < best) { best = cost; bestR = R; bestCW = cw; }
-        }
+    int nseg = (W + 127) / 128;
+    int bestCW = ((W + nseg - 1) / nseg + 3) / 4 * 4;
+    int bestR = 1;
+    for (int R = 1; R <= std::min(H, 16); ++R) {
+        size_t lds = ((size_t)NB * (R * bestCW + 1) + (size_t)CB * ((R + 2) * (bestCW + 2) + 1)) * 4;
+        if (lds <= lds_cap && R * bestCW <= 512) bestR = R;
     }
     a->R = bestR;
     a->CW = bestCW;
@@ -219,7 +220,7 @@ void wgrad3x3_geometry(int B, int H, int W, int cin, int cout, WgradArgs* a) {
     a->nrb = ceil_div(H, a->R);
     a->nchunks = B * a->nrb * a->nseg;
     const int ngroups = (cout / NB) * (cin / CB);
-    int want = std::max(1, 1024 / ngroups);
+    int want = std::max(8, 1024 / ngroups);
     want = std::min(want, a->nchunks);
     a->per_slice = ceil_div(a->nchunks, want);
     a->nslice = ceil_div(a->nchunks, a->per_slice);
@@ -235,7 +236,7 @@ int launch_wgrad3x3(int pro, WgradArgs a, hipStream_t s) {
     const int P = a.R * a.CW;
     size_t smem = ((size_t)NB * (P + 1) + (size_t)CB * ((a.R + 2) * (a.CW + 2) + 1)) * sizeof(float);
     PCX_CHECK_ARG(smem <= 160 * 1024, "wgrad3x3: LDS %zu too large", smem);
-    dim3 grid(a.nslice, (a.cout / NB) * (a.cin / CB));
+    dim3 grid((unsigned)(((a.nslice + 7) / 8) * 8 * ((a.cout / NB) * (a.cin / CB))));
 #define PCX_WG(MT_, PW_, P_)                                                                     \
     if (a.MT == MT_ && pw == PW_ && pro == P_) {                                                \
         (void)hipFuncSetAttribute((const void*)wgrad3x3_kernel<MT_, PW_, P_>,                   \
