@@ -15,7 +15,7 @@
 // channels), B = input pixels (N = 32 consecutive flattened pixels per lane group), so each
 // accumulator register holds one channel for 32 consecutive pixels and the output stores are
 // 128-byte coalesced rows of a channel plane.
-#include "kernels.h"
+#include "conv_epilogue.h"
 
 namespace pcx {
 namespace {
@@ -36,14 +36,6 @@ __device__ __forceinline__ int xcd_remap(int orig, int nb) {
     // range of tiles so neighbouring tiles (which share halo rows) hit the same L2.  Bijective.
     int q = nb >> 3, r = nb & 7, x = orig & 7;
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (orig >> 3);
-}
-
-__device__ __forceinline__ float lanebcast(float v, int src) { return __shfl(v, src, 64); }
-
-__device__ __forceinline__ float sum32(float v) {  // reduce within each 32-lane half
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
 }
 
 // ------------------------------------------------------------------ prologue (staging)
@@ -245,119 +237,7 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvArgs a) {
 
     // ------------------------------------------------------------------ epilogues
     __syncthreads();  // LDS is reused for the cross-wave statistics below
-    float* red = smem;
-    const int cnt_w = (int)max((int64_t)0, min((int64_t)WN * 32, Mtot - (m0 + wave * WN * 32)));
-    if (EPI == EPI_FWD) {
-#pragma unroll
-        for (int mi = 0; mi < WM; ++mi)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int chl = mi * 32 + acc_row(r, h);
-                const int ch = n0 + chl;
-                float K = lanebcast(acc[mi][0][r], h * 32);
-                float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-                for (int ni = 0; ni < WN; ++ni) {
-                    float v = acc[mi][ni][r];
-                    if (valid[ni]) {
-                        a.out[((int64_t)pb[ni] * a.cout + ch) * HW + pp[ni]] = v;
-                        float d = v - K;
-                        s1 += d;
-                        s2 = fmaf(d, d, s2);
-                    }
-                }
-                s1 = sum32(s1);
-                s2 = sum32(s2);
-                if (l32 == 0) {
-                    float n = (float)cnt_w;
-                    float mean = cnt_w ? K + s1 / n : 0.f;
-                    float m2 = cnt_w ? fmaxf(s2 - s1 * s1 / n, 0.f) : 0.f;
-                    float* d = red + (wave * COUT_T + chl) * 3;
-                    d[0] = n; d[1] = mean; d[2] = m2;
-                }
-            }
-        __syncthreads();
-        if (tid < COUT_T) {
-            float n = 0.f, mean = 0.f, m2 = 0.f;
-#pragma unroll
-            for (int w = 0; w < 4; ++w) {
-                const float* d = red + (w * COUT_T + tid) * 3;
-                if (d[0] > 0.f) {
-                    float nt = n + d[0];
-                    float delta = d[1] - mean;
-                    mean += delta * d[0] / nt;
-                    m2 += d[2] + delta * delta * n * d[0] / nt;
-                    n = nt;
-                }
-            }
-            a.part0[(int64_t)(n0 + tid) * a.nblk + tile] = n * mean;
-            a.part1[(int64_t)(n0 + tid) * a.nblk + tile] = m2;
-            if (tid == 0 && n0 == 0) a.partn[tile] = n;
-        }
-    } else {
-        // backward epilogues: sums of dz and dz*xhat per channel
-#pragma unroll
-        for (int mi = 0; mi < WM; ++mi)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int chl = mi * 32 + acc_row(r, h);
-                const int ch = n0 + chl;
-                const float4 cf = a.cf_out[ch];
-                float sdz = 0.f, sdx = 0.f;
-#pragma unroll
-                for (int ni = 0; ni < WN; ++ni) {
-                    if (!valid[ni]) continue;
-                    const float g = acc[mi][ni][r];
-                    if (EPI == EPI_BWD_RELU) {
-                        int64_t o = ((int64_t)pb[ni] * a.cout + ch) * HW + pp[ni];
-                        float y = a.yprev[o];
-                        float dz = (fmaf(y, cf.x, cf.y) > 0.f) ? g : 0.f;
-                        a.out[o] = dz;
-                        sdz += dz;
-                        sdx = fmaf(dz, (y - cf.z) * cf.w, sdx);
-                    } else {  // EPI_BWD_POOL
-                        const int hp = pp[ni] / a.W, wp = pp[ni] - hp * a.W;
-                        float gd = a.drop_out ? g * a.drop_out[(int64_t)pb[ni] * a.cout + ch] : g;
-                        int64_t o = ((int64_t)pb[ni] * a.cout + ch) * a.Hs * a.Ws +
-                                    (int64_t)(2 * hp) * a.Ws + 2 * wp;
-                        float y0 = a.yprev[o], y1 = a.yprev[o + 1];
-                        float y2 = a.yprev[o + a.Ws], y3 = a.yprev[o + a.Ws + 1];
-                        float r0 = fmaxf(fmaf(y0, cf.x, cf.y), 0.f), r1 = fmaxf(fmaf(y1, cf.x, cf.y), 0.f);
-                        float r2 = fmaxf(fmaf(y2, cf.x, cf.y), 0.f), r3 = fmaxf(fmaf(y3, cf.x, cf.y), 0.f);
-                        // first maximum in window scan order, as torch's max_pool2d
-                        int arg = 0;
-                        float best = r0, ya = y0;
-                        if (r1 > best) { best = r1; arg = 1; ya = y1; }
-                        if (r2 > best) { best = r2; arg = 2; ya = y2; }
-                        if (r3 > best) { best = r3; arg = 3; ya = y3; }
-                        float d = best > 0.f ? gd : 0.f;
-                        a.out[o] = arg == 0 ? d : 0.f;
-                        a.out[o + 1] = arg == 1 ? d : 0.f;
-                        a.out[o + a.Ws] = arg == 2 ? d : 0.f;
-                        a.out[o + a.Ws + 1] = arg == 3 ? d : 0.f;
-                        sdz += d;
-                        sdx = fmaf(d, (ya - cf.z) * cf.w, sdx);
-                    }
-                }
-                sdz = sum32(sdz);
-                sdx = sum32(sdx);
-                if (l32 == 0) {
-                    float* d = red + (wave * COUT_T + chl) * 2;
-                    d[0] = sdz; d[1] = sdx;
-                }
-            }
-        __syncthreads();
-        if (tid < COUT_T) {
-            float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-            for (int w = 0; w < 4; ++w) {
-                s0 += red[(w * COUT_T + tid) * 2];
-                s1 += red[(w * COUT_T + tid) * 2 + 1];
-            }
-            a.part0[(int64_t)(n0 + tid) * a.nblk + tile] = s0;
-            a.part1[(int64_t)(n0 + tid) * a.nblk + tile] = s1;
-        }
-    }
+    conv_epilogue<WM, WN, EPI>(a, acc, smem, tile, n0, m0, Mtot, HW, wave, tid, valid, pb, pp);
 }
 
 template <int WM, int WN>

@@ -1,0 +1,318 @@
+// 3x3 / stride 1 / pad 1 conv (forward and data gradient) with asynchronous LDS-DMA staging.
+//
+// Same implicit GEMM and epilogues as conv.hip, different operand path (MI355X-first):
+//  * the raw input rows of a K-chunk (CK channels x NR staged rows, dense [c][row][W] image) and
+//    the weight chunk are copied HBM/L2 -> LDS by global_load_lds (dwordx4 when rows are 16-byte
+//    aligned, dword otherwise) into one of two buffers; chunk k+1 is in flight while the MFMAs of
+//    chunk k run, so staging latency is hidden and costs no VGPRs;
+//  * the prologue (BN+ReLU of the producer, or the BN backward (dz, y) -> dy for the data
+//    gradient) is applied when a B operand is read from LDS, together with the zero-padding /
+//    sample-boundary mask of its tap (3-5 VALU per operand, under the 64-cycle MFMA shadow);
+//  * one barrier per chunk; all per-chunk tables live in the single dynamic LDS array (no second
+//    __shared__ object, so hipcc does not drain the DMA queue before LDS reads).
+#include "conv_epilogue.h"
+
+namespace pcx {
+namespace {
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ int fdiv(int n, int d, float inv) {  // n / d, 0 <= n < 2^22
+    int q = (int)((float)n * inv);
+    int r = n - q * d;
+    if (r < 0) --q;
+    else if (r >= d) ++q;
+    return q;
+}
+
+__device__ __forceinline__ int xcd_remap(int orig, int nb) {
+    int q = nb >> 3, r = nb & 7, x = orig & 7;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (orig >> 3);
+}
+
+// global -> LDS DMA of VEC floats per lane; LDS destination = wave-uniform base + lane * VEC.
+// Issued through inline asm: the builtin makes the waitcnt pass put a vmcnt(0) in front of every
+// later ds_read (it cannot tell the DMA target from the buffer being read), which serialises the
+// double buffer.  Completion is ordered explicitly by the vmcnt(0) + barrier at each chunk start.
+template <int VEC>
+__device__ __forceinline__ void dma(const float* g, unsigned lds_byte_addr) {
+    const unsigned m0 = __builtin_amdgcn_readfirstlane(lds_byte_addr);
+    if constexpr (VEC == 4)
+        asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" :: "v"(g), "{m0}"(m0) : "memory");
+    else
+        asm volatile("s_nop 0\n\tglobal_load_lds_dword %0, off" :: "v"(g), "{m0}"(m0) : "memory");
+}
+
+
+// raw image of one K-chunk: NSRC tensors x CK channels x NR staged rows x W columns (dense)
+template <int VEC, int NSRC>
+__device__ __forceinline__ void issue_raw(const ConvArgs& a, const int2* rinfo, unsigned raw, int c0,
+                                          int wave, int lane, int total, int CK, float invPL,
+                                          float invW) {
+    const int PL = a.NR * a.W;  // floats per channel plane of the image
+    for (int base = wave * 64 * VEC; base < total; base += 4 * 64 * VEC) {
+        const int f = min(base + lane * VEC, total - VEC);
+        const int src = (NSRC == 2) ? (f >= CK * PL ? 1 : 0) : 0;
+        const int ff = f - src * CK * PL;
+        const int cl = fdiv(ff, PL, invPL);
+        const int rem = ff - cl * PL;
+        const int lr = fdiv(rem, a.W, invW);
+        const int w = rem - lr * a.W;
+        const int2 ri = rinfo[lr];
+        const int b = ri.x < 0 ? 0 : ri.x;
+        const float* t = (src == 0) ? a.src : a.src2;
+        const float* g = t + ((((int64_t)b * a.cin + c0 + cl) * a.H + ri.y) * a.W + w);
+        dma<VEC>(g, raw + 4u * base);
+    }
+}
+
+template <int WM>
+__device__ __forceinline__ void issue_wts(const ConvArgs& a, unsigned wts, int c0, int n0, int wave,
+                                          int lane, int CK) {
+    constexpr int COUT_T = 32 * WM;
+    const int total = 9 * CK * COUT_T;
+    for (int base = wave * 256; base < total; base += 4 * 256) {
+        const int f = min(base + lane * 4, total - 4);
+        const int row = f / COUT_T, col = f - row * COUT_T;
+        const int tap = row / CK, cc = row - tap * CK;
+        dma<4>(a.wpack + ((int64_t)(tap * a.cin + c0 + cc)) * a.cout + n0 + col, wts + 4u * base);
+    }
+}
+
+template <int WM, int WN, int VEC, int PRO, int EPI, int CK>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv3x3_dma_kernel(ConvArgs a) {
+    constexpr int COUT_T = 32 * WM;
+    constexpr int BP = 4 * WN * 32;
+    constexpr int NSRC = (PRO == PRO_BNBWD) ? 2 : 1;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int PL = a.NR * a.W;
+    const int rawf = ((NSRC * CK * PL + 64 * VEC - 1) / (64 * VEC)) * (64 * VEC);
+    const int wtsf = ((9 * CK * COUT_T + 255) / 256) * 256;
+    float4* cft = reinterpret_cast<float4*>(smem);                        // [cin]
+    int2* rinfo = reinterpret_cast<int2*>(smem + 4 * a.cin);              // [NR] (padded to 4)
+    float* raw0 = smem + 4 * a.cin + ((2 * a.NR + 3) & ~3);
+    float* wts0 = raw0 + 2 * rawf;
+    // LDS byte addresses of the DMA targets (M0 operand)
+    const unsigned lds0 = (unsigned)(uintptr_t)(lds_void*)smem;
+    const unsigned raw_lds = lds0 + 4u * (unsigned)(raw0 - smem);
+    const unsigned wts_lds = lds0 + 4u * (unsigned)(wts0 - smem);
+
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int ny = a.cout / COUT_T;
+    const int flat = xcd_remap(blockIdx.x, gridDim.x);
+    const int tile = flat / ny;
+    const int n0 = (flat - tile * ny) * COUT_T;
+    const int64_t HW = (int64_t)a.H * a.W;
+    const int64_t Mtot = (int64_t)a.B * HW;
+    const int64_t m0 = (int64_t)tile * BP;
+    const int64_t row0 = m0 / a.W - 1;
+    const int64_t nrows = (int64_t)a.B * a.H;
+
+    // ---- per-block tables (ordinary loads, all consumed before the first DMA is issued)
+    if (PRO != PRO_RAW)
+        for (int c = tid; c < a.cin; c += 256) cft[c] = a.cf_in[c];
+    for (int lr = tid; lr < a.NR; lr += 256) {
+        int64_t gr = row0 + lr;
+        bool ok = gr >= 0 && gr < nrows;
+        int b = ok ? (int)(gr / a.H) : -1;
+        rinfo[lr] = make_int2(b, ok ? (int)(gr - (int64_t)b * a.H) : 0);
+    }
+    int pixoff[WN];
+    bool vup[WN], vdn[WN], vl[WN], vr[WN], valid[WN];
+    int pb[WN], pp[WN];
+#pragma unroll
+    for (int ni = 0; ni < WN; ++ni) {
+        int64_t m = m0 + (wave * WN + ni) * 32 + l32;
+        valid[ni] = m < Mtot;
+        int64_t mm = valid[ni] ? m : Mtot - 1;
+        int64_t gr = mm / a.W;
+        int w = (int)(mm - gr * a.W);
+        int b = (int)(gr / a.H);
+        int hr = (int)(gr - (int64_t)b * a.H);
+        pixoff[ni] = (int)(gr - row0) * a.W + w;
+        vup[ni] = hr > 0;
+        vdn[ni] = hr < a.H - 1;
+        vl[ni] = w > 0;
+        vr[ni] = w < a.W - 1;
+        pb[ni] = b;
+        pp[ni] = hr * a.W + w;
+    }
+    __syncthreads();
+
+    f32x16 acc[WM][WN];
+#pragma unroll
+    for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < WN; ++ni) acc[mi][ni] = f32x16{0.f};
+
+    const int rawtotal = NSRC * CK * PL;
+    const float invPL = 1.f / PL, invW = 1.f / a.W;
+    const int nchunk = a.cin / CK;
+    issue_raw<VEC, NSRC>(a, rinfo, raw_lds, 0, wave, lane, rawtotal, CK, invPL, invW);
+    issue_wts<WM>(a, wts_lds, 0, n0, wave, lane, CK);
+    for (int k = 0; k < nchunk; ++k) {
+        const int c0 = k * CK;
+        float* raw = raw0 + (k & 1) * rawf;
+        float* wts = wts0 + (k & 1) * wtsf;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // chunk k visible to all waves; chunk k-1 fully consumed
+        if (k + 1 < nchunk) {
+            const unsigned nb = (unsigned)((k + 1) & 1);
+            issue_raw<VEC, NSRC>(a, rinfo, raw_lds + nb * 4u * rawf, c0 + CK, wave, lane, rawtotal,
+                                 CK, invPL, invW);
+            issue_wts<WM>(a, wts_lds + nb * 4u * wtsf, c0 + CK, n0, wave, lane, CK);
+        }
+        float4 cf[CK / 2];
+        if (PRO != PRO_RAW) {
+#pragma unroll
+            for (int s = 0; s < CK / 2; ++s) cf[s] = cft[c0 + 2 * s + h];
+        }
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            const int dh = tap / 3 - 1, dw = tap % 3 - 1;
+            const int toff = dh * a.W + dw;
+#pragma unroll
+            for (int s = 0; s < CK / 2; ++s) {
+                float av[WM], bv[WN];
+#pragma unroll
+                for (int mi = 0; mi < WM; ++mi)
+                    av[mi] = wts[(tap * CK + 2 * s + h) * COUT_T + mi * 32 + l32];
+#pragma unroll
+                for (int ni = 0; ni < WN; ++ni) {
+                    const int o = (2 * s + h) * PL + pixoff[ni] + toff;
+                    float v;
+                    if (PRO == PRO_RAW) {
+                        v = raw[o];
+                    } else if (PRO == PRO_BNRELU) {
+                        v = fmaxf(fmaf(raw[o], cf[s].x, cf[s].y), 0.f);
+                    } else {  // PRO_BNBWD: dy = a * (dz - mb - (y - mean) * mgi)
+                        v = cf[s].x * (raw[o] - cf[s].y - (raw[o + CK * PL] - cf[s].w) * cf[s].z);
+                    }
+                    bool ok = true;
+                    if (dh < 0) ok = ok && vup[ni];
+                    if (dh > 0) ok = ok && vdn[ni];
+                    if (dw < 0) ok = ok && vl[ni];
+                    if (dw > 0) ok = ok && vr[ni];
+                    bv[ni] = ok ? v : 0.f;
+                }
+#pragma unroll
+                for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+                    for (int ni = 0; ni < WN; ++ni) acc[mi][ni] = mfma32(av[mi], bv[ni], acc[mi][ni]);
+            }
+        }
+    }
+    __syncthreads();  // LDS is reused for the cross-wave statistics
+    conv_epilogue<WM, WN, EPI>(a, acc, smem, tile, n0, m0, Mtot, HW, wave, tid, valid, pb, pp);
+}
+
+// ------------------------------------------------------------------ BN + ReLU + MaxPool2 + Dropout2d
+// x[b,c,h,w] = drop[b,c] * max_{2x2} relu(y*s + t)  (reference block tail phoneme_cnn.py:40-43)
+__global__ __launch_bounds__(256) void bn_relu_pool_kernel(const float* __restrict__ y, const float4* __restrict__ cf,
+                                                           const float* __restrict__ drop, float* __restrict__ x,
+                                                           int B, int C, int Hs, int Ws, int Hp, int Wp) {
+    const int64_t nq = (int64_t)B * C * Hp * ((Wp + 3) / 4);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int Wq = (Wp + 3) / 4;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nq; e += stride) {
+        const int q = (int)(e % Wq);
+        const int64_t r = e / Wq;           // (b*C + c)*Hp + h
+        const int hp = (int)(r % Hp);
+        const int64_t bc = r / Hp;
+        const int c = (int)(bc % C);
+        const float4 k = cf[c];
+        const float d = drop ? drop[bc] : 1.f;
+        const float* s0 = y + (bc * Hs + 2 * hp) * Ws;
+        const float* s1 = s0 + Ws;
+        float out[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int w = 4 * q + j;
+            if (w < Wp) {
+                float m = fmaxf(fmaxf(fmaf(s0[2 * w], k.x, k.y), fmaf(s0[2 * w + 1], k.x, k.y)),
+                                fmaxf(fmaf(s1[2 * w], k.x, k.y), fmaf(s1[2 * w + 1], k.x, k.y)));
+                out[j] = d * fmaxf(m, 0.f);
+            }
+        }
+        float* dst = x + r * Wp + 4 * q;
+        if ((Wp & 3) == 0) {
+            st4(dst, make_float4(out[0], out[1], out[2], out[3]));
+        } else {
+            for (int j = 0; j < 4 && 4 * q + j < Wp; ++j) dst[j] = out[j];
+        }
+    }
+}
+
+}  // namespace
+
+int conv3x3_dma_ck(int pro, int cout, int W, int NR, int cin) {
+    // largest K-chunk whose double-buffered raw image + weights fit ~76 KB (2 blocks per CU)
+    const int nsrc = pro == PRO_BNBWD ? 2 : 1;
+    const int cout_t = cout == 32 ? 32 : 64;
+    for (int ck = 8; ck >= 2; ck >>= 1) {
+        if (cin % ck) continue;
+        size_t raw = (size_t)nsrc * ck * NR * W + 256;
+        size_t wts = (size_t)9 * ck * cout_t + 256;
+        size_t bytes = (2 * raw + 2 * wts + 4 * (size_t)cin + 2 * NR + 8) * 4;
+        if (bytes <= 76 * 1024) return ck;
+    }
+    return 2;
+}
+
+int launch_conv3x3_dma(int pro, int epi, ConvArgs a, hipStream_t s) {
+    PCX_CHECK_ARG(a.cout == 32 || a.cout % 64 == 0, "conv3x3: cout %d unsupported", a.cout);
+    PCX_CHECK_ARG(pro == PRO_RAW || pro == PRO_BNRELU || pro == PRO_BNBWD, "conv3x3_dma: prologue %d", pro);
+    const int wm = a.cout == 32 ? 1 : 2, wn = a.cout == 32 ? 4 : 2;
+    const int bp = 4 * wn * 32, cout_t = 32 * wm;
+    const int64_t M = (int64_t)a.B * a.H * a.W;
+    const int ntile = ceil_div(M, bp);
+    PCX_CHECK_ARG(a.nblk == ntile, "conv3x3: partial buffer sized for %d tiles, need %d", a.nblk, ntile);
+    a.NR = (bp - 1 + a.W - 1) / a.W + 1 + 2;
+    const int ck = conv3x3_dma_ck(pro, a.cout, a.W, a.NR, a.cin);
+    PCX_CHECK_ARG(a.cin % ck == 0, "conv3x3: cin %d not a multiple of %d", a.cin, ck);
+    const int vec = (a.W % 4 == 0) ? 4 : 1;
+    const int nsrc = pro == PRO_BNBWD ? 2 : 1;
+    const int PL = a.NR * a.W;
+    const int rawf = ((nsrc * ck * PL + 64 * vec - 1) / (64 * vec)) * (64 * vec);
+    const int wtsf = ((9 * ck * cout_t + 255) / 256) * 256;
+    size_t smem = ((size_t)4 * a.cin + ((2 * a.NR + 3) & ~3) + 2 * (size_t)rawf + 2 * (size_t)wtsf) * 4;
+    size_t red = (size_t)4 * cout_t * 3 * 4;
+    if (smem < red) smem = red;
+    PCX_CHECK_ARG(smem <= 160 * 1024, "conv3x3_dma: W=%d needs %zu B of LDS", a.W, smem);
+    dim3 grid((unsigned)(ntile * (a.cout / cout_t)));
+#define PCX_DMA_CASE(WM_, WN_, V_, P_, E_, CK_)                                                   \
+    if (wm == WM_ && vec == V_ && pro == P_ && epi == E_ && ck == CK_) {                         \
+        (void)hipFuncSetAttribute((const void*)conv3x3_dma_kernel<WM_, WN_, V_, P_, E_, CK_>,    \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);        \
+        conv3x3_dma_kernel<WM_, WN_, V_, P_, E_, CK_><<<grid, 256, smem, s>>>(a);                \
+        PCX_LAUNCH_CHECK("conv3x3_dma_kernel");                                                  \
+        return PCX_OK;                                                                           \
+    }
+#define PCX_DMA_CK(WM_, WN_, V_, P_, E_) \
+    PCX_DMA_CASE(WM_, WN_, V_, P_, E_, 8) PCX_DMA_CASE(WM_, WN_, V_, P_, E_, 4) PCX_DMA_CASE(WM_, WN_, V_, P_, E_, 2)
+#define PCX_DMA_V(WM_, WN_, P_, E_) PCX_DMA_CK(WM_, WN_, 4, P_, E_) PCX_DMA_CK(WM_, WN_, 1, P_, E_)
+#define PCX_DMA_ALL(P_, E_) PCX_DMA_V(1, 4, P_, E_) PCX_DMA_V(2, 2, P_, E_)
+    PCX_DMA_ALL(PRO_RAW, EPI_FWD)
+    PCX_DMA_ALL(PRO_BNRELU, EPI_FWD)
+    PCX_DMA_ALL(PRO_BNBWD, EPI_BWD_RELU)
+    PCX_DMA_ALL(PRO_BNBWD, EPI_BWD_POOL)
+#undef PCX_DMA_ALL
+#undef PCX_DMA_V
+#undef PCX_DMA_CK
+#undef PCX_DMA_CASE
+    set_error("conv3x3_dma: unsupported combination (pro %d epi %d ck %d vec %d)", pro, epi, ck, vec);
+    return PCX_EINVAL;
+}
+
+int launch_bn_relu_pool(const float* y, const float4* cf, const float* drop, float* x, int B, int C,
+                        int Hs, int Ws, hipStream_t s) {
+    const int Hp = Hs / 2, Wp = Ws / 2;
+    const int64_t nq = (int64_t)B * C * Hp * ((Wp + 3) / 4);
+    const int blocks = (int)std::min<int64_t>(8192, std::max<int64_t>(1, (nq + 255) / 256));
+    bn_relu_pool_kernel<<<blocks, 256, 0, s>>>(y, cf, drop, x, B, C, Hs, Ws, Hp, Wp);
+    PCX_LAUNCH_CHECK("bn_relu_pool_kernel");
+    return PCX_OK;
+}
+
+}  // namespace pcx

@@ -1,0 +1,558 @@
+// General convolution (any cin/cout, KxK, stride 1 or 2, zero pad) as an implicit GEMM on
+// v_mfma_f32_32x32x2_f32, plus the elementwise / per-channel-statistics kernels of the residual
+// network (reference src/models/phoneme_cnn.py:146-304, PhonemeNetDeep + ResidualBlock).
+//
+//  mode 0  forward     y[b,n,oh,ow]   = sum_{c,kh,kw} W[n,c,kh,kw] x[b,c,oh*s-p+kh,ow*s-p+kw]
+//                      GEMM  M = cout, N = B*OH*OW, K = cin*KH*KW
+//  mode 1  data grad   dx[b,c,ih,iw]  = sum_{n,kh,kw} W[n,c,kh,kw] dy[b,n,(ih+p-kh)/s,(iw+p-kw)/s]
+//                      (only taps where the division is exact and in range)
+//                      GEMM  M = cin,  N = B*IH*IW, K = cout*KH*KW
+//  mode 2  weight grad dW[n,c,kh,kw]  = sum_{b,oh,ow} dy[b,n,oh,ow] x[b,c,oh*s-p+kh,ow*s-p+kw]
+//                      GEMM  M = cout, N = cin*KH*KW, K = B*OH*OW split into slices (partials)
+//
+// Block = 4 waves in 2x2, each wave (32*WM) x (32*WN) of accumulators; K advances in chunks of 16
+// staged through double-buffered LDS with the next chunk's global gathers in flight during the
+// current chunk's MFMAs (one barrier per chunk).  Operands are gathered straight from the NCHW
+// tensors (no im2col buffer).  Every output element is written by exactly one lane (no atomics):
+// results are deterministic.
+#include "kernels.h"
+
+namespace pcx {
+namespace {
+
+constexpr int KC = 16;
+
+template <int MODE, int KH, int KW, int WM, int WN>
+__global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
+    constexpr int KK = KH * KW;
+    constexpr int BM = 64 * WM, BN = 64 * WN;
+    constexpr int SA = BM + 4, SB = BN + 4;
+    constexpr int NA = BM / 16, NBv = BN / 16;  // staged elements per thread per chunk
+    __shared__ float As[2][KC][SA];
+    __shared__ float Bs[2][KC][SB];
+
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+    const int wave = tid >> 6, wr = wave >> 1, wc = wave & 1;
+    const int64_t OHW = (int64_t)a.OH * a.OW, IHW = (int64_t)a.IH * a.IW;
+    const int s = a.stride, pad = a.pad;
+
+    int64_t M, N, K;
+    if (MODE == 0) { M = a.cout; N = a.B * OHW; K = (int64_t)a.cin * KK; }
+    else if (MODE == 1) { M = a.cin; N = a.B * IHW; K = (int64_t)a.cout * KK; }
+    else { M = a.cout; N = (int64_t)a.cin * KK; K = a.B * OHW; }
+    const int64_t mt = (M + BM - 1) / BM, nt = (N + BN - 1) / BN;
+    int64_t bid = blockIdx.x;
+    const int64_t tm = bid % mt;
+    bid /= mt;
+    const int64_t tn = bid % nt;
+    const int slice = (int)(bid / nt);
+    const int64_t m0 = tm * BM, n0 = tn * BN;
+    int64_t k_begin = 0, k_end = K;
+    if (MODE == 2) {
+        k_begin = (int64_t)slice * a.kslice;
+        k_end = min(K, k_begin + a.kslice);
+    }
+    const int nch = (int)((k_end - k_begin + KC - 1) / KC);
+
+    // ---- per-thread staging state
+    const int kq = tid & 15;       // k-fast mapping: k offset within the chunk
+    const int colq = tid >> 4;     // k-fast mapping: first column
+    // column-fast mapping (B of modes 0/1): fixed pixel per thread
+    const int bcol = tid % BN;
+    const int brow = tid / BN;     // first k row; rows advance by 256/BN
+    constexpr int BROWS = 256 / BN;
+    int64_t xbase = 0;             // mode 0: x + b*cin*IHW ; mode 1: dy + b*cout*OHW
+    int ih0 = 0, iw0 = 0;          // mode 0: oh*s-p, ow*s-p ; mode 1: ih+p, iw+p
+    bool bvalid = false;
+    if (MODE == 0 || MODE == 1) {
+        const int64_t m = n0 + bcol;
+        bvalid = m < N;
+        const int64_t mm = bvalid ? m : 0;
+        if (MODE == 0) {
+            const int64_t b = mm / OHW, p = mm - b * OHW;
+            const int oh = (int)(p / a.OW), ow = (int)(p - (int64_t)(p / a.OW) * a.OW);
+            xbase = b * a.cin * IHW;
+            ih0 = oh * s - pad;
+            iw0 = ow * s - pad;
+        } else {
+            const int64_t b = mm / IHW, p = mm - b * IHW;
+            const int ih = (int)(p / a.IW), iw = (int)(p - (int64_t)(p / a.IW) * a.IW);
+            xbase = b * a.cout * OHW;
+            ih0 = ih + pad;
+            iw0 = iw + pad;
+        }
+    }
+    // mode 2: pixel tracker of k = k_begin + chunk*KC + kq
+    int64_t pb = 0;
+    int poh = 0, pow_ = 0;
+    if (MODE == 2) {
+        const int64_t q = k_begin + kq;
+        pb = q / OHW;
+        const int64_t p = q - pb * OHW;
+        poh = (int)(p / a.OW);
+        pow_ = (int)(p - (int64_t)poh * a.OW);
+    }
+
+    float ra[NA], rb[NBv];
+    auto gather = [&](int chunk) {
+        const int64_t kbase = k_begin + (int64_t)chunk * KC;
+        if (MODE == 0) {
+            const int64_t k = kbase + kq;
+#pragma unroll
+            for (int j = 0; j < NA; ++j) {
+                const int64_t n = m0 + colq + 16 * j;
+                ra[j] = (n < M && k < K) ? a.w[n * K + k] : 0.f;
+            }
+#pragma unroll
+            for (int i = 0; i < NBv; ++i) {
+                const int64_t kb = kbase + brow + BROWS * i;
+                float v = 0.f;
+                if (bvalid && kb < K) {
+                    const int c = (int)(kb / KK), r = (int)(kb - (int64_t)(kb / KK) * KK);
+                    const int ih = ih0 + r / KW, iw = iw0 + r % KW;
+                    if (ih >= 0 && ih < a.IH && iw >= 0 && iw < a.IW)
+                        v = a.x[xbase + ((int64_t)c * a.IH + ih) * a.IW + iw];
+                }
+                rb[i] = v;
+            }
+        } else if (MODE == 1) {
+            const int64_t k = kbase + kq;
+            const int n = (int)(k / KK), r = (int)(k - (int64_t)(k / KK) * KK);
+#pragma unroll
+            for (int j = 0; j < NA; ++j) {
+                const int64_t c = m0 + colq + 16 * j;
+                ra[j] = (c < M && k < K) ? a.w[((int64_t)n * a.cin + c) * KK + r] : 0.f;
+            }
+#pragma unroll
+            for (int i = 0; i < NBv; ++i) {
+                const int64_t kb = kbase + brow + BROWS * i;
+                float v = 0.f;
+                if (bvalid && kb < K) {
+                    const int nn = (int)(kb / KK), rr = (int)(kb - (int64_t)(kb / KK) * KK);
+                    const int th = ih0 - rr / KW, tw = iw0 - rr % KW;
+                    if (th >= 0 && tw >= 0) {
+                        int oh = th, ow = tw;
+                        bool ok = true;
+                        if (s == 2) {
+                            ok = ((th | tw) & 1) == 0;
+                            oh = th >> 1;
+                            ow = tw >> 1;
+                        }
+                        if (ok && oh < a.OH && ow < a.OW)
+                            v = a.dy[xbase + ((int64_t)nn * a.OH + oh) * a.OW + ow];
+                    }
+                }
+                rb[i] = v;
+            }
+        } else {
+            const bool kval = (kbase + kq) < k_end;
+            const int64_t pofs = (int64_t)poh * a.OW + pow_;
+#pragma unroll
+            for (int j = 0; j < NA; ++j) {
+                const int64_t n = m0 + colq + 16 * j;
+                ra[j] = (kval && n < M) ? a.dy[(pb * a.cout + n) * OHW + pofs] : 0.f;
+            }
+#pragma unroll
+            for (int i = 0; i < NBv; ++i) {
+                const int64_t jj = n0 + colq + 16 * i;
+                float v = 0.f;
+                if (kval && jj < N) {
+                    const int c = (int)(jj / KK), r = (int)(jj - (int64_t)(jj / KK) * KK);
+                    const int ih = poh * s - pad + r / KW, iw = pow_ * s - pad + r % KW;
+                    if (ih >= 0 && ih < a.IH && iw >= 0 && iw < a.IW)
+                        v = a.x[((pb * a.cin + c) * a.IH + ih) * a.IW + iw];
+                }
+                rb[i] = v;
+            }
+            // advance the pixel tracker by KC
+            pow_ += KC;
+            while (pow_ >= a.OW) {
+                pow_ -= a.OW;
+                if (++poh == a.OH) { poh = 0; ++pb; }
+            }
+        }
+    };
+    auto stash = [&](int buf) {
+#pragma unroll
+        for (int j = 0; j < NA; ++j) As[buf][kq][colq + 16 * j] = ra[j];
+        if (MODE == 2) {
+#pragma unroll
+            for (int i = 0; i < NBv; ++i) Bs[buf][kq][colq + 16 * i] = rb[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < NBv; ++i) Bs[buf][brow + BROWS * i][bcol] = rb[i];
+        }
+    };
+
+    f32x16 acc[WM][WN];
+#pragma unroll
+    for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < WN; ++ni) acc[mi][ni] = f32x16{0.f};
+
+    if (nch > 0) {
+        gather(0);
+        stash(0);
+    }
+    __syncthreads();
+    for (int ch = 0; ch < nch; ++ch) {
+        const int buf = ch & 1;
+        if (ch + 1 < nch) gather(ch + 1);
+#pragma unroll
+        for (int ks = 0; ks < KC / 2; ++ks) {
+            float av[WM], bv[WN];
+#pragma unroll
+            for (int mi = 0; mi < WM; ++mi) av[mi] = As[buf][2 * ks + h][wr * 32 * WM + mi * 32 + l32];
+#pragma unroll
+            for (int ni = 0; ni < WN; ++ni) bv[ni] = Bs[buf][2 * ks + h][wc * 32 * WN + ni * 32 + l32];
+#pragma unroll
+            for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < WN; ++ni) acc[mi][ni] = mfma32(av[mi], bv[ni], acc[mi][ni]);
+        }
+        if (ch + 1 < nch) stash(buf ^ 1);
+        __syncthreads();
+    }
+
+    // ---- epilogue: row = M index, column = N index (32 consecutive columns per lane group)
+#pragma unroll
+    for (int ni = 0; ni < WN; ++ni) {
+        const int64_t col = n0 + wc * 32 * WN + ni * 32 + l32;
+        if (col >= N) continue;
+        int64_t obase;
+        int64_t ostride;  // distance between consecutive rows (M index)
+        if (MODE == 0) {
+            const int64_t b = col / OHW;
+            obase = b * a.cout * OHW + (col - b * OHW);
+            ostride = OHW;
+        } else if (MODE == 1) {
+            const int64_t b = col / IHW;
+            obase = b * a.cin * IHW + (col - b * IHW);
+            ostride = IHW;
+        } else {
+            obase = (int64_t)slice * M * N + col;
+            ostride = N;
+        }
+#pragma unroll
+        for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int64_t row = m0 + wr * 32 * WM + mi * 32 + acc_row(r, h);
+                if (row < M) {
+                    float* o = a.out + obase + row * ostride;
+                    if (MODE == 1 && a.accumulate) *o += acc[mi][ni][r];
+                    else *o = acc[mi][ni][r];
+                }
+            }
+    }
+}
+
+// ------------------------------------------------------------------ per-channel statistics
+__device__ __forceinline__ double block_sum(double v, double* red) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    __syncthreads();
+    if ((tid & 63) == 0) red[tid >> 6] = v;
+    __syncthreads();
+    return red[0] + red[1] + red[2] + red[3];
+}
+
+// Forward BN partials of y [B][C][P]: block (c, slice) -> (sum, M2 about the block mean, count),
+// accumulated in float64 about a shift (first element) — consumed by launch_bn_fwd_finalize.
+__global__ __launch_bounds__(256) void chan_stats_kernel(const float* __restrict__ y, int B, int C, int64_t P,
+                                                         int bps, float* part0, float* part1, float* partn) {
+    __shared__ double red[4];
+    const int c = blockIdx.x, sl = blockIdx.y, nsl = gridDim.y;
+    const int b0 = sl * bps, b1 = min(B, b0 + bps);
+    const double K = b0 < B ? (double)y[((int64_t)b0 * C + c) * P] : 0.0;
+    double s1 = 0.0, s2 = 0.0;
+    for (int b = b0; b < b1; ++b) {
+        const float* yc = y + ((int64_t)b * C + c) * P;
+        for (int64_t p = threadIdx.x; p < P; p += 256) {
+            const double d = (double)yc[p] - K;
+            s1 += d;
+            s2 += d * d;
+        }
+    }
+    s1 = block_sum(s1, red);
+    s2 = block_sum(s2, red);
+    if (threadIdx.x == 0) {
+        const double n = (double)(b1 > b0 ? b1 - b0 : 0) * (double)P;
+        part0[(int64_t)c * nsl + sl] = (float)(n * K + s1);
+        part1[(int64_t)c * nsl + sl] = n > 0 ? (float)fmax(s2 - s1 * s1 / n, 0.0) : 0.f;
+        if (c == 0) partn[sl] = (float)n;
+    }
+}
+
+// Backward BN partials: g = d (+ d2) masked, written to g; sums of g and g*xhat_k for up to two
+// BNs (the main-path BN and the shortcut BN of a residual block share the same upstream g).
+__global__ __launch_bounds__(256) void bwd_prep_kernel(BwdPrepArgs a) {
+    __shared__ double red[4];
+    const int c = blockIdx.x, sl = blockIdx.y, nsl = gridDim.y;
+    const int b0 = sl * a.bps, b1 = min(a.B, b0 + a.bps);
+    const float4 mc = a.mask_cf ? a.mask_cf[c] : make_float4(1.f, 0.f, 0.f, 1.f);
+    const float4 c1 = a.cf1 ? a.cf1[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 c2 = a.cf2 ? a.cf2[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    double sg = 0.0, sx1 = 0.0, sx2 = 0.0;
+    for (int b = b0; b < b1; ++b) {
+        const int64_t o = ((int64_t)b * a.C + c) * a.P;
+        const float dr = a.drop ? a.drop[(int64_t)b * a.C + c] : 1.f;
+        for (int64_t p = threadIdx.x; p < a.P; p += 256) {
+            float g = a.d[o + p];
+            if (a.d2) g += a.d2[o + p];
+            if (a.mask_mode == MASK_OUT) {
+                g = a.mask_src[o + p] > 0.f ? g : 0.f;
+            } else if (a.mask_mode == MASK_BN) {
+                g = fmaf(a.mask_src[o + p], mc.x, mc.y) > 0.f ? g * dr : 0.f;
+            }
+            a.g[o + p] = g;
+            sg += (double)g;
+            if (a.y1) sx1 += (double)g * (double)((a.y1[o + p] - c1.z) * c1.w);
+            if (a.y2) sx2 += (double)g * (double)((a.y2[o + p] - c2.z) * c2.w);
+        }
+    }
+    sg = block_sum(sg, red);
+    sx1 = block_sum(sx1, red);
+    sx2 = block_sum(sx2, red);
+    if (threadIdx.x == 0) {
+        a.p_g[(int64_t)c * nsl + sl] = (float)sg;
+        if (a.p_x1) a.p_x1[(int64_t)c * nsl + sl] = (float)sx1;
+        if (a.p_x2) a.p_x2[(int64_t)c * nsl + sl] = (float)sx2;
+    }
+}
+
+// ------------------------------------------------------------------ elementwise (row tiled)
+// rows = B*C planes of P elements; TP threads per row, 256/TP rows per block
+struct RowTile {
+    int64_t row;
+    int col0, step;
+};
+__device__ __forceinline__ RowTile row_tile(int TP) {
+    RowTile t;
+    t.row = (int64_t)blockIdx.x * (256 / TP) + threadIdx.x / TP;
+    t.col0 = threadIdx.x % TP;
+    t.step = TP;
+    return t;
+}
+
+// out = drop[b,c] * relu(y*s + t + res')   res' = res*rs + rt (rcf) | res | 0
+__global__ __launch_bounds__(256) void bn_act_kernel(const float* __restrict__ y, const float4* __restrict__ cf,
+                                                     const float* __restrict__ res, const float4* __restrict__ rcf,
+                                                     const float* __restrict__ drop, float* __restrict__ out,
+                                                     int64_t rows, int C, int64_t P, int TP) {
+    const RowTile t = row_tile(TP);
+    if (t.row >= rows) return;
+    const int c = (int)(t.row % C);
+    const float4 k = cf[c];
+    const float4 rk = rcf ? rcf[c] : make_float4(1.f, 0.f, 0.f, 0.f);
+    const float d = drop ? drop[t.row] : 1.f;
+    const int64_t o = t.row * P;
+    for (int64_t p = t.col0; p < P; p += t.step) {
+        float v = fmaf(y[o + p], k.x, k.y);
+        if (res) v += fmaf(res[o + p], rk.x, rk.y);
+        out[o + p] = d * fmaxf(v, 0.f);
+    }
+}
+
+// dy = a*(g - mb - (y - mean)*mgi)      (cf = {a, mb, mgi, mean})
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* g, const float* __restrict__ y,
+                                                           const float4* __restrict__ cf, float* dy,
+                                                           int64_t rows, int C, int64_t P, int TP) {
+    const RowTile t = row_tile(TP);
+    if (t.row >= rows) return;
+    const float4 k = cf[(int)(t.row % C)];
+    const int64_t o = t.row * P;
+    for (int64_t p = t.col0; p < P; p += t.step)
+        dy[o + p] = k.x * (g[o + p] - k.y - (y[o + p] - k.w) * k.z);
+}
+
+// MaxPool2d(3, stride 2, pad 1) of relu(BN(y))  (reference phoneme_cnn.py:211-216)
+__global__ __launch_bounds__(256) void maxpool3_fwd_kernel(const float* __restrict__ y, const float4* __restrict__ cf,
+                                                           float* __restrict__ out, int64_t rows, int C, int H,
+                                                           int W, int OH, int OW) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t n = rows * OH * OW;
+    if (e >= n) return;
+    const int64_t row = e / ((int64_t)OH * OW);
+    const int p = (int)(e - row * OH * OW);
+    const int oh = p / OW, ow = p % OW;
+    const float4 k = cf[(int)(row % C)];
+    const float* yp = y + row * H * W;
+    float m = -INFINITY;
+    for (int kh = 0; kh < 3; ++kh) {
+        const int ih = 2 * oh - 1 + kh;
+        if (ih < 0 || ih >= H) continue;
+        for (int kw = 0; kw < 3; ++kw) {
+            const int iw = 2 * ow - 1 + kw;
+            if (iw < 0 || iw >= W) continue;
+            m = fmaxf(m, fmaxf(fmaf(yp[ih * W + iw], k.x, k.y), 0.f));
+        }
+    }
+    out[e] = m;
+}
+
+// gradient of MaxPool(3,2,1)(relu(BN(y))) w.r.t. the BN output: each input position collects the
+// windows whose first maximum (row-major scan, torch's tie rule) it is, times the ReLU mask
+__global__ __launch_bounds__(256) void maxpool3_bwd_kernel(const float* __restrict__ y, const float4* __restrict__ cf,
+                                                           const float* __restrict__ dout, float* __restrict__ dz,
+                                                           int64_t rows, int C, int H, int W, int OH, int OW) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t n = rows * H * W;
+    if (e >= n) return;
+    const int64_t row = e / ((int64_t)H * W);
+    const int p = (int)(e - row * H * W);
+    const int ih = p / W, iw = p % W;
+    const float4 k = cf[(int)(row % C)];
+    const float* yp = y + row * H * W;
+    const float z = fmaf(yp[p], k.x, k.y);
+    float g = 0.f;
+    if (z > 0.f) {
+        const int oh_lo = max(0, ih / 2), oh_hi = min(OH - 1, (ih + 1) / 2);
+        const int ow_lo = max(0, iw / 2), ow_hi = min(OW - 1, (iw + 1) / 2);
+        for (int oh = oh_lo; oh <= oh_hi; ++oh)
+            for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+                // window rows 2oh-1..2oh+1 / cols 2ow-1..2ow+1 must contain (ih, iw)
+                if (ih < 2 * oh - 1 || ih > 2 * oh + 1 || iw < 2 * ow - 1 || iw > 2 * ow + 1) continue;
+                float m = -INFINITY;
+                int arg = -1;
+                for (int kh = 0; kh < 3; ++kh) {
+                    const int hh = 2 * oh - 1 + kh;
+                    if (hh < 0 || hh >= H) continue;
+                    for (int kw = 0; kw < 3; ++kw) {
+                        const int ww = 2 * ow - 1 + kw;
+                        if (ww < 0 || ww >= W) continue;
+                        const float v = fmaxf(fmaf(yp[hh * W + ww], k.x, k.y), 0.f);
+                        if (v > m) { m = v; arg = hh * W + ww; }
+                    }
+                }
+                if (arg == p) g += dout[row * OH * OW + oh * OW + ow];
+            }
+    }
+    dz[e] = g;
+}
+
+__global__ void fill_cf_kernel(float4* cf, int C, float4 v) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < C) cf[c] = v;
+}
+
+int row_threads(int64_t P) {
+    int tp = 32;
+    while (tp < 256 && tp < P) tp <<= 1;
+    return tp;
+}
+
+}  // namespace
+
+// ====================================================================== host launchers
+int convg_nslice(const ConvGArgs& a, int64_t* kslice) {
+    // weight-gradient split: enough (M-tile, N-tile, slice) blocks to fill the chip several times
+    const int64_t K = (int64_t)a.B * a.OH * a.OW;
+    const int wm = a.cout >= 128 ? 2 : 1;
+    const int64_t mt = ceil_div(a.cout, 64 * wm), nt = ceil_div((int64_t)a.cin * a.KH * a.KW, 128);
+    int64_t want = std::max<int64_t>(1, 2048 / (mt * nt));
+    int64_t ks = (K + want - 1) / want;
+    ks = std::max<int64_t>(ks, 256);
+    ks = (ks + KC - 1) / KC * KC;
+    *kslice = ks;
+    return (int)((K + ks - 1) / ks);
+}
+
+int launch_convg(ConvGArgs a, hipStream_t s) {
+    PCX_CHECK_ARG(a.stride == 1 || a.stride == 2, "convg: stride %d unsupported", a.stride);
+    PCX_CHECK_ARG(a.B > 0 && a.cin > 0 && a.cout > 0, "convg: empty tensor");
+    const int64_t IHW = (int64_t)a.IH * a.IW, OHW = (int64_t)a.OH * a.OW;
+    int64_t M, N;
+    if (a.mode == 0) { M = a.cout; N = a.B * OHW; }
+    else if (a.mode == 1) { M = a.cin; N = a.B * IHW; }
+    else { M = a.cout; N = (int64_t)a.cin * a.KH * a.KW; }
+    const int wm = M >= 128 ? 2 : 1, wn = 2;
+    const int64_t mt = ceil_div(M, 64 * wm), nt = ceil_div(N, 64 * wn);
+    const int64_t nblocks = mt * nt * (a.mode == 2 ? a.nslice : 1);
+    PCX_CHECK_ARG(nblocks < ((int64_t)1 << 31), "convg: grid too large");
+    if (a.mode == 2) PCX_CHECK_ARG(a.kslice % KC == 0 && a.nslice >= 1, "convg: bad weight-gradient split");
+    dim3 grid((unsigned)nblocks);
+#define PCX_CG(MODE_, KH_, WM_)                                                  \
+    if (a.mode == MODE_ && a.KH == KH_ && wm == WM_) {                           \
+        convg_kernel<MODE_, KH_, KH_, WM_, 2><<<grid, 256, 0, s>>>(a);           \
+        PCX_LAUNCH_CHECK("convg_kernel");                                        \
+        return PCX_OK;                                                           \
+    }
+#define PCX_CG_K(KH_) PCX_CG(0, KH_, 1) PCX_CG(0, KH_, 2) PCX_CG(1, KH_, 1) PCX_CG(1, KH_, 2) \
+                      PCX_CG(2, KH_, 1) PCX_CG(2, KH_, 2)
+    PCX_CHECK_ARG(a.KH == a.KW, "convg: square kernels only");
+    PCX_CG_K(1)
+    PCX_CG_K(3)
+    PCX_CG_K(7)
+#undef PCX_CG_K
+#undef PCX_CG
+    set_error("convg: kernel size %d unsupported", a.KH);
+    return PCX_EINVAL;
+}
+
+int chan_slices(int B, int C, int* bps) {
+    int want = std::max(1, std::min(B, 2048 / std::max(C, 1)));
+    *bps = ceil_div(B, want);
+    return ceil_div(B, *bps);
+}
+
+int launch_chan_stats(const float* y, int B, int C, int64_t P, float* part0, float* part1, float* partn,
+                      int* nslice, hipStream_t s) {
+    int bps;
+    const int ns = chan_slices(B, C, &bps);
+    *nslice = ns;
+    chan_stats_kernel<<<dim3(C, ns), 256, 0, s>>>(y, B, C, P, bps, part0, part1, partn);
+    PCX_LAUNCH_CHECK("chan_stats_kernel");
+    return PCX_OK;
+}
+
+int launch_bwd_prep(BwdPrepArgs a, int* nslice, hipStream_t s) {
+    const int ns = chan_slices(a.B, a.C, &a.bps);
+    *nslice = ns;
+    bwd_prep_kernel<<<dim3(a.C, ns), 256, 0, s>>>(a);
+    PCX_LAUNCH_CHECK("bwd_prep_kernel");
+    return PCX_OK;
+}
+
+int launch_bn_act(const float* y, const float4* cf, const float* res, const float4* rcf, const float* drop,
+                  float* out, int B, int C, int64_t P, hipStream_t s) {
+    const int tp = row_threads(P);
+    const int64_t rows = (int64_t)B * C;
+    bn_act_kernel<<<ceil_div(rows, 256 / tp), 256, 0, s>>>(y, cf, res, rcf, drop, out, rows, C, P, tp);
+    PCX_LAUNCH_CHECK("bn_act_kernel");
+    return PCX_OK;
+}
+
+int launch_bn_bwd_apply(const float* g, const float* y, const float4* cf, float* dy, int B, int C, int64_t P,
+                        hipStream_t s) {
+    const int tp = row_threads(P);
+    const int64_t rows = (int64_t)B * C;
+    bn_bwd_apply_kernel<<<ceil_div(rows, 256 / tp), 256, 0, s>>>(g, y, cf, dy, rows, C, P, tp);
+    PCX_LAUNCH_CHECK("bn_bwd_apply_kernel");
+    return PCX_OK;
+}
+
+int launch_maxpool3_fwd(const float* y, const float4* cf, float* out, int B, int C, int H, int W, int OH, int OW,
+                        hipStream_t s) {
+    const int64_t rows = (int64_t)B * C;
+    maxpool3_fwd_kernel<<<ceil_div(rows * OH * OW, 256), 256, 0, s>>>(y, cf, out, rows, C, H, W, OH, OW);
+    PCX_LAUNCH_CHECK("maxpool3_fwd_kernel");
+    return PCX_OK;
+}
+
+int launch_maxpool3_bwd(const float* y, const float4* cf, const float* dout, float* dz, int B, int C, int H, int W,
+                        int OH, int OW, hipStream_t s) {
+    const int64_t rows = (int64_t)B * C;
+    maxpool3_bwd_kernel<<<ceil_div(rows * H * W, 256), 256, 0, s>>>(y, cf, dout, dz, rows, C, H, W, OH, OW);
+    PCX_LAUNCH_CHECK("maxpool3_bwd_kernel");
+    return PCX_OK;
+}
+
+int launch_fill_cf(float4* cf, int C, float4 v, hipStream_t s) {
+    fill_cf_kernel<<<ceil_div(C, 256), 256, 0, s>>>(cf, C, v);
+    PCX_LAUNCH_CHECK("fill_cf_kernel");
+    return PCX_OK;
+}
+
+}  // namespace pcx

@@ -1,0 +1,507 @@
+// cnn_deep plan: PhonemeNetDeep forward / backward (reference src/models/phoneme_cnn.py:146-304).
+//
+//   stem   y0 = conv7x7(x) (pad 3)      a0 = MaxPool(3,2,1)(ReLU(BN0(y0)))            :211-216
+//   block  y1 = conv3x3_s(a)   d1 = Dropout2d(ReLU(BN1(y1)))                          :174-176
+//          y2 = conv3x3(d1)    sc = a | BNsc(conv1x1_s(a))                            :166-171,177-180
+//          a' = ReLU(BN2(y2) + sc)                                                     :181
+//   (use_residual = false, :230-243:  a' = Dropout2d(ReLU(BN2(conv(ReLU(BN1(conv_s(a))))))))
+//   head   attention(512) -> mean -> Linear -> BN1d -> normalize (shared with cnn_small, head.hip)
+//
+// Raw conv outputs (bias excluded: every conv feeds a train-mode BN, so its bias only shifts the
+// running mean) and the block outputs are kept in the workspace; BN statistics are reduced in
+// float64 by the same finalisers as cnn_small.  Convolutions run on the general implicit-GEMM
+// MFMA kernel (convg.hip); BN / ReLU / residual / dropout are elementwise passes.
+#include "plan.h"
+
+namespace pcx {
+
+struct DeepBlock {
+    int cin, cout, stride, Hi, Wi, Ho, Wo;
+    bool sc;                      // 1x1 conv + BN shortcut
+    int pidx, bnidx, drop_idx;
+    size_t y1, d1, y2, ysc, out;  // forward tensors
+    size_t cf1, cf2, cfsc, cfb1, cfb2, cfbsc;
+    size_t da;                    // gradient w.r.t. the block input
+};
+
+struct DeepPlan {
+    bool residual;
+    int h[4];
+    int H0, W0, H1, W1;
+    size_t y0, a0, cf0, cfb0, dz0;
+    DeepBlock blk[4];
+    size_t g, dyA, dyB, dd, hdz;   // backward scratch
+    size_t stat, wgp, ident;
+    int ia, ip;                    // attention / projection parameter indices
+    int bn_proj;
+};
+
+namespace {
+
+int64_t planes(int B, int C, int H, int W) { return (int64_t)B * C * H * W; }
+
+}  // namespace
+
+int build_deep(Plan& p) {
+    auto dp = std::make_shared<DeepPlan>();
+    DeepPlan& d = *dp;
+    const int B = p.B;
+    d.residual = p.cfg.use_residual != 0;
+    for (int i = 0; i < 4; ++i) {
+        d.h[i] = p.cfg.hidden_dims[i];
+        PCX_CHECK_ARG(d.h[i] >= 1 && d.h[i] <= 4096, "PhonemeNetDeep: hidden_dims[%d] = %d unsupported", i, d.h[i]);
+    }
+    PCX_CHECK_ARG(p.F >= 1 && p.T >= 1, "PhonemeNetDeep: empty input");
+    d.H0 = p.F; d.W0 = p.T;
+    d.H1 = (d.H0 - 1) / 2 + 1; d.W1 = (d.W0 - 1) / 2 + 1;
+    const int C0 = d.h[0];
+    d.y0 = p.carve("y0", planes(B, C0, d.H0, d.W0) * 4);
+    d.dz0 = p.carve("dz0", planes(B, C0, d.H0, d.W0) * 4);
+    d.a0 = p.carve("a0", planes(B, C0, d.H1, d.W1) * 4);
+    d.cf0 = p.carve("cf0", C0 * 16);
+    d.cfb0 = p.carve("cfb0", C0 * 16);
+    int pidx = 4, bnidx = 1, cin = C0, H = d.H1, W = d.W1;
+    size_t gmax = 0, stat = 0, wg = 0;
+    auto wg_need = [&](int ci, int co, int k, int oh, int ow) {
+        ConvGArgs a{};
+        a.B = B; a.cin = ci; a.cout = co; a.KH = a.KW = k; a.OH = oh; a.OW = ow;
+        int64_t ks;
+        int ns = convg_nslice(a, &ks);
+        wg = std::max(wg, (size_t)ns * co * ci * k * k);
+    };
+    auto stat_need = [&](int C) {
+        int bps;
+        int ns = chan_slices(B, C, &bps);
+        stat = std::max(stat, (size_t)3 * C * ns + ns);
+    };
+    stat_need(C0);
+    wg_need(1, C0, 7, d.H0, d.W0);
+    for (int i = 0; i < 4; ++i) {
+        DeepBlock& k = d.blk[i];
+        k.cin = cin; k.cout = d.h[i]; k.stride = i == 0 ? 1 : 2;
+        k.Hi = H; k.Wi = W;
+        k.Ho = (H - 1) / k.stride + 1; k.Wo = (W - 1) / k.stride + 1;
+        k.sc = d.residual && (k.stride != 1 || k.cin != k.cout);
+        k.pidx = pidx; k.bnidx = bnidx; k.drop_idx = i;
+        pidx += 8 + (k.sc ? 4 : 0);
+        bnidx += 2 + (k.sc ? 1 : 0);
+        const size_t no = (size_t)planes(B, k.cout, k.Ho, k.Wo) * 4;
+        char nm[24];
+        snprintf(nm, sizeof nm, "b%d_y1", i); k.y1 = p.carve(nm, no);
+        snprintf(nm, sizeof nm, "b%d_d1", i); k.d1 = p.carve(nm, no);
+        snprintf(nm, sizeof nm, "b%d_y2", i); k.y2 = p.carve(nm, no);
+        snprintf(nm, sizeof nm, "b%d_out", i); k.out = p.carve(nm, no);
+        k.ysc = k.sc ? p.carve("ysc", no) : 0;
+        snprintf(nm, sizeof nm, "b%d_da", i);
+        k.da = p.carve(nm, (size_t)planes(B, k.cin, k.Hi, k.Wi) * 4);
+        k.cf1 = p.carve("cf", k.cout * 16); k.cf2 = p.carve("cf", k.cout * 16);
+        k.cfb1 = p.carve("cf", k.cout * 16); k.cfb2 = p.carve("cf", k.cout * 16);
+        k.cfsc = p.carve("cf", k.cout * 16); k.cfbsc = p.carve("cf", k.cout * 16);
+        gmax = std::max(gmax, no);
+        stat_need(k.cout);
+        wg_need(k.cin, k.cout, 3, k.Ho, k.Wo);
+        wg_need(k.cout, k.cout, 3, k.Ho, k.Wo);
+        if (k.sc) wg_need(k.cin, k.cout, 1, k.Ho, k.Wo);
+        cin = k.cout; H = k.Ho; W = k.Wo;
+    }
+    d.g = p.carve("g", gmax);
+    d.dyA = p.carve("dyA", gmax);
+    d.dyB = p.carve("dyB", gmax);
+    d.dd = p.carve("dd", gmax);
+    const int C4 = d.h[3];
+    p.C6 = C4;
+    p.P6 = H * W;
+    d.hdz = p.carve("hdz", (size_t)planes(B, C4, H, W) * 4);
+    stat = std::max(stat, (size_t)2 * C4 * B);
+    d.stat = p.carve("stat_part", stat * 4);
+    d.wgp = p.carve("wg_part", wg * 4);
+    d.ident = p.carve("ident", (size_t)C4 * 16);
+    d.ia = pidx;
+    d.ip = pidx + (p.cfg.use_attention ? 2 : 0);
+    d.bn_proj = bnidx;
+    const int D = p.D, K = C4;
+    p.pooled = p.carve("pooled", (size_t)B * K * 4);
+    p.att = p.carve("att", (size_t)B * p.P6 * 4);
+    p.h = p.carve("h", (size_t)B * D * 4);
+    p.cfp = p.carve("cfp", (size_t)D * 16);
+    p.cfpb = p.carve("cfpb", (size_t)D * 16);
+    p.norm = p.carve("norm", (size_t)B * 4);
+    p.dzp = p.carve("dzp", (size_t)B * D * 4);
+    p.dh = p.carve("dh", (size_t)B * D * 4);
+    p.dpooled = p.carve("dpooled", (size_t)B * K * 4);
+    p.wt = p.carve("wt", (size_t)K * D * 4);
+    p.hp_dwa = p.carve("hp_dwa", (size_t)K * B * 4);
+    p.hp_dba = p.carve("hp_dba", (size_t)B * 4);
+    p.nparams = d.ip + 4;
+    p.nbn = bnidx + 1;
+    p.ndrop = 4;
+    for (int i = 0; i < 4; ++i) p.drop_ch[i] = d.h[i];
+    p.deep = dp;
+    return PCX_OK;
+}
+
+namespace {
+
+struct Ctx {
+    const Plan& p;
+    const DeepPlan& d;
+    void* ws;
+    hipStream_t s;
+    template <class T>
+    T* w(size_t off) const { return at<T>(ws, off); }
+};
+
+// forward conv (raw output, no bias) + train-mode statistics + BN finalise -> cf
+int conv_bn_fwd(const Ctx& c, const char* label, int layer, const float* x, int cin, int IH, int IW, int k, int stride,
+                int pad, const float* wgt, float* y, int cout, int OH, int OW, const float* gamma, const float* beta,
+                const float* bias, float* rmean, float* rvar, int64_t* nbt, int train, float4* cf) {
+    ConvGArgs a{};
+    a.mode = 0;
+    a.B = c.p.B; a.cin = cin; a.cout = cout;
+    a.IH = IH; a.IW = IW; a.OH = OH; a.OW = OW;
+    a.KH = a.KW = k; a.stride = stride; a.pad = pad;
+    a.x = x; a.w = wgt; a.out = y;
+    { Scope sc(&c.p.prof, c.s, label, layer); RC(launch_convg(a, c.s)); }
+    float* part = c.w<float>(c.d.stat);
+    int ns = 1;
+    BnFwdArgs f{};
+    f.C = cout;
+    if (train) {
+        Scope sc(&c.p.prof, c.s, "chan_stats");
+        int bps;
+        const int nsl = chan_slices(c.p.B, cout, &bps);
+        f.part0 = part;
+        f.part1 = part + (size_t)cout * nsl;
+        f.partn = part + (size_t)2 * cout * nsl;
+        RC(launch_chan_stats(y, c.p.B, cout, (int64_t)OH * OW, const_cast<float*>(f.part0),
+                             const_cast<float*>(f.part1), const_cast<float*>(f.partn), &ns, c.s));
+    }
+    f.nblk = ns;
+    f.gamma = gamma; f.beta = beta; f.bias = bias;
+    f.rmean = rmean; f.rvar = rvar; f.nbt = nbt;
+    f.momentum = 0.1f; f.eps = 1e-5f; f.train = train;
+    f.cf = cf;
+    Scope sc(&c.p.prof, c.s, "bn_fwd_finalize");
+    return launch_bn_fwd_finalize(f, c.s);
+}
+
+// weight gradient of a conv into G (partials summed deterministically) + zero bias gradient
+int conv_wgrad(const Ctx& c, int layer, const float* x, int cin, int IH, int IW, int k, int stride, int pad,
+               const float* dy, int cout, int OH, int OW, float* gw, float* gb) {
+    ConvGArgs a{};
+    a.mode = 2;
+    a.B = c.p.B; a.cin = cin; a.cout = cout;
+    a.IH = IH; a.IW = IW; a.OH = OH; a.OW = OW;
+    a.KH = a.KW = k; a.stride = stride; a.pad = pad;
+    a.x = x; a.dy = dy;
+    a.nslice = convg_nslice(a, &a.kslice);
+    float* wgp = c.w<float>(c.d.wgp);
+    a.out = wgp;
+    { Scope sc(&c.p.prof, c.s, "wgrad", layer); RC(launch_convg(a, c.s)); }
+    RC(launch_sum_slices(wgp, a.nslice, (int64_t)cout * cin * k * k, gw, c.s));
+    // the conv feeds a train-mode BN: d(loss)/d(bias) = sum of the BN backward = 0 exactly
+    return hip_status_ok(hipMemsetAsync(gb, 0, (size_t)cout * 4, c.s), "memset bias grad");
+}
+
+int conv_dgrad(const Ctx& c, int layer, const float* dy, int cout, int OH, int OW, int k, int stride, int pad,
+               const float* wgt, float* dx, int cin, int IH, int IW, int accumulate) {
+    ConvGArgs a{};
+    a.mode = 1;
+    a.B = c.p.B; a.cin = cin; a.cout = cout;
+    a.IH = IH; a.IW = IW; a.OH = OH; a.OW = OW;
+    a.KH = a.KW = k; a.stride = stride; a.pad = pad;
+    a.w = wgt; a.dy = dy; a.out = dx; a.accumulate = accumulate;
+    Scope sc(&c.p.prof, c.s, "conv_dgrad", layer);
+    return launch_convg(a, c.s);
+}
+
+// BN backward: finalize (dgamma, dbeta, coefficients) from bwd_prep partials
+int bn_bwd(const Ctx& c, int C, int ns, const float* pg, const float* px, const float* gamma, const float4* cf_fwd,
+           float* dgamma, float* dbeta, float4* cfb, double count) {
+    BnBwdArgs f{};
+    f.C = C; f.nblk = ns; f.count = count;
+    f.part0 = pg; f.part1 = px;
+    f.gamma = gamma; f.cf_fwd = cf_fwd;
+    f.dgamma = dgamma; f.dbeta = dbeta; f.cf = cfb;
+    Scope sc(&c.p.prof, c.s, "bn_bwd_finalize");
+    return launch_bn_bwd_finalize(f, c.s);
+}
+
+}  // namespace
+
+int deep_forward(const Plan& p, const float* const* P, float* const* bnstat, int64_t* const* nbt, const float* x,
+                 const float* const* drop, int train, float* emb, void* ws, hipStream_t s) {
+    const DeepPlan& d = *p.deep;
+    const Ctx c{p, d, ws, s};
+    const int B = p.B;
+    const float* dmask[4] = {nullptr, nullptr, nullptr, nullptr};
+    if (train && drop)
+        for (int i = 0; i < 4; ++i) dmask[i] = drop[i];
+    auto bnp = [&](int idx, int j) { return bnstat[2 * idx + j]; };
+    auto nb = [&](int idx) { return nbt ? nbt[idx] : nullptr; };
+    const int C0 = d.h[0];
+    // stem
+    RC(conv_bn_fwd(c, "conv_fwd", 0, x, 1, d.H0, d.W0, 7, 1, 3, P[0], c.w<float>(d.y0), C0, d.H0, d.W0, P[2], P[3],
+                   P[1], bnp(0, 0), bnp(0, 1), nb(0), train, c.w<float4>(d.cf0)));
+    {
+        Scope sc(&p.prof, s, "maxpool_fwd");
+        RC(launch_maxpool3_fwd(c.w<float>(d.y0), c.w<float4>(d.cf0), c.w<float>(d.a0), B, C0, d.H0, d.W0, d.H1,
+                               d.W1, s));
+    }
+    const float* a = c.w<float>(d.a0);
+    for (int i = 0; i < 4; ++i) {
+        const DeepBlock& k = d.blk[i];
+        const int q = k.pidx, L = 2 * i + 1;
+        RC(conv_bn_fwd(c, "conv_fwd", L, a, k.cin, k.Hi, k.Wi, 3, k.stride, 1, P[q], c.w<float>(k.y1), k.cout, k.Ho,
+                       k.Wo, P[q + 2], P[q + 3], P[q + 1], bnp(k.bnidx, 0), bnp(k.bnidx, 1), nb(k.bnidx), train,
+                       c.w<float4>(k.cf1)));
+        const int64_t P2 = (int64_t)k.Ho * k.Wo;
+        {
+            Scope sc(&p.prof, s, "bn_act");
+            RC(launch_bn_act(c.w<float>(k.y1), c.w<float4>(k.cf1), nullptr, nullptr,
+                             d.residual ? dmask[i] : nullptr, c.w<float>(k.d1), B, k.cout, P2, s));
+        }
+        RC(conv_bn_fwd(c, "conv_fwd", L + 1, c.w<float>(k.d1), k.cout, k.Ho, k.Wo, 3, 1, 1, P[q + 4], c.w<float>(k.y2),
+                       k.cout, k.Ho, k.Wo, P[q + 6], P[q + 7], P[q + 5], bnp(k.bnidx + 1, 0), bnp(k.bnidx + 1, 1),
+                       nb(k.bnidx + 1), train, c.w<float4>(k.cf2)));
+        const float* res = nullptr;
+        const float4* rcf = nullptr;
+        if (k.sc) {
+            RC(conv_bn_fwd(c, "shortcut_fwd", i, a, k.cin, k.Hi, k.Wi, 1, k.stride, 0, P[q + 8], c.w<float>(k.ysc),
+                           k.cout, k.Ho, k.Wo, P[q + 10], P[q + 11], P[q + 9], bnp(k.bnidx + 2, 0),
+                           bnp(k.bnidx + 2, 1), nb(k.bnidx + 2), train, c.w<float4>(k.cfsc)));
+            res = c.w<float>(k.ysc);
+            rcf = c.w<float4>(k.cfsc);
+        } else if (d.residual) {
+            res = a;
+        }
+        {
+            Scope sc(&p.prof, s, "bn_act");
+            RC(launch_bn_act(c.w<float>(k.y2), c.w<float4>(k.cf2), res, rcf, d.residual ? nullptr : dmask[i],
+                             c.w<float>(k.out), B, k.cout, P2, s));
+        }
+        a = c.w<float>(k.out);
+    }
+    // head on the (already non-negative) trunk output: identity BN coefficients
+    RC(launch_fill_cf(c.w<float4>(d.ident), d.h[3], make_float4(1.f, 0.f, 0.f, 1.f), s));
+    {
+        HeadPoolArgs h{};
+        h.B = B; h.C = p.C6; h.P = p.P6;
+        h.y = a;
+        h.cf = c.w<float4>(d.ident);
+        h.drop = nullptr;
+        h.wa = p.cfg.use_attention ? P[d.ia] : nullptr;
+        h.ba = p.cfg.use_attention ? P[d.ia + 1] : nullptr;
+        h.pooled = at<float>(ws, p.pooled);
+        h.att = at<float>(ws, p.att);
+        Scope sc(&p.prof, s, "head_pool_fwd");
+        RC(launch_head_pool_fwd(h, s));
+    }
+    {
+        const int ip = d.ip;
+        RC(launch_transpose(P[ip], at<float>(ws, p.wt), p.D, p.C6, s));
+        ProjArgs j{};
+        j.B = B; j.K = p.C6; j.D = p.D;
+        j.pooled = at<float>(ws, p.pooled);
+        j.w = P[ip];
+        j.wt = at<float>(ws, p.wt);
+        j.bias = P[ip + 1];
+        j.gamma = P[ip + 2];
+        j.beta = P[ip + 3];
+        j.rmean = bnp(d.bn_proj, 0);
+        j.rvar = bnp(d.bn_proj, 1);
+        j.nbt = nb(d.bn_proj);
+        j.momentum = 0.1f;
+        j.eps = 1e-5f;
+        j.train = train;
+        j.h = at<float>(ws, p.h);
+        j.cf = at<float4>(ws, p.cfp);
+        j.emb = emb;
+        j.norm = at<float>(ws, p.norm);
+        Scope sc(&p.prof, s, "proj_fwd");
+        RC(launch_proj_fwd(j, s));
+    }
+    return PCX_OK;
+}
+
+int deep_backward(const Plan& p, const float* const* P, const float* x, const float* const* drop, const float* emb,
+                  const float* demb, float* const* G, void* ws, hipStream_t s) {
+    const DeepPlan& d = *p.deep;
+    const Ctx c{p, d, ws, s};
+    const int B = p.B;
+    const float* dmask[4] = {nullptr, nullptr, nullptr, nullptr};
+    if (drop)
+        for (int i = 0; i < 4; ++i) dmask[i] = drop[i];
+    float* part = c.w<float>(d.stat);
+    const int ip = d.ip, ia = d.ia;
+    {
+        ProjArgs j{};
+        j.B = B; j.K = p.C6; j.D = p.D;
+        j.pooled = at<float>(ws, p.pooled);
+        j.w = P[ip];
+        j.gamma = P[ip + 2];
+        j.h = at<float>(ws, p.h);
+        j.cf = at<float4>(ws, p.cfp);
+        j.emb = const_cast<float*>(emb);
+        j.norm = at<float>(ws, p.norm);
+        j.demb = demb;
+        j.dzp = at<float>(ws, p.dzp);
+        j.cfb = at<float4>(ws, p.cfpb);
+        j.dh = at<float>(ws, p.dh);
+        j.dpooled = at<float>(ws, p.dpooled);
+        j.dw = G[ip];
+        j.db = G[ip + 1];
+        j.dgamma = G[ip + 2];
+        j.dbeta = G[ip + 3];
+        Scope sc(&p.prof, s, "proj_bwd");
+        RC(launch_proj_bwd(j, s));
+    }
+    {
+        HeadPoolArgs h{};
+        h.B = B; h.C = p.C6; h.P = p.P6;
+        h.y = c.w<float>(d.blk[3].out);
+        h.cf = c.w<float4>(d.ident);
+        h.drop = nullptr;
+        h.wa = p.cfg.use_attention ? P[ia] : nullptr;
+        h.ba = p.cfg.use_attention ? P[ia + 1] : nullptr;
+        h.att = at<float>(ws, p.att);
+        h.dpooled = at<float>(ws, p.dpooled);
+        h.dz = c.w<float>(d.hdz);
+        h.p_dz = part;
+        h.p_dzx = part + (size_t)p.C6 * B;
+        h.p_dwa = at<float>(ws, p.hp_dwa);
+        h.p_dba = at<float>(ws, p.hp_dba);
+        { Scope sc(&p.prof, s, "head_pool_bwd"); RC(launch_head_pool_bwd(h, s)); }
+        if (p.cfg.use_attention) {
+            RC(launch_row_sum(h.p_dwa, p.C6, B, G[ia], s));
+            RC(launch_row_sum(h.p_dba, 1, B, G[ia + 1], s));
+        }
+    }
+    // upstream gradient of the current block's output (already ReLU-masked for the last block)
+    const float* dout = c.w<float>(d.hdz);
+    bool masked = true;
+    for (int i = 3; i >= 0; --i) {
+        const DeepBlock& k = d.blk[i];
+        const int q = k.pidx, L = 2 * i + 1;
+        const int64_t P2 = (int64_t)k.Ho * k.Wo;
+        const double count = (double)B * P2;
+        const float* a_in = i == 0 ? c.w<float>(d.a0) : c.w<float>(d.blk[i - 1].out);
+        float* g = c.w<float>(d.g);
+        float* dy2 = c.w<float>(d.dyA);
+        float* dysc = c.w<float>(d.dyB);
+        int ns = 0;
+        // ---- g = dL/d(pre-activation sum) (residual) or dL/d(BN2 output) (plain); BN2 [+ BNsc] sums
+        {
+            BwdPrepArgs b{};
+            b.B = B; b.C = k.cout; b.P = P2;
+            b.d = dout;
+            if (d.residual) {
+                b.mask_mode = masked ? MASK_NONE : MASK_OUT;
+                b.mask_src = c.w<float>(k.out);
+            } else {
+                b.mask_mode = MASK_BN;
+                b.mask_src = c.w<float>(k.y2);
+                b.mask_cf = c.w<float4>(k.cf2);
+                b.drop = dmask[i];
+            }
+            b.g = g;
+            b.y1 = c.w<float>(k.y2);
+            b.cf1 = c.w<float4>(k.cf2);
+            if (k.sc) { b.y2 = c.w<float>(k.ysc); b.cf2 = c.w<float4>(k.cfsc); }
+            int bps;
+            const int nsl = chan_slices(B, k.cout, &bps);
+            b.p_g = part;
+            b.p_x1 = part + (size_t)k.cout * nsl;
+            b.p_x2 = k.sc ? part + (size_t)2 * k.cout * nsl : nullptr;
+            { Scope sc(&p.prof, s, "bwd_prep", L + 1); RC(launch_bwd_prep(b, &ns, s)); }
+            RC(bn_bwd(c, k.cout, ns, b.p_g, b.p_x1, P[q + 6], c.w<float4>(k.cf2), G[q + 6], G[q + 7],
+                      c.w<float4>(k.cfb2), count));
+            if (k.sc)
+                RC(bn_bwd(c, k.cout, ns, b.p_g, b.p_x2, P[q + 10], c.w<float4>(k.cfsc), G[q + 10], G[q + 11],
+                          c.w<float4>(k.cfbsc), count));
+        }
+        {
+            Scope sc(&p.prof, s, "bn_bwd_apply");
+            RC(launch_bn_bwd_apply(g, c.w<float>(k.y2), c.w<float4>(k.cfb2), dy2, B, k.cout, P2, s));
+            if (k.sc) RC(launch_bn_bwd_apply(g, c.w<float>(k.ysc), c.w<float4>(k.cfbsc), dysc, B, k.cout, P2, s));
+        }
+        // ---- conv2
+        RC(conv_wgrad(c, L + 1, c.w<float>(k.d1), k.cout, k.Ho, k.Wo, 3, 1, 1, dy2, k.cout, k.Ho, k.Wo, G[q + 4],
+                      G[q + 5]));
+        float* dd = c.w<float>(d.dd);
+        RC(conv_dgrad(c, L + 1, dy2, k.cout, k.Ho, k.Wo, 3, 1, 1, P[q + 4], dd, k.cout, k.Ho, k.Wo, 0));
+        // ---- through Dropout2d / ReLU / BN1
+        {
+            BwdPrepArgs b{};
+            b.B = B; b.C = k.cout; b.P = P2;
+            b.d = dd;
+            b.mask_mode = MASK_BN;
+            b.mask_src = c.w<float>(k.y1);
+            b.mask_cf = c.w<float4>(k.cf1);
+            b.drop = d.residual ? dmask[i] : nullptr;
+            b.g = dd;
+            b.y1 = c.w<float>(k.y1);
+            b.cf1 = c.w<float4>(k.cf1);
+            int bps;
+            const int nsl = chan_slices(B, k.cout, &bps);
+            b.p_g = part;
+            b.p_x1 = part + (size_t)k.cout * nsl;
+            { Scope sc(&p.prof, s, "bwd_prep", L); RC(launch_bwd_prep(b, &ns, s)); }
+            RC(bn_bwd(c, k.cout, ns, b.p_g, b.p_x1, P[q + 2], c.w<float4>(k.cf1), G[q + 2], G[q + 3],
+                      c.w<float4>(k.cfb1), count));
+        }
+        float* dy1 = dy2;  // dy2 is dead after conv2's gradients
+        {
+            Scope sc(&p.prof, s, "bn_bwd_apply");
+            RC(launch_bn_bwd_apply(dd, c.w<float>(k.y1), c.w<float4>(k.cfb1), dy1, B, k.cout, P2, s));
+        }
+        // ---- conv1 (+ shortcut): gradients of the weights and of the block input
+        RC(conv_wgrad(c, L, a_in, k.cin, k.Hi, k.Wi, 3, k.stride, 1, dy1, k.cout, k.Ho, k.Wo, G[q], G[q + 1]));
+        float* da = c.w<float>(k.da);
+        int acc = 0;
+        if (d.residual && !k.sc) {  // identity shortcut: the block input receives g directly
+            RC(hip_status_ok(hipMemcpyAsync(da, g, (size_t)B * k.cout * P2 * 4, hipMemcpyDeviceToDevice, s),
+                             "copy shortcut grad"));
+            acc = 1;
+        }
+        RC(conv_dgrad(c, L, dy1, k.cout, k.Ho, k.Wo, 3, k.stride, 1, P[q], da, k.cin, k.Hi, k.Wi, acc));
+        if (k.sc) {
+            RC(conv_wgrad(c, 100 + i, a_in, k.cin, k.Hi, k.Wi, 1, k.stride, 0, dysc, k.cout, k.Ho, k.Wo, G[q + 8],
+                          G[q + 9]));
+            RC(conv_dgrad(c, 100 + i, dysc, k.cout, k.Ho, k.Wo, 1, k.stride, 0, P[q + 8], da, k.cin, k.Hi, k.Wi, 1));
+        }
+        dout = da;
+        masked = false;
+    }
+    // ---- stem: MaxPool(3,2,1) + ReLU backward, BN0 backward, 7x7 weight gradient
+    const int C0 = d.h[0];
+    const int64_t P0 = (int64_t)d.H0 * d.W0;
+    float* dz0 = c.w<float>(d.dz0);
+    {
+        Scope sc(&p.prof, s, "maxpool_bwd");
+        RC(launch_maxpool3_bwd(c.w<float>(d.y0), c.w<float4>(d.cf0), dout, dz0, B, C0, d.H0, d.W0, d.H1, d.W1, s));
+    }
+    {
+        BwdPrepArgs b{};
+        b.B = B; b.C = C0; b.P = P0;
+        b.d = dz0;
+        b.mask_mode = MASK_NONE;
+        b.g = dz0;
+        b.y1 = c.w<float>(d.y0);
+        b.cf1 = c.w<float4>(d.cf0);
+        int bps, ns;
+        const int nsl = chan_slices(B, C0, &bps);
+        b.p_g = part;
+        b.p_x1 = part + (size_t)C0 * nsl;
+        { Scope sc(&p.prof, s, "bwd_prep", 0); RC(launch_bwd_prep(b, &ns, s)); }
+        RC(bn_bwd(c, C0, ns, b.p_g, b.p_x1, P[2], c.w<float4>(d.cf0), G[2], G[3], c.w<float4>(d.cfb0),
+                  (double)B * P0));
+    }
+    {
+        Scope sc(&p.prof, s, "bn_bwd_apply");
+        RC(launch_bn_bwd_apply(dz0, c.w<float>(d.y0), c.w<float4>(d.cfb0), dz0, B, C0, P0, s));
+    }
+    return conv_wgrad(c, 0, x, 1, d.H0, d.W0, 7, 1, 3, dz0, C0, d.H0, d.W0, G[0], G[1]);
+}
+
+}  // namespace pcx

@@ -48,6 +48,12 @@ struct ConvArgs {
 
 int launch_conv3x3(int pro, int epi, ConvArgs a, hipStream_t s);
 size_t conv3x3_nblk(int B, int H, int W, int cout);
+// Same GEMM with raw rows DMA'd (global_load_lds, double-buffered) and the prologue applied at
+// operand-read time (conv_dma.hip).  Prologues PRO_RAW, PRO_BNRELU, PRO_BNBWD.
+int launch_conv3x3_dma(int pro, int epi, ConvArgs a, hipStream_t s);
+// materialised block tail x = drop * maxpool2(relu(y*s + t)) (feeds PRO_RAW convs)
+int launch_bn_relu_pool(const float* y, const float4* cf, const float* drop, float* x, int B, int C,
+                        int Hs, int Ws, hipStream_t s);
 
 // Cin = 1 convolution (first layer), 3x3 pad 1, with BN statistics.
 struct Conv1Args {
@@ -193,5 +199,57 @@ int launch_transpose(const float* in, float* out, int rows, int cols, hipStream_
 
 // out[r] = sum_c part[r][c] (float64, fixed order)
 int launch_row_sum(const float* part, int rows, int64_t cols, float* out, hipStream_t s);
+
+// ------------------------------------------------------------------ residual network (convg.hip)
+// General KxK / stride 1|2 conv as an implicit GEMM: mode 0 forward, 1 data grad, 2 weight grad.
+struct ConvGArgs {
+    int mode;
+    int B, cin, cout;
+    int IH, IW, OH, OW;   // input / output resolution of the forward conv
+    int KH, KW, stride, pad;
+    const float* x;       // modes 0, 2: [B][cin][IH][IW]
+    const float* w;       // modes 0, 1: [cout][cin][KH][KW] (reference layout)
+    const float* dy;      // modes 1, 2: [B][cout][OH][OW]
+    float* out;           // 0: y [B][cout][OH][OW]; 1: dx [B][cin][IH][IW]; 2: [nslice][cout][cin*KH*KW]
+    int accumulate;       // mode 1: dx += result
+    int64_t kslice;       // mode 2: pixels per slice (multiple of 16)
+    int nslice;
+};
+int launch_convg(ConvGArgs a, hipStream_t s);
+int convg_nslice(const ConvGArgs& a, int64_t* kslice);
+
+enum MaskMode { MASK_NONE = 0, MASK_OUT = 1, MASK_BN = 2 };
+struct BwdPrepArgs {
+    int B, C;
+    int64_t P;
+    int bps;                  // samples per slice (set by the launcher)
+    const float* d;           // upstream gradient
+    const float* d2;          // optional second upstream gradient (added)
+    int mask_mode;            // MASK_OUT: g = d*[mask_src > 0]; MASK_BN: g = d*drop*[mask_src*s+t > 0]
+    const float* mask_src;
+    const float4* mask_cf;
+    const float* drop;
+    float* g;                 // masked gradient (may alias d)
+    const float* y1;          // BN inputs whose sum(g*xhat) is needed (or NULL)
+    const float4* cf1;
+    const float* y2;
+    const float4* cf2;
+    float* p_g;               // [C][nslice] partial sums of g
+    float* p_x1;              // [C][nslice] partial sums of g*xhat1
+    float* p_x2;
+};
+int launch_bwd_prep(BwdPrepArgs a, int* nslice, hipStream_t s);
+int chan_slices(int B, int C, int* bps);
+int launch_chan_stats(const float* y, int B, int C, int64_t P, float* part0, float* part1, float* partn,
+                      int* nslice, hipStream_t s);
+int launch_bn_act(const float* y, const float4* cf, const float* res, const float4* rcf, const float* drop,
+                  float* out, int B, int C, int64_t P, hipStream_t s);
+int launch_bn_bwd_apply(const float* g, const float* y, const float4* cf, float* dy, int B, int C, int64_t P,
+                        hipStream_t s);
+int launch_maxpool3_fwd(const float* y, const float4* cf, float* out, int B, int C, int H, int W, int OH, int OW,
+                        hipStream_t s);
+int launch_maxpool3_bwd(const float* y, const float4* cf, const float* dout, float* dz, int B, int C, int H, int W,
+                        int OH, int OW, hipStream_t s);
+int launch_fill_cf(float4* cf, int C, float4 v, hipStream_t s);
 
 }  // namespace pcx

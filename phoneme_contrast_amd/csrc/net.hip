@@ -10,111 +10,20 @@
 //   y2 = conv2(r1)          x3 = Dropout2d(MaxPool2(r2))   y3 = conv3(x3)
 //   y4 = conv4(r3)          x5 = Dropout2d(MaxPool2(r4))   y5 = conv5(x5)
 //   y6 = conv6(r5)          x6 = Dropout2d(r6) -> attention -> mean -> Linear -> BN1d -> normalize
+#include <cstdlib>
+#include <cstring>
 #include <string>
 #include <vector>
 
-#include "kernels.h"
+#include "plan.h"
 
 namespace pcx {
-namespace {
-
-struct Region {
-    std::string name;
-    size_t off, bytes;
-};
-
-// Optional per-launch HIP-event timing (pcx_net_profile): lets bench.py time individual kernels
-// on the stream they run on, inside its timed region.
-struct Profiler {
-    bool on = false;
-    std::vector<hipEvent_t> pool;
-    size_t used = 0;
-    std::vector<std::string> labels;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> spans;
-    hipEvent_t get() {
-        if (used == pool.size()) {
-            hipEvent_t e;
-            if (hipEventCreate(&e) != hipSuccess) return nullptr;
-            pool.push_back(e);
-        }
-        return pool[used++];
-    }
-    void clear() {
-        used = 0;
-        labels.clear();
-        spans.clear();
-    }
-    ~Profiler() {
-        for (auto e : pool) (void)hipEventDestroy(e);
-    }
-};
-
-struct Scope {
-    Profiler* p;
-    hipStream_t s;
-    hipEvent_t a = nullptr;
-    std::string label;
-    Scope(Profiler* prof, hipStream_t st, const char* lab, int layer = -1) : p(prof), s(st) {
-        if (!p->on) return;
-        label = lab;
-        if (layer >= 0) label += "_L" + std::to_string(layer);
-        a = p->get();
-        if (a) (void)hipEventRecord(a, s);
-    }
-    ~Scope() {
-        if (!p->on || !a) return;
-        hipEvent_t b = p->get();
-        if (!b) return;
-        (void)hipEventRecord(b, s);
-        p->labels.push_back(label);
-        p->spans.push_back({a, b});
-    }
-};
-
-struct Layer {  // one 3x3 conv of the trunk (L = 1..6)
-    int cin, cout, H, W;   // conv resolution
-    int srcH, srcW;        // resolution of the tensor its prologue reads
-    bool pooled_in;        // prologue includes MaxPool2 + Dropout2d
-    int drop_idx;          // dropout layer feeding its input (pooled_in) or -1
-    size_t y, dz, cf, cfb, wp, wpd;  // workspace offsets
-    int nblk;              // forward statistics tiles
-    WgradArgs wg;          // weight-gradient geometry
-};
-
-struct Plan {
-    pcx_net_config cfg;
-    int B, F, T, D, C6, P6;
-    Layer L[7];
-    int conv1_nblk, conv1_rows;
-    int wg1_nslice, wg1_rows;
-    size_t stat_part, stat_bytes;   // shared scratch for BN partials
-    size_t wg_part, wg_bytes;       // shared scratch for weight-gradient partials
-    size_t pooled, att, h, cfp, cfpb, norm, dzp, dh, dpooled, wt, hp_dz, hp_dzx, hp_dwa, hp_dba;
-    size_t total;
-    std::vector<Region> regions;
-    int nparams, nbn, ndrop, drop_ch[4];
-    mutable Profiler prof;
-
-    size_t carve(const char* name, size_t bytes) {
-        size_t off = total;
-        total += (bytes + 255) / 256 * 256;
-        regions.push_back({name, off, bytes});
-        return off;
-    }
-};
-
-inline int hip_status_ok(hipError_t e, const char* what) { return e == hipSuccess ? 0 : hip_status(e, what); }
-
-template <class T>
-T* at(void* ws, size_t off) {
-    return reinterpret_cast<T*>(static_cast<char*>(ws) + off);
-}
 
 // parameter indices (state_dict / named_parameters order) for cnn_small
-inline int p_conv_w(int L) { return 8 * ((L - 1) / 2) + 4 * ((L - 1) % 2); }
-inline int p_conv_b(int L) { return p_conv_w(L) + 1; }
-inline int p_bn_g(int L) { return p_conv_w(L) + 2; }
-inline int p_bn_b(int L) { return p_conv_w(L) + 3; }
+static inline int p_conv_w(int L) { return 8 * ((L - 1) / 2) + 4 * ((L - 1) % 2); }
+static inline int p_conv_b(int L) { return p_conv_w(L) + 1; }
+static inline int p_bn_g(int L) { return p_conv_w(L) + 2; }
+static inline int p_bn_b(int L) { return p_conv_w(L) + 3; }
 
 int build_small(Plan& p) {
     const int B = p.B, H1 = p.F, W1 = p.T;
@@ -144,6 +53,10 @@ int build_small(Plan& p) {
         L.cf = p.carve(nm, L.cout * 16);
         snprintf(nm, sizeof nm, "cfb%d", l);
         L.cfb = p.carve(nm, L.cout * 16);
+        if (L.pooled_in) {
+            snprintf(nm, sizeof nm, "xp%d", l);
+            L.xp = p.carve(nm, (size_t)B * L.cin * L.H * L.W * 4);
+        }
         if (l >= 2) {
             L.wp = p.carve("wp", (size_t)9 * L.cin * L.cout * 4);
             L.wpd = p.carve("wpd", (size_t)9 * L.cin * L.cout * 4);
@@ -190,11 +103,6 @@ int build_small(Plan& p) {
     return PCX_OK;
 }
 
-#define RC(x)                   \
-    do {                        \
-        int _rc = (x);          \
-        if (_rc) return _rc;    \
-    } while (0)
 
 int small_forward(const Plan& p, const float* const* P, float* const* bnstat, int64_t* const* nbt,
                   const float* x, const float* const* drop, int train, float* emb, void* ws,
@@ -260,7 +168,22 @@ int small_forward(const Plan& p, const float* const* P, float* const* bnstat, in
         c.part1 = part + (size_t)L.cout * L.nblk;
         c.partn = part + (size_t)2 * L.cout * L.nblk;
         c.nblk = L.nblk;
-        { Scope sc(&p.prof, s, "conv_fwd", l); RC(launch_conv3x3(L.pooled_in ? PRO_BNRELU_POOL : PRO_BNRELU, EPI_FWD, c, s)); }
+        if (p.dma) {
+            int pro = PRO_BNRELU;
+            if (L.pooled_in) {  // block tail materialised once; the conv and its wgrad read it raw
+                Scope sc(&p.prof, s, "bn_relu_pool", l);
+                RC(launch_bn_relu_pool(c.src, c.cf_in, c.drop_in, at<float>(ws, L.xp), B, L.cin, L.srcH,
+                                       L.srcW, s));
+                c.src = at<float>(ws, L.xp);
+                c.srcH = L.H; c.srcW = L.W;
+                pro = PRO_RAW;
+            }
+            Scope sc(&p.prof, s, "conv_fwd", l);
+            RC(launch_conv3x3_dma(pro, EPI_FWD, c, s));
+        } else {
+            Scope sc(&p.prof, s, "conv_fwd", l);
+            RC(launch_conv3x3(L.pooled_in ? PRO_BNRELU_POOL : PRO_BNRELU, EPI_FWD, c, s));
+        }
         RC(finalize(l));
     }
     // head: attention + mean pool on x6 = Dropout2d(ReLU(BN6(y6)))
@@ -391,7 +314,13 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
             w.drop = L.pooled_in ? dmask[L.drop_idx] : nullptr;
             w.srcH = L.srcH; w.srcW = L.srcW;
             w.part = wgp;
-            { Scope sc(&p.prof, s, "wgrad", l); RC(launch_wgrad3x3(L.pooled_in ? PRO_BNRELU_POOL : PRO_BNRELU, w, s)); }
+            int pro = L.pooled_in ? PRO_BNRELU_POOL : PRO_BNRELU;
+            if (p.dma && L.pooled_in) {  // pooled input materialised by the forward
+                w.src = at<float>(ws, L.xp);
+                w.srcH = L.H; w.srcW = L.W;
+                pro = PRO_RAW;
+            }
+            { Scope sc(&p.prof, s, "wgrad", l); RC(launch_wgrad3x3(pro, w, s)); }
             { Scope sc(&p.prof, s, "wgrad_reduce", l); RC(launch_sum_slices(wgp, w.nslice, (int64_t)L.cout * L.cin * 9, G[p_conv_w(l)], s)); }
         }
         // ---- data gradient -> dz of the previous BN (through ReLU / MaxPool / Dropout2d)
@@ -417,7 +346,11 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
             c.part0 = part;
             c.part1 = part + (size_t)L.cin * nblk;
             c.nblk = nblk;
-            { Scope sc(&p.prof, s, "conv_dgrad", l); RC(launch_conv3x3(PRO_BNBWD, L.pooled_in ? EPI_BWD_POOL : EPI_BWD_RELU, c, s)); }
+            {
+                Scope sc(&p.prof, s, "conv_dgrad", l);
+                const int epi = L.pooled_in ? EPI_BWD_POOL : EPI_BWD_RELU;
+                RC(p.dma ? launch_conv3x3_dma(PRO_BNBWD, epi, c, s) : launch_conv3x3(PRO_BNBWD, epi, c, s));
+            }
             RC(bwd_finalize(l - 1, nblk, (double)B * Lp.H * Lp.W));
         }
     }
@@ -440,7 +373,6 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
     return PCX_OK;
 }
 
-}  // namespace
 }  // namespace pcx
 
 // ====================================================================== C ABI
@@ -462,8 +394,13 @@ extern "C" void* pcx_net_create(const pcx_net_config* cfg, int64_t B, int64_t F,
     p->cfg = *cfg;
     p->B = (int)B; p->F = (int)F; p->T = (int)T; p->D = cfg->embedding_dim;
     p->total = 0;
+    {
+        const char* impl = getenv("PCX_CONV");  // A/B switch for measurements: "legacy" = conv.hip
+        p->dma = !(impl && strcmp(impl, "legacy") == 0);
+    }
     int rc = PCX_EINVAL;
     if (cfg->kind == PCX_NET_CNN_SMALL) rc = build_small(*p);
+    else if (cfg->kind == PCX_NET_CNN_DEEP) rc = build_deep(*p);
     else set_error("pcx_net_create: network kind %d not supported", cfg->kind);
     if (rc) { delete p; return nullptr; }
     return p;
@@ -512,6 +449,7 @@ extern "C" int pcx_net_forward(const void* plan, const float* const* params, flo
         set_error("Expected more than 1 value per channel when training, got input size [1, %d]", p->D);
         return PCX_EINVAL;
     }
+    if (p->deep) return deep_forward(*p, params, bn_stats, bn_counts, x, dropout, train, emb, ws, stream);
     return small_forward(*p, params, bn_stats, bn_counts, x, dropout, train, emb, ws, stream);
 }
 
@@ -522,6 +460,7 @@ extern "C" int pcx_net_backward(const void* plan, const float* const* params, co
     PCX_CHECK_ARG(plan && params && x && emb && d_emb && grads && ws, "pcx_net_backward: NULL argument");
     const Plan* p = static_cast<const Plan*>(plan);
     if (ws_bytes < p->total) { set_error("pcx_net_backward: workspace too small"); return PCX_EWORKSPACE; }
+    if (p->deep) return deep_backward(*p, params, x, dropout, emb, d_emb, grads, ws, stream);
     return small_backward(*p, params, x, dropout, emb, d_emb, grads, ws, stream);
 }
 

@@ -1,0 +1,132 @@
+// Host-side network plan shared by the cnn_small (net.hip) and cnn_deep (deep.hip) orchestrators.
+#pragma once
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+
+namespace pcx {
+
+struct Region {
+    std::string name;
+    size_t off, bytes;
+};
+
+// Optional per-launch HIP-event timing (pcx_net_profile): lets bench.py time individual kernels
+// on the stream they run on, inside its timed region.
+struct Profiler {
+    bool on = false;
+    std::vector<hipEvent_t> pool;
+    size_t used = 0;
+    std::vector<std::string> labels;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> spans;
+    hipEvent_t get() {
+        if (used == pool.size()) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+            pool.push_back(e);
+        }
+        return pool[used++];
+    }
+    void clear() {
+        used = 0;
+        labels.clear();
+        spans.clear();
+    }
+    ~Profiler() {
+        for (auto e : pool) (void)hipEventDestroy(e);
+    }
+};
+
+struct Scope {
+    Profiler* p;
+    hipStream_t s;
+    hipEvent_t a = nullptr;
+    std::string label;
+    Scope(Profiler* prof, hipStream_t st, const char* lab, int layer = -1) : p(prof), s(st) {
+        if (!p->on) return;
+        label = lab;
+        if (layer >= 0) label += "_L" + std::to_string(layer);
+        a = p->get();
+        if (a) (void)hipEventRecord(a, s);
+    }
+    ~Scope() {
+        if (!p->on || !a) return;
+        hipEvent_t b = p->get();
+        if (!b) return;
+        (void)hipEventRecord(b, s);
+        p->labels.push_back(label);
+        p->spans.push_back({a, b});
+    }
+};
+
+struct Layer {  // one 3x3 conv of the trunk (L = 1..6)
+    int cin, cout, H, W;   // conv resolution
+    int srcH, srcW;        // resolution of the tensor its prologue reads
+    bool pooled_in;        // prologue includes MaxPool2 + Dropout2d
+    int drop_idx;          // dropout layer feeding its input (pooled_in) or -1
+    size_t y, dz, cf, cfb, wp, wpd;  // workspace offsets
+    size_t xp;             // pooled_in: materialised input drop * maxpool2(relu(bn(y_prev)))
+    int nblk;              // forward statistics tiles
+    WgradArgs wg;          // weight-gradient geometry
+};
+
+struct DeepPlan;  // deep.hip
+
+struct Plan {
+    pcx_net_config cfg;
+    std::shared_ptr<DeepPlan> deep;  // cnn_deep layout (null for cnn_small)
+    int B, F, T, D, C6, P6;
+    Layer L[7];
+    int conv1_nblk, conv1_rows;
+    int wg1_nslice, wg1_rows;
+    size_t stat_part, stat_bytes;   // shared scratch for BN partials
+    size_t wg_part, wg_bytes;       // shared scratch for weight-gradient partials
+    size_t pooled, att, h, cfp, cfpb, norm, dzp, dh, dpooled, wt, hp_dz, hp_dzx, hp_dwa, hp_dba;
+    size_t total;
+    std::vector<Region> regions;
+    int nparams, nbn, ndrop, drop_ch[4];
+    bool dma;                       // LDS-DMA conv path (default); PCX_CONV=legacy selects conv.hip
+    mutable Profiler prof;
+
+    size_t carve(const char* name, size_t bytes) {
+        size_t off = total;
+        total += (bytes + 255) / 256 * 256;
+        regions.push_back({name, off, bytes});
+        return off;
+    }
+};
+
+inline int hip_status_ok(hipError_t e, const char* what) { return e == hipSuccess ? 0 : hip_status(e, what); }
+
+template <class T>
+T* at(void* ws, size_t off) {
+    return reinterpret_cast<T*>(static_cast<char*>(ws) + off);
+}
+
+
+#define RC(x)                   \
+    do {                        \
+        int _rc = (x);          \
+        if (_rc) return _rc;    \
+    } while (0)
+
+// cnn_small (net.hip)
+int build_small(Plan& p);
+int small_forward(const Plan& p, const float* const* P, float* const* bnstat, int64_t* const* nbt,
+                  const float* x, const float* const* drop, int train, float* emb, void* ws,
+                  hipStream_t s);
+int small_backward(const Plan& p, const float* const* P, const float* x, const float* const* drop,
+                   const float* emb, const float* demb, float* const* G, void* ws, hipStream_t s);
+// cnn_deep (deep.hip)
+int build_deep(Plan& p);
+int deep_forward(const Plan& p, const float* const* P, float* const* bnstat, int64_t* const* nbt,
+                 const float* x, const float* const* drop, int train, float* emb, void* ws,
+                 hipStream_t s);
+int deep_backward(const Plan& p, const float* const* P, const float* x, const float* const* drop,
+                  const float* emb, const float* demb, float* const* G, void* ws, hipStream_t s);
+
+}  // namespace pcx
