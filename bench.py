@@ -27,6 +27,7 @@ sys.path.insert(0, ROOT)
 FP32_PEAK_TFLOPS = 157.3     # MI355X vector == matrix fp32 (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0        # HBM3E spec
 METRIC = "MFCC-samples/sec per train step (cnn_small, batch 4096) at 1/2/4/8 MI355X"
+DEEP_DIMS = [64, 128, 256, 512]
 
 
 def log(*a):
@@ -65,6 +66,46 @@ def kernel_costs(B, F, T, D=128):
         # wgrad: reads dz_l, y_l and the forward input source
         out[f"wgrad_L{l}"] = (2 * macs, 2 * y_out + x_in)
     return out
+
+
+def deep_convs(F, T, h=DEEP_DIMS):
+    """(fwd label, wgrad label, dgrad label or None, cin, cout, k, stride, IH, IW, OH, OW) of every
+    conv of cnn_deep, labelled as deep.hip profiles them."""
+    out = [("conv_fwd_L0", "wgrad_L0", None, 1, h[0], 7, 1, F, T, F, T)]
+    H, W, cin = (F - 1) // 2 + 1, (T - 1) // 2 + 1, h[0]
+    for i, co in enumerate(h):
+        s = 1 if i == 0 else 2
+        Ho, Wo = (H - 1) // s + 1, (W - 1) // s + 1
+        L = 2 * i + 1
+        out.append((f"conv_fwd_L{L}", f"wgrad_L{L}", f"conv_dgrad_L{L}", cin, co, 3, s, H, W, Ho, Wo))
+        out.append((f"conv_fwd_L{L + 1}", f"wgrad_L{L + 1}", f"conv_dgrad_L{L + 1}", co, co, 3, 1, Ho, Wo, Ho, Wo))
+        if s != 1 or cin != co:
+            out.append((f"shortcut_fwd_L{i}", f"wgrad_L{100 + i}", f"conv_dgrad_L{100 + i}", cin, co, 1, s, H, W,
+                        Ho, Wo))
+        H, W, cin = Ho, Wo, co
+    return out
+
+
+def deep_kernel_costs(B, F, T):
+    out = {}
+    for fl, wl, dl, ci, co, k, s, IH, IW, OH, OW in deep_convs(F, T):
+        macs = B * OH * OW * co * ci * k * k
+        x_b, y_b = 4 * B * ci * IH * IW, 4 * B * co * OH * OW
+        out[fl] = (2 * macs, x_b + y_b)
+        out[wl] = (2 * macs, x_b + y_b)
+        if dl:
+            out[dl] = (2 * macs, x_b + y_b)
+    return out
+
+
+def deep_step_cost(B, F, T, D=128):
+    flops, act = 0, 4 * 2 * B * F * T
+    for fl, wl, dl, ci, co, k, s, IH, IW, OH, OW in deep_convs(F, T):
+        macs = B * OH * OW * co * ci * k * k
+        flops += 2 * macs * (3 if dl else 2)
+        act += 4 * 5 * B * co * OH * OW
+    flops += 4 * B * B * D + 3 * 2 * B * DEEP_DIMS[-1] * D
+    return flops, act + 40 * 4968833 + 12 * B * D
 
 
 def step_cost(B, F, T, D=128):
@@ -128,6 +169,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=4096, help="per-GPU batch (views)")
     ap.add_argument("--T", type=int, default=200)
+    ap.add_argument("--model", choices=["cnn_small", "cnn_deep"], default="cnn_small",
+                    help="cnn_small is the north-star workload; cnn_deep is reported as a side line")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     args = ap.parse_args()
@@ -145,8 +188,14 @@ def main():
     B, F, T, D = args.batch, 40, args.T, 128
 
     torch.manual_seed(42)
-    model = model_registry.create("phoneme_cnn", {"in_channels": 1, "embedding_dim": D,
-                                                  "use_attention": True, "dropout_rate": 0.1})
+    deep = args.model == "cnn_deep"
+    if deep:
+        model = model_registry.create("phoneme_cnn_deep", {"in_channels": 1, "embedding_dim": D,
+                                                           "use_attention": True, "dropout_rate": 0.2,
+                                                           "hidden_dims": DEEP_DIMS})
+    else:
+        model = model_registry.create("phoneme_cnn", {"in_channels": 1, "embedding_dim": D,
+                                                      "use_attention": True, "dropout_rate": 0.1})
     model = model.to(dev).train()
     ddp.broadcast_module(model)
     opt = FusedAdam(model.parameters(), lr=3e-4, weight_decay=1e-4)
@@ -201,7 +250,7 @@ def main():
 
     ms_step = 1000.0 * el / args.steps
     value = world * B * args.steps / el
-    costs = kernel_costs(B, F, T, D)
+    costs = deep_kernel_costs(B, F, T) if deep else kernel_costs(B, F, T, D)
     roof = None
     kernels = {}
     if prof:
@@ -225,20 +274,20 @@ def main():
         roof["algorithmic_flops_per_launch"] = fl
         roof["algorithmic_bytes_per_launch"] = by
         roof["avg_launch_ms"] = round(avg_s * 1000.0, 4)
-    sf, sb = step_cost(B, F, T, D)
+    sf, sb = deep_step_cost(B, F, T, D) if deep else step_cost(B, F, T, D)
     step_roof = {"flops_per_step": sf, "bytes_per_step": sb,
                  "mfma_fraction": round(sf / (el / args.steps) / (FP32_PEAK_TFLOPS * 1e12), 4),
                  "hbm_fraction": round(sb / (el / args.steps) / (HBM_PEAK_GBS * 1e9), 4)}
 
     cpu = None
-    if world == 1 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline and not deep:
         try:
             cpu = cpu_baseline()
         except Exception as exc:  # pragma: no cover - reported, never fatal for the GPU number
             cpu = {"error": repr(exc)}
 
     out = {
-        "metric": METRIC,
+        "metric": METRIC if not deep else f"MFCC-samples/sec per train step (cnn_deep, batch {B})",
         "value": round(value, 1),
         "unit": "samples/s",
         "n_gpus": world,
@@ -249,8 +298,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp32",
-        "data": "synthetic N(0,1) MFCC [B,1,40,T], random-init cnn_small (seed 42)",
-        "config": {"workload": "cnn_small contrastive train step: fwd + SupCon(T=0.15) + bwd + "
+        "data": f"synthetic N(0,1) MFCC [B,1,40,T], random-init {args.model} (seed 42)",
+        "config": {"workload": f"{args.model} contrastive train step: fwd + SupCon(T=0.15) + bwd + "
                                "grad all-reduce + Adam(lr 3e-4, wd 1e-4)",
                    "per_gpu_batch": B, "global_batch": B * world, "n_mfcc": F, "T": T,
                    "embedding_dim": D, "parallelism": f"dp{world}"},

@@ -203,15 +203,23 @@ void wgrad3x3_geometry(int B, int H, int W, int cin, int cout, WgradArgs* a) {
     a->MT = MT; a->NPM = NPM; a->NPC = NPC;
     const int NB = NPM * MT, CB = NPC * MT;
     const int KS = MT == 32 ? 2 : 4;
-    // chunk shape: whole rows (DRAM bursts stay >= 128 B; the halo rows of consecutive chunks of a
-    // slice are L2 hits), columns split only for very wide rows; as many rows as fit ~76 KB of LDS.
+    // chunk shape: minimise staged elements (incl. halo) plus padded MFMA work within ~76 KB of
+    // LDS (measured: whole-row chunks with taller halos were slower — staging latency dominates)
     const size_t lds_cap = 76 * 1024;
-    int nseg = (W + 127) / 128;
-    int bestCW = ((W + nseg - 1) / nseg + 3) / 4 * 4;
-    int bestR = 1;
-    for (int R = 1; R <= std::min(H, 16); ++R) {
-        size_t lds = ((size_t)NB * (R * bestCW + 1) + (size_t)CB * ((R + 2) * (bestCW + 2) + 1)) * 4;
-        if (lds <= lds_cap && R * bestCW <= 512) bestR = R;
+    int bestR = 1, bestCW = KS;
+    double best = 1e300;
+    const int wmax = (W + 3) / 4 * 4;
+    for (int cw = 4; cw <= std::max(4, std::min(wmax, 128)); cw += 4) {
+        for (int R = 1; R <= std::min(H, 16); ++R) {
+            int P = R * cw;
+            size_t lds = ((size_t)NB * (P + 1) + (size_t)CB * ((R + 2) * (cw + 2) + 1)) * 4;
+            if (lds > lds_cap || P > 512) continue;
+            double nch = (double)((W + cw - 1) / cw) * ((H + R - 1) / R);
+            double staged = nch * ((double)NB * P + (double)CB * (R + 2) * (cw + 2));
+            double compute = nch * P * 0.5 * NB * CB / 64.0;  // position-MACs incl. padding waste
+            double cost = staged * 4.0 + compute;
+            if (cost < best) { best = cost; bestR = R; bestCW = cw; }
+        }
     }
     a->R = bestR;
     a->CW = bestCW;

@@ -50,7 +50,19 @@ def main(name="cnn_small_T200", cfg=None):
     for l in range(6, 0, -1):
         ref = keep[f"z{l}"].grad
         got = plan.region(ws, f"dz{l}", ref.shape).cpu().double()
-        print(f"dz{l}", "err %.3e  max %.3e" % ((got - ref).abs().max().item(), ref.abs().max().item()))
+        err = (got - ref).abs()
+        print(f"dz{l}", "err %.3e  max %.3e" % (err.max().item(), ref.abs().max().item()))
+        if l in (2, 4):  # MaxPool2 follows: are the largest errors at near-tied 2x2 windows?
+            r = torch.relu(keep[f"z{l}"].detach())
+            Hp, Wp = r.shape[2] // 2, r.shape[3] // 2
+            win = r[:, :, :2 * Hp, :2 * Wp].reshape(r.shape[0], r.shape[1], Hp, 2, Wp, 2)
+            win = win.permute(0, 1, 2, 4, 3, 5).reshape(r.shape[0], r.shape[1], Hp, Wp, 4)
+            top = win.topk(2, dim=-1).values
+            gap = (top[..., 0] - top[..., 1])
+            e2 = err[:, :, :2 * Hp, :2 * Wp].reshape(r.shape[0], r.shape[1], Hp, 2, Wp, 2).amax(dim=(3, 5))
+            idx = e2.flatten().topk(5).indices
+            print(f"   worst dz{l} windows: err", [f"{e2.flatten()[i].item():.2e}" for i in idx],
+                  "top-2 gap", [f"{gap.flatten()[i].item():.2e}" for i in idx])
     for (k, p), g in zip(m.named_parameters(), grads):
         ref = sd[k].grad
         print(f"grad {k:32s} relerr %.3e  max %.3e" % ((g.cpu().double() - ref).abs().max().item() / (ref.abs().max().item() + 1e-30), ref.abs().max().item()))

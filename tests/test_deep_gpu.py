@@ -118,7 +118,8 @@ def test_deep_matches_float64_torch(residual, T):
     ref.train()
     xr = x.double().requires_grad_(False)
     er = _torch_reference(ref, xr, [k.double() for k in masks])
-    lr_ = SupervisedContrastiveLoss(temperature=0.15)(er, labels)
+    from oracle import torch_port as tp
+    lr_ = tp.supcon(er, labels, 0.15, 0.07)
     lr_.backward()
     assert (e.detach().cpu().double() - er.detach()).abs().max() < 1e-5
     assert abs(loss.item() - lr_.item()) < 1e-4
