@@ -295,8 +295,8 @@ int launch_conv3x3_dma(int pro, int epi, ConvArgs a, hipStream_t s) {
 #define PCX_DMA_ALL(P_, E_) PCX_DMA_V(1, 4, P_, E_) PCX_DMA_V(2, 2, P_, E_)
     PCX_DMA_ALL(PRO_RAW, EPI_FWD)
     PCX_DMA_ALL(PRO_BNRELU, EPI_FWD)
-    PCX_DMA_ALL(PRO_BNBWD, EPI_BWD_RELU)
-    PCX_DMA_ALL(PRO_BNBWD, EPI_BWD_POOL)
+    PCX_DMA_ALL(PRO_RAW, EPI_BWD_RELU)   // data gradient on the dy materialised by the wgrad
+    PCX_DMA_ALL(PRO_RAW, EPI_BWD_POOL)
 #undef PCX_DMA_ALL
 #undef PCX_DMA_V
 #undef PCX_DMA_CK

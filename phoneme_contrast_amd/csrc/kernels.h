@@ -81,11 +81,15 @@ struct WgradArgs {
     const float* drop;
     int srcH, srcW;
     float* part;          // [nslice][cout][cin][9]
+    float* dy_out;        // optional: dy = BNBWD(dz, y) written here (consumed by the data grad)
     int R, CW, nseg, nrb, nchunks, per_slice, nslice;
     int MT, NPM, NPC;     // MFMA tile (16 or 32), tiles per block along cout / cin
 };
 int launch_wgrad3x3(int pro, WgradArgs a, hipStream_t s);
 void wgrad3x3_geometry(int B, int H, int W, int cin, int cout, WgradArgs* a);
+// software-pipelined variant (wgrad_pipe.hip, the default): prologues PRO_RAW / PRO_BNRELU
+int launch_wgrad_pipe(int pro, WgradArgs a, hipStream_t s);
+void wgrad_pipe_geometry(int B, int H, int W, int cin, int cout, WgradArgs* a);
 
 // first-layer (Cin = 1) weight gradient
 struct Wgrad1Args {

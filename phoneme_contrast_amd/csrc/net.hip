@@ -61,7 +61,8 @@ int build_small(Plan& p) {
             L.wp = p.carve("wp", (size_t)9 * L.cin * L.cout * 4);
             L.wpd = p.carve("wpd", (size_t)9 * L.cin * L.cout * 4);
             L.nblk = (int)conv3x3_nblk(B, L.H, L.W, L.cout);
-            wgrad3x3_geometry(B, L.H, L.W, L.cin, L.cout, &L.wg);
+            if (p.wgrad_impl == 0) wgrad_pipe_geometry(B, L.H, L.W, L.cin, L.cout, &L.wg);
+            else wgrad3x3_geometry(B, L.H, L.W, L.cin, L.cout, &L.wg);
             wg = std::max(wg, (size_t)L.wg.nslice * L.cout * L.cin * 9);
         } else {
             L.nblk = conv1_nblk(B, L.H, &p.conv1_rows);
@@ -80,6 +81,11 @@ int build_small(Plan& p) {
     p.P6 = H5 * W5;
     stat = std::max(stat, (size_t)2 * p.C6 * B);
     p.stat_part = p.carve("stat_part", stat * 4);
+    {
+        size_t dymax = 0;
+        for (int l = 2; l <= 6; ++l) dymax = std::max(dymax, (size_t)B * p.L[l].cout * p.L[l].H * p.L[l].W);
+        p.dyb = p.carve("dy", dymax * 4);
+    }
     p.wg_part = p.carve("wg_part", wg * 4);
     const int D = p.D, K = p.C6;
     p.pooled = p.carve("pooled", (size_t)B * K * 4);
@@ -320,7 +326,11 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
                 w.srcH = L.H; w.srcW = L.W;
                 pro = PRO_RAW;
             }
-            { Scope sc(&p.prof, s, "wgrad", l); RC(launch_wgrad3x3(pro, w, s)); }
+            if (p.dma) w.dy_out = at<float>(ws, p.dyb);
+            {
+                Scope sc(&p.prof, s, "wgrad", l);
+                RC(p.wgrad_impl == 0 ? launch_wgrad_pipe(pro, w, s) : launch_wgrad3x3(pro, w, s));
+            }
             { Scope sc(&p.prof, s, "wgrad_reduce", l); RC(launch_sum_slices(wgp, w.nslice, (int64_t)L.cout * L.cin * 9, G[p_conv_w(l)], s)); }
         }
         // ---- data gradient -> dz of the previous BN (through ReLU / MaxPool / Dropout2d)
@@ -335,6 +345,7 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
             c.src = at<float>(ws, L.dz);
             c.src2 = at<float>(ws, L.y);
             c.cf_in = at<float4>(ws, L.cfb);
+            if (p.dma) c.src = at<float>(ws, p.dyb);  // dy materialised by the weight gradient
             c.srcH = L.H; c.srcW = L.W;
             c.wpack = at<float>(ws, L.wpd);
             c.out = dzp;
@@ -349,7 +360,7 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
             {
                 Scope sc(&p.prof, s, "conv_dgrad", l);
                 const int epi = L.pooled_in ? EPI_BWD_POOL : EPI_BWD_RELU;
-                RC(p.dma ? launch_conv3x3_dma(PRO_BNBWD, epi, c, s) : launch_conv3x3(PRO_BNBWD, epi, c, s));
+                RC(p.dma ? launch_conv3x3_dma(PRO_RAW, epi, c, s) : launch_conv3x3(PRO_BNBWD, epi, c, s));
             }
             RC(bwd_finalize(l - 1, nblk, (double)B * Lp.H * Lp.W));
         }
@@ -397,6 +408,8 @@ extern "C" void* pcx_net_create(const pcx_net_config* cfg, int64_t B, int64_t F,
     {
         const char* impl = getenv("PCX_CONV");  // A/B switch for measurements: "legacy" = conv.hip
         p->dma = !(impl && strcmp(impl, "legacy") == 0);
+        const char* wg = getenv("PCX_WGRAD");  // "dma" / "legacy" for A/B measurements
+        p->wgrad_impl = (!p->dma || (wg && strcmp(wg, "legacy") == 0)) ? 2 : 0;
     }
     int rc = PCX_EINVAL;
     if (cfg->kind == PCX_NET_CNN_SMALL) rc = build_small(*p);

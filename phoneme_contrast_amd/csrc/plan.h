@@ -84,12 +84,14 @@ struct Plan {
     int conv1_nblk, conv1_rows;
     int wg1_nslice, wg1_rows;
     size_t stat_part, stat_bytes;   // shared scratch for BN partials
+    size_t dyb;                     // dy of the layer being back-propagated (DMA path)
     size_t wg_part, wg_bytes;       // shared scratch for weight-gradient partials
     size_t pooled, att, h, cfp, cfpb, norm, dzp, dh, dpooled, wt, hp_dz, hp_dzx, hp_dwa, hp_dba;
     size_t total;
     std::vector<Region> regions;
     int nparams, nbn, ndrop, drop_ch[4];
     bool dma;                       // LDS-DMA conv path (default); PCX_CONV=legacy selects conv.hip
+    int wgrad_impl;                 // 0 pipelined (default), 2 legacy wgrad.hip (PCX_WGRAD=legacy)
     mutable Profiler prof;
 
     size_t carve(const char* name, size_t bytes) {

@@ -134,6 +134,9 @@ __global__ __launch_bounds__(256) void wgrad3x3_kernel(WgradArgs a) {
                 const float4 cf = a.cf_dy[n0 + n];
                 v[u] = ok ? cf.x * (dz - cf.y - (y - cf.w) * cf.z) : 0.f;
                 dst[u] = in ? n * PS + pos : -1;
+                // the first cin-group also materialises dy for the data-gradient conv (which then
+                // reads one tensor instead of recomputing the BN backward from two)
+                if (a.dy_out && c0 == 0 && ok) a.dy_out[o] = v[u];
             }
 #pragma unroll
             for (int u = 0; u < U; ++u)

@@ -18,4 +18,4 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -f csv -d "$ROOT/$OUT/pmc_fetch" -o
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -f csv -d "$ROOT/$OUT/pmc_write" -o run -- \
     python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing \
     > /dev/null 2> "$ROOT/$OUT/pmc_write.err"
-find "$OUT" -name "*.csv" | head -50
+python3 "$ROOT/scripts/pmc_summary.py" "$OUT" "$ROOT/$OUT/pmc_traffic.json" "$ROOT/$OUT/trace_layers.json" > /dev/null
