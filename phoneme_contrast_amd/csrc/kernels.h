@@ -90,6 +90,9 @@ void wgrad3x3_geometry(int B, int H, int W, int cin, int cout, WgradArgs* a);
 // software-pipelined variant (wgrad_pipe.hip, the default): prologues PRO_RAW / PRO_BNRELU
 int launch_wgrad_pipe(int pro, WgradArgs a, hipStream_t s);
 void wgrad_pipe_geometry(int B, int H, int W, int cin, int cout, WgradArgs* a);
+// sliding-row-window variant (wgrad_win.hip, the default): prologues PRO_RAW / PRO_BNRELU
+int launch_wgrad_win(int pro, WgradArgs a, hipStream_t s);
+void wgrad_win_geometry(int B, int H, int W, int cin, int cout, WgradArgs* a);
 
 // first-layer (Cin = 1) weight gradient
 struct Wgrad1Args {

@@ -91,7 +91,7 @@ struct Plan {
     std::vector<Region> regions;
     int nparams, nbn, ndrop, drop_ch[4];
     bool dma;                       // LDS-DMA conv path (default); PCX_CONV=legacy selects conv.hip
-    int wgrad_impl;                 // 0 pipelined (default), 2 legacy wgrad.hip (PCX_WGRAD=legacy)
+    int wgrad_impl;                 // 0 row window (default), 1 pipelined chunks, 2 wgrad.hip (PCX_WGRAD)
     mutable Profiler prof;
 
     size_t carve(const char* name, size_t bytes) {

@@ -18,7 +18,7 @@ DGRAD = [f"conv_dgrad_L{l}" for l in range(6, 1, -1)]
 # kernel family (name up to '<' / '(') -> layer labels in per-step dispatch order
 ORDER = {
     "conv3x3_dma_kernel": FWD + DGRAD,
-    "wgrad_dma_kernel": [f"wgrad_L{l}" for l in range(6, 1, -1)],
+    "wgrad_pipe_kernel": [f"wgrad_L{l}" for l in range(6, 1, -1)],
     "bn_relu_pool_kernel": ["bn_relu_pool_L3", "bn_relu_pool_L5"],
     "conv1_fwd_kernel": ["conv1_fwd_L1"],
     "wgrad1_kernel": ["wgrad_L1"],
