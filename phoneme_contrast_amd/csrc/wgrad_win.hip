@@ -25,14 +25,6 @@ namespace {
 constexpr int U = 8;            // elements per thread per staging unit
 constexpr int ZERO = -0x40000;  // element outside the sample: stored as 0
 
-__device__ __forceinline__ int fdiv(int n, int d, float inv) {  // n / d for 0 <= n < 2^22
-    int q = (int)((float)n * inv);
-    int r = n - q * d;
-    if (r < 0) --q;
-    else if (r >= d) ++q;
-    return q;
-}
-
 template <int MT>
 struct Mf;
 template <>
@@ -60,7 +52,6 @@ struct Mf<16> {
 // sample column w0 - 1 + jj for jj < CW + 2)
 struct Geo {
     int CW, DS, XS, XSP, ndy, nx, NU, dyslot, xslot, xbase;
-    float invCW, invXS;
 };
 
 struct Unit {
@@ -70,43 +61,79 @@ struct Unit {
     int o[U];     // dy: offset inside the sample's [cout][H][W] block (dy_out)
 };
 
-// one unit of the staging of (dy row rdy into dy slot ds) and (x row rx into x slot xs_);
-// rdy < 0: no dy row; rx outside [0, H): the x row is written as zeros
-__device__ __forceinline__ void load_unit(const WgradArgs& a, const Geo& g, Unit& un, int u, int b, int w0, int rdy,
-                                          int ds, int rx, int xs_, int n0, int c0, int tid) {
-    const int64_t HW = (int64_t)a.H * a.W;
+// Staging cursor: element e = tid + 256*k of the flattened [dy row: NB x CW | x row: CB x XS]
+// image, advanced incrementally (no divisions in the pipelined loop).
+struct Cursor {
+    int e, n, j, c, jj;
+};
+
+struct Steps {
+    int e0, n0, j0, c0, jj0;  // this thread's first dy element and first x element
+    int dn, dj, dc, djj;      // advance per 256 elements
+};
+
+__device__ __forceinline__ Steps make_steps(const Geo& g, int tid) {
+    Steps st;
+    st.e0 = tid;
+    st.n0 = tid / g.CW;
+    st.j0 = tid - st.n0 * g.CW;
+    const int k = g.ndy > tid ? (g.ndy - tid + 255) / 256 : 0;  // first element index >= ndy
+    const int ex = tid + 256 * k - g.ndy;
+    st.c0 = ex / g.XS;
+    st.jj0 = ex - st.c0 * g.XS;
+    st.dn = 256 / g.CW;
+    st.dj = 256 - st.dn * g.CW;
+    st.dc = 256 / g.XS;
+    st.djj = 256 - st.dc * g.XS;
+    return st;
+}
+
+__device__ __forceinline__ void reset(Cursor& cu, const Steps& st) {
+    cu.e = st.e0;
+    cu.n = st.n0;
+    cu.j = st.j0;
+    cu.c = st.c0;
+    cu.jj = st.jj0;
+}
+
+// one unit (U elements) of the staging of (dy row rdy into dy slot ds) and (x row rx into x slot
+// xs_); rdy < 0: no dy row; rx outside [0, H): the x row is written as zeros
+__device__ __forceinline__ void load_unit(const WgradArgs& a, const Geo& g, const Steps& st, Cursor& cu, Unit& un,
+                                          const float* dzb, const float* yb, const float* xb, int w0, int rdy,
+                                          int ds, int rx, int xs_, int n0) {
+    const int HW = a.H * a.W;
+    const int wlim = a.W - 1 - w0;  // last valid strip column
+    const bool rxok = rx >= 0 && rx < a.H;
 #pragma unroll
     for (int i = 0; i < U; ++i) {
-        const int e = tid + 256 * (u * U + i);
         un.dst[i] = -1;
         un.code[i] = ZERO;
         un.o[i] = 0;
         un.va[i] = 0.f;
         un.vb[i] = 0.f;
-        if (e < g.ndy) {
+        if (cu.e < g.ndy) {
             if (rdy >= 0) {
-                const int n = fdiv(e, g.CW, g.invCW);
-                const int j = e - n * g.CW;
-                const int w = w0 + j;
-                const int o = (n0 + n) * (int)HW + rdy * a.W + min(w, a.W - 1);
-                const int64_t go = (int64_t)b * a.cout * HW + o;
-                un.va[i] = a.dz[go];
-                un.vb[i] = a.y[go];
+                const int o = (n0 + cu.n) * HW + rdy * a.W + w0 + min(cu.j, wlim);
+                un.va[i] = dzb[o];
+                un.vb[i] = yb[o];
                 un.o[i] = o;
-                un.dst[i] = ds * g.dyslot + n * g.DS + j;
-                un.code[i] = w < a.W ? n : ZERO;
+                un.dst[i] = ds * g.dyslot + cu.n * g.DS + cu.j;
+                un.code[i] = cu.j <= wlim ? cu.n : ZERO;
             }
-        } else if (e - g.ndy < g.nx) {
-            const int ex = e - g.ndy;
-            const int c = fdiv(ex, g.XS, g.invXS);
-            const int jj = ex - c * g.XS;
-            const int w = w0 - 1 + jj;
-            const bool ok = rx >= 0 && rx < a.H && w >= 0 && w < a.W;
-            if (ok)
-                un.va[i] = a.src[(((int64_t)b * a.cin + c0 + c) * a.H + rx) * a.W + w];
-            un.dst[i] = g.xbase + xs_ * g.xslot + c * g.XSP + jj;
-            un.code[i] = ok ? -(c + 1) : ZERO;
+            cu.n += st.dn;
+            cu.j += st.dj;
+            if (cu.j >= g.CW) { cu.j -= g.CW; ++cu.n; }
+        } else if (cu.e - g.ndy < g.nx) {
+            const int w = w0 - 1 + cu.jj;
+            const bool ok = rxok && w >= 0 && w < a.W;
+            if (ok) un.va[i] = xb[(cu.c * a.H + rx) * a.W + w];
+            un.dst[i] = g.xbase + xs_ * g.xslot + cu.c * g.XSP + cu.jj;
+            un.code[i] = ok ? -(cu.c + 1) : ZERO;
+            cu.c += st.dc;
+            cu.jj += st.djj;
+            if (cu.jj >= g.XS) { cu.jj -= g.XS; ++cu.c; }
         }
+        cu.e += 256;
     }
 }
 
@@ -141,18 +168,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int NB = a.NPM * MT, CB = a.NPC * MT;
     Geo g;
+    // LDS row strides chosen bank-conflict free for the MFMA operand reads (ds_read_b32 serves
+    // lanes 0-31 and 32-63 as groups of 32 banks): MT = 32 reads 32 channels (li) per group ->
+    // odd stride; MT = 16 reads 16 channels x 2 pixels (kg) per group -> stride = 2 * odd
     g.CW = a.CW;
-    g.DS = a.CW + 1;
+    g.DS = MT == 32 ? a.CW + 1 : a.CW + 2;
     g.XS = a.CW + 2;
-    g.XSP = a.CW + 3;
+    g.XSP = MT == 32 ? a.CW + 3 : a.CW + 2;
     g.ndy = NB * a.CW;
     g.nx = CB * g.XS;
     g.NU = (g.ndy + g.nx + 256 * U - 1) / (256 * U);
     g.dyslot = NB * g.DS;
     g.xslot = CB * g.XSP;
     g.xbase = 2 * g.dyslot;
-    g.invCW = 1.f / a.CW;
-    g.invXS = 1.f / g.XS;
     float4* cfd = reinterpret_cast<float4*>(smem);  // [NB]
     float4* cfx = cfd + NB;                          // [CB]
     float* lds = smem + 4 * (NB + CB);
@@ -192,6 +220,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
         for (int t = 0; t < 9; ++t) acc[k][t] = Acc{0.f};
 
     const bool write_dy = a.dy_out != nullptr && c0 == 0;
+    const Steps st = make_steps(g, tid);
+    Cursor cu;
     const int NK = a.CW / KS;
     const int S = max(1, NK / (g.NU + 1));  // k-steps between staging actions
     const int t0 = slice * a.per_slice, t1 = min(a.nchunks, t0 + a.per_slice);
@@ -200,16 +230,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
         const int b = task / a.nseg;
         const int w0 = (task - b * a.nseg) * a.CW;
         float* dyo = write_dy ? a.dy_out + (int64_t)b * a.cout * HW : nullptr;
+        const float* dzb = a.dz + (int64_t)b * a.cout * HW;
+        const float* yb = a.y + (int64_t)b * a.cout * HW;
+        const float* xb = a.src + ((int64_t)b * a.cin + c0) * HW;
         // ---- prologue: x rows -1, 0, 1 -> slots 0, 1, 2 and dy row 0 -> dy slot 0
-        for (int u = 0; u < g.NU; ++u) {
-            load_unit(a, g, un, u, b, w0, 0, 0, -1, 0, n0, c0, tid);
-            store_unit<PRO>(un, lds, cfd, cfx, dyo);
-        }
-        for (int q = 0; q <= 1; ++q)
+        for (int q = -1; q <= 1; ++q) {
+            reset(cu, st);
             for (int u = 0; u < g.NU; ++u) {
-                load_unit(a, g, un, u, b, w0, -1, 0, q, q + 1, n0, c0, tid);
+                load_unit(a, g, st, cu, un, dzb, yb, xb, w0, q == -1 ? 0 : -1, 0, q, q + 1, n0);
                 store_unit<PRO>(un, lds, cfd, cfx, dyo);
             }
+        }
         __syncthreads();
         for (int r = 0; r < a.H; ++r) {
             const bool pre = r + 1 < a.H;  // stage dy row r+1 and x row r+2 (zeros at r+2 == H)
@@ -219,6 +250,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
             const float* xr2 = lds + g.xbase + ((r + 2) & 3) * g.xslot;
             int u_next = 0;
             bool pending = false;
+            reset(cu, st);
             for (int ks = 0; ks < NK; ++ks) {
                 if (pre && (ks % S) == 0) {
                     if (pending) {
@@ -226,7 +258,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
                         pending = false;
                     }
                     if (u_next < g.NU) {
-                        load_unit(a, g, un, u_next, b, w0, r + 1, (r + 1) & 1, r + 2, (r + 3) & 3, n0, c0, tid);
+                        load_unit(a, g, st, cu, un, dzb, yb, xb, w0, r + 1, (r + 1) & 1, r + 2, (r + 3) & 3, n0);
                         ++u_next;
                         pending = true;
                     }
@@ -246,7 +278,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
             if (pre) {
                 if (pending) store_unit<PRO>(un, lds, cfd, cfx, dyo);
                 for (; u_next < g.NU; ++u_next) {
-                    load_unit(a, g, un, u_next, b, w0, r + 1, (r + 1) & 1, r + 2, (r + 3) & 3, n0, c0, tid);
+                    load_unit(a, g, st, cu, un, dzb, yb, xb, w0, r + 1, (r + 1) & 1, r + 2, (r + 3) & 3, n0);
                     store_unit<PRO>(un, lds, cfd, cfx, dyo);
                 }
             }
@@ -266,8 +298,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
             }
 }
 
-size_t win_lds(int NB, int CB, int CW) {
-    return ((size_t)2 * NB * (CW + 1) + (size_t)4 * CB * (CW + 3) + 4 * (size_t)(NB + CB)) * 4;
+size_t win_lds(int MT, int NB, int CB, int CW) {
+    const int ds = MT == 32 ? CW + 1 : CW + 2, xsp = MT == 32 ? CW + 3 : CW + 2;
+    return ((size_t)2 * NB * ds + (size_t)4 * CB * xsp + 4 * (size_t)(NB + CB)) * 4;
 }
 
 }  // namespace
@@ -290,7 +323,7 @@ void wgrad_win_geometry(int B, int H, int W, int cin, int cout, WgradArgs* a) {
     double best = 1e300;
     int bCW = KS;
     for (int cw = KS; cw <= std::max(KS, std::min(128, (W + KS - 1) / KS * KS)); cw += KS) {
-        if (win_lds(NB, CB, cw) > cap) continue;
+        if (win_lds(MT, NB, CB, cw) > cap) continue;
         const int nseg = (W + cw - 1) / cw;
         const double mfma = (double)pw * 9 * cw * (MT == 32 ? 32.0 : 8.0);
         const double lines_dy = cw * 4.0 / 128.0 + 1.0, lines_x = (cw + 2) * 4.0 / 128.0 + 1.0;
@@ -319,7 +352,7 @@ int launch_wgrad_win(int pro, WgradArgs a, hipStream_t s) {
     PCX_CHECK_ARG((int64_t)a.cout * a.H * a.W < ((int64_t)1 << 31), "wgrad_win: sample block too large");
     const int pw = a.NPM * a.NPC / 4;
     PCX_CHECK_ARG(pw * 4 == a.NPM * a.NPC && pw >= 1 && pw <= 2, "wgrad_win: bad tile split");
-    const size_t smem = win_lds(NB, CB, a.CW);
+    const size_t smem = win_lds(a.MT, NB, CB, a.CW);
     PCX_CHECK_ARG(smem <= 160 * 1024, "wgrad_win: LDS %zu too large", smem);
     dim3 grid((unsigned)(((a.nslice + 7) / 8) * 8 * ((a.cout / NB) * (a.cin / CB))));
 #define PCX_WGW(MT_, PW_, P_)                                                                    \
