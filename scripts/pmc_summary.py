@@ -19,6 +19,8 @@ DGRAD = [f"conv_dgrad_L{l}" for l in range(6, 1, -1)]
 ORDER = {
     "conv3x3_dma_kernel": FWD + DGRAD,
     "wgrad_pipe_kernel": [f"wgrad_L{l}" for l in range(6, 1, -1)],
+    "wgrad_win_kernel": [f"wgrad_L{l}" for l in range(6, 1, -1)],
+    "wgrad3x3_kernel": [f"wgrad_L{l}" for l in range(6, 1, -1)],
     "bn_relu_pool_kernel": ["bn_relu_pool_L3", "bn_relu_pool_L5"],
     "conv1_fwd_kernel": ["conv1_fwd_L1"],
     "wgrad1_kernel": ["wgrad_L1"],
@@ -93,5 +95,28 @@ def main(prof_dir, out_json, out_dur=None):
         print(json.dumps(d, indent=1))
 
 
+def stalls(csv_path, out_json):
+    """Median of every counter of one --pmc pass, per layer label (analysis aid)."""
+    names = sorted({r["Counter_Name"] for r in _rows(csv_path)})
+    res = defaultdict(dict)
+    for c in names:
+        for lab, vals in counters(csv_path, c).items():
+            res[lab][c] = sorted(vals)[len(vals) // 2]
+    for lab, d in res.items():
+        if d.get("SQ_WAVE_CYCLES"):
+            for c in list(d):
+                if c.startswith("SQ_WAIT") or c.startswith("SQ_ACTIVE"):
+                    d[c + "/WAVE_CYCLES"] = round(d[c] / d["SQ_WAVE_CYCLES"], 4)
+        if d.get("GRBM_GUI_ACTIVE") and "SQ_VALU_MFMA_BUSY_CYCLES" in d:
+            # MFMA busy per SIMD: 1024 SIMDs x (GRBM_GUI_ACTIVE / 8 XCDs)
+            d["mfma_busy_frac"] = round(d["SQ_VALU_MFMA_BUSY_CYCLES"] / (128.0 * d["GRBM_GUI_ACTIVE"]), 4)
+    with open(out_json, "w") as fo:
+        json.dump(res, fo, indent=1, sort_keys=True)
+    print(json.dumps(res, indent=1, sort_keys=True))
+
+
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    if sys.argv[1] == "--stalls":
+        stalls(sys.argv[2], sys.argv[3])
+    else:
+        main(*sys.argv[1:4])
