@@ -19,6 +19,18 @@ int hip_status(hipError_t e, const char* what) {
     return PCX_EHIP;
 }
 
+int num_cus() {  // compute units of the current device (cached per device; 256 on MI355X)
+    static int cache[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cache[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cache[dev] = n;
+    }
+    return cache[dev];
+}
+
 }  // namespace pcx
 
 extern "C" int pcx_version(void) { return 100; }

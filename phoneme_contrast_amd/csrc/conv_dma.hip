@@ -79,8 +79,14 @@ __device__ __forceinline__ void issue_wts(const ConvArgs& a, unsigned wts, int c
     }
 }
 
+// Occupancy: latency hiding here comes from co-resident blocks (4 waves of a block share one
+// chunk barrier), so the LDS footprint is sized for DMA_OCC(WM) blocks per CU and the register
+// budget for as many waves per SIMD (measured: 4 resident blocks run the same GEMM at 72 % of the
+// fp32 MFMA peak where 2 reach 60 %).
+constexpr int dma_occ(int wm) { return wm == 2 ? 4 : 3; }
+
 template <int WM, int WN, int VEC, int PRO, int EPI, int CK>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv3x3_dma_kernel(ConvArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_occ(WM)))) void conv3x3_dma_kernel(ConvArgs a) {
     constexpr int COUT_T = 32 * WM;
     constexpr int BP = 4 * WN * 32;
     constexpr int NSRC = (PRO == PRO_BNBWD) ? 2 : 1;
@@ -168,39 +174,54 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
 #pragma unroll
             for (int s = 0; s < CK / 2; ++s) cf[s] = cft[c0 + 2 * s + h];
         }
+        // (tap, s) steps, software-pipelined by hand: the LDS operands of step i+1 are requested
+        // before the MFMAs of step i (sched_barrier keeps the scheduler from sinking the reads
+        // next to their use, which exposes the LDS latency in front of the MFMAs)
+        constexpr int NST = 9 * (CK / 2);
+        float av[2][WM], rv[2][WN], rv2[2][WN];
+        auto load = [&](int st, float (&a_)[WM], float (&r_)[WN], float (&r2_)[WN]) {
+            const int tap = st / (CK / 2), s = st % (CK / 2);
+            const int toff = (tap / 3 - 1) * a.W + (tap % 3 - 1);
 #pragma unroll
-        for (int tap = 0; tap < 9; ++tap) {
-            const int dh = tap / 3 - 1, dw = tap % 3 - 1;
-            const int toff = dh * a.W + dw;
+            for (int mi = 0; mi < WM; ++mi) a_[mi] = wts[(tap * CK + 2 * s + h) * COUT_T + mi * 32 + l32];
 #pragma unroll
-            for (int s = 0; s < CK / 2; ++s) {
-                float av[WM], bv[WN];
-#pragma unroll
-                for (int mi = 0; mi < WM; ++mi)
-                    av[mi] = wts[(tap * CK + 2 * s + h) * COUT_T + mi * 32 + l32];
-#pragma unroll
-                for (int ni = 0; ni < WN; ++ni) {
-                    const int o = (2 * s + h) * PL + pixoff[ni] + toff;
-                    float v;
-                    if (PRO == PRO_RAW) {
-                        v = raw[o];
-                    } else if (PRO == PRO_BNRELU) {
-                        v = fmaxf(fmaf(raw[o], cf[s].x, cf[s].y), 0.f);
-                    } else {  // PRO_BNBWD: dy = a * (dz - mb - (y - mean) * mgi)
-                        v = cf[s].x * (raw[o] - cf[s].y - (raw[o + CK * PL] - cf[s].w) * cf[s].z);
-                    }
-                    bool ok = true;
-                    if (dh < 0) ok = ok && vup[ni];
-                    if (dh > 0) ok = ok && vdn[ni];
-                    if (dw < 0) ok = ok && vl[ni];
-                    if (dw > 0) ok = ok && vr[ni];
-                    bv[ni] = ok ? v : 0.f;
-                }
-#pragma unroll
-                for (int mi = 0; mi < WM; ++mi)
-#pragma unroll
-                    for (int ni = 0; ni < WN; ++ni) acc[mi][ni] = mfma32(av[mi], bv[ni], acc[mi][ni]);
+            for (int ni = 0; ni < WN; ++ni) {
+                const int o = (2 * s + h) * PL + pixoff[ni] + toff;
+                r_[ni] = raw[o];
+                if (PRO == PRO_BNBWD) r2_[ni] = raw[o + CK * PL];
             }
+        };
+        load(0, av[0], rv[0], rv2[0]);
+#pragma unroll
+        for (int st = 0; st < NST; ++st) {
+            const int cur = st & 1;
+            if (st + 1 < NST) load(st + 1, av[cur ^ 1], rv[cur ^ 1], rv2[cur ^ 1]);
+            __builtin_amdgcn_sched_barrier(0);
+            const int tap = st / (CK / 2), s = st % (CK / 2);
+            const int dh = tap / 3 - 1, dw = tap % 3 - 1;
+            float bv[WN];
+#pragma unroll
+            for (int ni = 0; ni < WN; ++ni) {
+                float v;
+                if (PRO == PRO_RAW) {
+                    v = rv[cur][ni];
+                } else if (PRO == PRO_BNRELU) {
+                    v = fmaxf(fmaf(rv[cur][ni], cf[s].x, cf[s].y), 0.f);
+                } else {  // PRO_BNBWD: dy = a * (dz - mb - (y - mean) * mgi)
+                    v = cf[s].x * (rv[cur][ni] - cf[s].y - (rv2[cur][ni] - cf[s].w) * cf[s].z);
+                }
+                bool ok = true;
+                if (dh < 0) ok = ok && vup[ni];
+                if (dh > 0) ok = ok && vdn[ni];
+                if (dw < 0) ok = ok && vl[ni];
+                if (dw > 0) ok = ok && vr[ni];
+                bv[ni] = ok ? v : 0.f;
+            }
+#pragma unroll
+            for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < WN; ++ni) acc[mi][ni] = mfma32(av[cur][mi], bv[ni], acc[mi][ni]);
+            __builtin_amdgcn_sched_barrier(0);
         }
     }
     __syncthreads();  // LDS is reused for the cross-wave statistics
@@ -247,7 +268,7 @@ __global__ __launch_bounds__(256) void bn_relu_pool_kernel(const float* __restri
 }  // namespace
 
 int conv3x3_dma_ck(int pro, int cout, int W, int NR, int cin) {
-    // largest K-chunk whose double-buffered raw image + weights fit ~76 KB (2 blocks per CU)
+    // largest K-chunk whose double-buffered raw image + weights let dma_occ blocks share a CU
     const int nsrc = pro == PRO_BNBWD ? 2 : 1;
     const int cout_t = cout == 32 ? 32 : 64;
     for (int ck = 8; ck >= 2; ck >>= 1) {
@@ -255,7 +276,7 @@ int conv3x3_dma_ck(int pro, int cout, int W, int NR, int cin) {
         size_t raw = (size_t)nsrc * ck * NR * W + 256;
         size_t wts = (size_t)9 * ck * cout_t + 256;
         size_t bytes = (2 * raw + 2 * wts + 4 * (size_t)cin + 2 * NR + 8) * 4;
-        if (bytes <= 76 * 1024) return ck;
+        if (bytes <= (size_t)160 * 1024 / dma_occ(cout == 32 ? 1 : 2)) return ck;
     }
     return 2;
 }

@@ -12,6 +12,7 @@ namespace pcx {
 // ---------------------------------------------------------------- error state (host)
 void set_error(const char* fmt, ...);
 int hip_status(hipError_t e, const char* what);
+int num_cus();  // compute units of the current device
 
 #define PCX_CHECK_ARG(cond, ...)                  \
     do {                                          \
