@@ -230,33 +230,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_occ(WM)
 
 // ------------------------------------------------------------------ BN + ReLU + MaxPool2 + Dropout2d
 // x[b,c,h,w] = drop[b,c] * max_{2x2} relu(y*s + t)  (reference block tail phoneme_cnn.py:40-43)
+// One block per group of PPB channel planes; thread = 4 pooled outputs of one row.  32-bit index
+// math only (int64 division per element made this kernel ALU-bound), paired loads when the
+// source rows are 8-byte aligned (even width).
+template <bool PAIR>
 __global__ __launch_bounds__(256) void bn_relu_pool_kernel(const float* __restrict__ y, const float4* __restrict__ cf,
                                                            const float* __restrict__ drop, float* __restrict__ x,
-                                                           int B, int C, int Hs, int Ws, int Hp, int Wp) {
-    const int64_t nq = (int64_t)B * C * Hp * ((Wp + 3) / 4);
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    const int Wq = (Wp + 3) / 4;
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nq; e += stride) {
-        const int q = (int)(e % Wq);
-        const int64_t r = e / Wq;           // (b*C + c)*Hp + h
-        const int hp = (int)(r % Hp);
-        const int64_t bc = r / Hp;
-        const int c = (int)(bc % C);
-        const float4 k = cf[c];
+                                                           int nplanes, int C, int Hs, int Ws, int Hp, int Wp, int ppb) {
+    const int Wq = (Wp + 3) / 4, nqp = Hp * Wq;
+    const int pbase = blockIdx.x * ppb;
+    const int tot = min(ppb, nplanes - pbase) * nqp;
+    for (int t = threadIdx.x; t < tot; t += blockDim.x) {
+        const int pl = t / nqp, rem = t - pl * nqp;
+        const int hp = rem / Wq, q = rem - hp * Wq;
+        const int bc = pbase + pl;
+        const float4 k = cf[bc % C];
         const float d = drop ? drop[bc] : 1.f;
-        const float* s0 = y + (bc * Hs + 2 * hp) * Ws;
+        const float* s0 = y + ((int64_t)bc * Hs + 2 * hp) * Ws;
         const float* s1 = s0 + Ws;
         float out[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int w = 4 * q + j;
             if (w < Wp) {
-                float m = fmaxf(fmaxf(fmaf(s0[2 * w], k.x, k.y), fmaf(s0[2 * w + 1], k.x, k.y)),
-                                fmaxf(fmaf(s1[2 * w], k.x, k.y), fmaf(s1[2 * w + 1], k.x, k.y)));
+                float u0, u1, v0, v1;
+                if (PAIR) {
+                    const float2 u = *reinterpret_cast<const float2*>(s0 + 2 * w);
+                    const float2 v = *reinterpret_cast<const float2*>(s1 + 2 * w);
+                    u0 = u.x; u1 = u.y; v0 = v.x; v1 = v.y;
+                } else {
+                    u0 = s0[2 * w]; u1 = s0[2 * w + 1]; v0 = s1[2 * w]; v1 = s1[2 * w + 1];
+                }
+                float m = fmaxf(fmaxf(fmaf(u0, k.x, k.y), fmaf(u1, k.x, k.y)),
+                                fmaxf(fmaf(v0, k.x, k.y), fmaf(v1, k.x, k.y)));
                 out[j] = d * fmaxf(m, 0.f);
             }
         }
-        float* dst = x + r * Wp + 4 * q;
+        float* dst = x + ((int64_t)bc * Hp + hp) * Wp + 4 * q;
         if ((Wp & 3) == 0) {
             st4(dst, make_float4(out[0], out[1], out[2], out[3]));
         } else {
@@ -329,9 +339,14 @@ int launch_conv3x3_dma(int pro, int epi, ConvArgs a, hipStream_t s) {
 int launch_bn_relu_pool(const float* y, const float4* cf, const float* drop, float* x, int B, int C,
                         int Hs, int Ws, hipStream_t s) {
     const int Hp = Hs / 2, Wp = Ws / 2;
-    const int64_t nq = (int64_t)B * C * Hp * ((Wp + 3) / 4);
-    const int blocks = (int)std::min<int64_t>(8192, std::max<int64_t>(1, (nq + 255) / 256));
-    bn_relu_pool_kernel<<<blocks, 256, 0, s>>>(y, cf, drop, x, B, C, Hs, Ws, Hp, Wp);
+    PCX_CHECK_ARG((int64_t)B * C < ((int64_t)1 << 31), "bn_relu_pool: too many planes");
+    const int nplanes = B * C, nqp = Hp * ((Wp + 3) / 4);
+    const int ppb = std::max(1, 1024 / std::max(1, nqp));  // ~1024 quads per block
+    const int blocks = ceil_div(nplanes, ppb);
+    if (Ws % 2 == 0)
+        bn_relu_pool_kernel<true><<<blocks, 256, 0, s>>>(y, cf, drop, x, nplanes, C, Hs, Ws, Hp, Wp, ppb);
+    else
+        bn_relu_pool_kernel<false><<<blocks, 256, 0, s>>>(y, cf, drop, x, nplanes, C, Hs, Ws, Hp, Wp, ppb);
     PCX_LAUNCH_CHECK("bn_relu_pool_kernel");
     return PCX_OK;
 }

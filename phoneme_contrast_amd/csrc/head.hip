@@ -285,19 +285,50 @@ __global__ __launch_bounds__(256) void proj_bwd_data_kernel(ProjArgs a) {
     }
 }
 
-// dW[d][k] = sum_b dh[b][d] pooled[b][k] ; db[d] = sum_b dh[b][d] ; one block per d
-__global__ __launch_bounds__(256) void proj_bwd_weight_kernel(ProjArgs a) {
-    __shared__ double red[256];
-    const int d = blockIdx.x, tid = threadIdx.x;
-    for (int k = tid; k < a.K; k += blockDim.x) {
-        float s = 0.f;
-        for (int b = 0; b < a.B; ++b) s = fmaf(a.dh[(int64_t)b * a.D + d], a.pooled[(int64_t)b * a.K + k], s);
-        a.dw[(int64_t)d * a.K + k] = s;
+// dW[d][k] = sum_b dh[b][d] pooled[b][k] ; db[d] = sum_b dh[b][d].  Block = (16 features,
+// slice of rows); 64-row tiles of dh and pooled staged in LDS; thread (half, k) accumulates 8
+// features for one k.  Per-slice partials, summed in fixed order by launch_sum_slices.
+__global__ __launch_bounds__(256) void proj_bwd_weight_part_kernel(ProjArgs a, int bps) {
+    __shared__ float sdh[64][17];
+    __shared__ float spo[64][128];
+    const int d0 = blockIdx.x * 16, slice = blockIdx.y, tid = threadIdx.x;
+    const int half = tid >> 7, kl = tid & 127;
+    const int b0 = slice * bps, b1 = min(a.B, b0 + bps);
+    const int nd = min(16, a.D - d0);
+    float* pw = a.part + (int64_t)slice * a.D * a.K;
+    float* pb = a.part + (int64_t)gridDim.y * a.D * a.K + (int64_t)slice * a.D;
+    for (int kb = 0; kb < a.K; kb += 128) {
+        float acc[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+        float sdb = 0.f;
+        for (int bb = b0; bb < b1; bb += 64) {
+            const int nb = min(64, b1 - bb);
+            __syncthreads();
+            for (int e = tid; e < 64 * 16; e += 256) {
+                const int r = e >> 4, j = e & 15;
+                sdh[r][j] = (r < nb && j < nd) ? a.dh[(int64_t)(bb + r) * a.D + d0 + j] : 0.f;
+            }
+            for (int e = tid; e < 64 * 128; e += 256) {
+                const int r = e >> 7, k = e & 127;
+                spo[r][k] = (r < nb && kb + k < a.K) ? a.pooled[(int64_t)(bb + r) * a.K + kb + k] : 0.f;
+            }
+            __syncthreads();
+            for (int r = 0; r < nb; ++r) {
+                const float pv = spo[r][kl];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[j] = fmaf(sdh[r][half * 8 + j], pv, acc[j]);
+            }
+            if (kb == 0 && tid < 16)
+                for (int r = 0; r < nb; ++r) sdb += sdh[r][tid];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int d = half * 8 + j;
+            if (d < nd && kb + kl < a.K) pw[(int64_t)(d0 + d) * a.K + kb + kl] = acc[j];
+        }
+        if (kb == 0 && tid < nd) pb[d0 + tid] = sdb;
     }
-    double s = 0.0;
-    for (int b = tid; b < a.B; b += blockDim.x) s += (double)a.dh[(int64_t)b * a.D + d];
-    s = bsum(s, red);
-    if (tid == 0) a.db[d] = (float)s;
 }
 
 __global__ void transpose_kernel(const float* __restrict__ in, float* __restrict__ out, int rows, int cols) {
@@ -356,6 +387,15 @@ int launch_proj_fwd(ProjArgs a, hipStream_t s) {
     return PCX_OK;
 }
 
+#define RC_(x)                  \
+    do {                        \
+        int _rc = (x);          \
+        if (_rc) return _rc;    \
+    } while (0)
+
+int proj_wg_nslice(int B) { return std::max(1, std::min(64, B / 64)); }
+size_t proj_part_floats(int B, int D, int K) { return (size_t)proj_wg_nslice(B) * D * (K + 1); }
+
 int launch_proj_bwd(ProjArgs a, hipStream_t s) {
     normalize_bwd_kernel<<<ceil_div(a.B, 4), 256, 0, s>>>(a);
     PCX_LAUNCH_CHECK("normalize_bwd_kernel");
@@ -365,8 +405,12 @@ int launch_proj_bwd(ProjArgs a, hipStream_t s) {
     (void)hipFuncSetAttribute((const void*)proj_bwd_data_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
     proj_bwd_data_kernel<<<ceil_div(a.B, PR), 256, sm, s>>>(a);
     PCX_LAUNCH_CHECK("proj_bwd_data_kernel");
-    proj_bwd_weight_kernel<<<a.D, 256, 0, s>>>(a);
-    PCX_LAUNCH_CHECK("proj_bwd_weight_kernel");
+    PCX_CHECK_ARG(a.part, "proj_bwd: no partial buffer");
+    const int ns = proj_wg_nslice(a.B), bps = ceil_div(a.B, ns);
+    proj_bwd_weight_part_kernel<<<dim3((unsigned)ceil_div(a.D, 16), (unsigned)ns), 256, 0, s>>>(a, bps);
+    PCX_LAUNCH_CHECK("proj_bwd_weight_part_kernel");
+    RC_(launch_sum_slices(a.part, ns, (int64_t)a.D * a.K, a.dw, s));
+    RC_(launch_sum_slices(a.part + (int64_t)ns * a.D * a.K, ns, a.D, a.db, s));
     return PCX_OK;
 }
 

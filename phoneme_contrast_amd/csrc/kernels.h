@@ -199,7 +199,10 @@ struct ProjArgs {
     float* db;             // [D]
     float* dgamma;
     float* dbeta;
+    float* part;           // [proj_part_floats] weight / bias gradient partials
 };
+int proj_wg_nslice(int B);
+size_t proj_part_floats(int B, int D, int K);
 int launch_proj_fwd(ProjArgs a, hipStream_t s);
 int launch_proj_bwd(ProjArgs a, hipStream_t s);
 int launch_transpose(const float* in, float* out, int rows, int cols, hipStream_t s);

@@ -98,6 +98,7 @@ int build_small(Plan& p) {
     p.dzp = p.carve("dzp", (size_t)B * D * 4);
     p.dh = p.carve("dh", (size_t)B * D * 4);
     p.dpooled = p.carve("dpooled", (size_t)B * K * 4);
+    p.proj_part = p.carve("proj_part", proj_part_floats(B, D, K) * 4);
     p.wt = p.carve("wt", (size_t)K * D * 4);
     p.hp_dz = p.carve("hp_dz", (size_t)K * B * 4);
     p.hp_dzx = p.carve("hp_dzx", (size_t)K * B * 4);
@@ -262,6 +263,7 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
         j.db = G[ip + 1];
         j.dgamma = G[ip + 2];
         j.dbeta = G[ip + 3];
+        j.part = at<float>(ws, p.proj_part);
         { Scope sc(&p.prof, s, "proj_bwd"); RC(launch_proj_bwd(j, s)); }
     }
     // attention + pool + Dropout2d + ReLU backward -> dz6 and BN6 partials

@@ -86,6 +86,7 @@ struct Plan {
     size_t stat_part, stat_bytes;   // shared scratch for BN partials
     size_t dyb;                     // dy of the layer being back-propagated (DMA path)
     size_t wg_part, wg_bytes;       // shared scratch for weight-gradient partials
+    size_t proj_part;
     size_t pooled, att, h, cfp, cfpb, norm, dzp, dh, dpooled, wt, hp_dz, hp_dzx, hp_dwa, hp_dba;
     size_t total;
     std::vector<Region> regions;
