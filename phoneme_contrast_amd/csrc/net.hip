@@ -330,6 +330,7 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
                 pro = PRO_RAW;
             }
             if (p.dma) w.dy_out = at<float>(ws, p.dyb);
+            if (const char* e = getenv("PCX_WGRAD_EXPT")) w.expt = atoi(e);
             {
                 Scope sc(&p.prof, s, "wgrad", l);
                 RC(p.wgrad_impl == 0 ? launch_wgrad_win(pro, w, s)
