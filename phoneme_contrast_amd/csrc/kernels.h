@@ -84,6 +84,7 @@ struct WgradArgs {
     float* dy_out;        // optional: dy = BNBWD(dz, y) written here (consumed by the data grad)
     int R, CW, nseg, nrb, nchunks, per_slice, nslice;
     int MT, NPM, NPC;     // MFMA tile (16 or 32), tiles per block along cout / cin
+    int VX;               // wgrad_win: vector width of the x staging
     int expt;             // timing experiments only (PCX_WGRAD_EXPT): 1 no staging, 2 no MFMA, 4 no barrier
 };
 int launch_wgrad3x3(int pro, WgradArgs a, hipStream_t s);

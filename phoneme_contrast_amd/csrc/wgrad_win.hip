@@ -35,7 +35,8 @@ template <int V>
 using vecf = float __attribute__((ext_vector_type(V)));
 
 // LDS: dy rows [2][NB][DS] | x rows [4][CB][XSP].  dy image column j = sample column w0 + j;
-// x image column jj = sample column w0 - VEC + jj (jj < CW + 2 VEC).  Image row rho of x lives in
+// x image column jj = sample column w0 - VX + jj (jj < CW + 2 VX; x is staged VX-wide, VX <= VEC,
+// so that narrower halos can buy a wider strip).  Image row rho of x lives in
 // slot (rho + 1) & 3, dy row rho in slot rho & 1.  DS and XSP are 2 * odd: the 16x16 operand reads
 // (16 channels x 2 pixels per 32-lane group) are bank-conflict free and b64 stores stay aligned.
 struct Geo {
@@ -68,9 +69,10 @@ __device__ __forceinline__ void lds_store(float* p, vecf<V> v) {
     }
 }
 
-template <int PRO, int VEC, int NQDY, int NQX>
+template <int PRO, int VEC, int VX, int NQDY, int NQX>
 struct RowStage {
-    vecf<VEC> dzv[NQDY], yv[NQDY], xv[NQX];
+    vecf<VEC> dzv[NQDY], yv[NQDY];
+    vecf<VX> xv[NQX];
 
     __device__ __forceinline__ void load_dy(const WgradArgs& a, const Geo& g, const Walk& wk, const float* dzb,
                                             const float* yb, int w0, int r, int NB) {
@@ -129,8 +131,8 @@ struct RowStage {
         const float* xr = xb + rx * a.W;
 #pragma unroll
         for (int i = 0; i < NQX; ++i) {
-            const int w = min(max(w0 - VEC + VEC * q, 0), a.W - VEC);
-            xv[i] = *reinterpret_cast<const vecf<VEC>*>(xr + min(c, CB - 1) * HW + w);
+            const int w = min(max(w0 - VX + VX * q, 0), a.W - VX);
+            xv[i] = *reinterpret_cast<const vecf<VX>*>(xr + min(c, CB - 1) * HW + w);
             c += wk.dc;
             q += wk.dqx;
             if (q >= g.QX) { q -= g.QX; ++c; }
@@ -142,14 +144,14 @@ struct RowStage {
         opaque(c, q);
 #pragma unroll
         for (int i = 0; i < NQX; ++i) {
-            const int w = w0 - VEC + VEC * q;
-            vecf<VEC> v = xv[i];
+            const int w = w0 - VX + VX * q;
+            vecf<VX> v = xv[i];
             if (PRO == PRO_BNRELU) {
                 const float4 k = cfx[min(c, CB - 1)];
 #pragma unroll
-                for (int e = 0; e < VEC; ++e) v[e] = fmaxf(fmaf(v[e], k.x, k.y), 0.f);
+                for (int e = 0; e < VX; ++e) v[e] = fmaxf(fmaf(v[e], k.x, k.y), 0.f);
             }
-            xv[i] = (w >= 0 && w < a.W) ? v : vecf<VEC>(0.f);
+            xv[i] = (w >= 0 && w < a.W) ? v : vecf<VX>(0.f);
             c += wk.dc;
             q += wk.dqx;
             if (q >= g.QX) { q -= g.QX; ++c; }
@@ -159,7 +161,7 @@ struct RowStage {
         opaque(c, q);
 #pragma unroll
         for (int i = 0; i < NQX; ++i) {
-            if (tid + 256 * i < g.nqx) lds_store<VEC>(lds + g.xbase + slot * g.xslot + c * g.XSP + VEC * q, xv[i]);
+            if (tid + 256 * i < g.nqx) lds_store<VX>(lds + g.xbase + slot * g.xslot + c * g.XSP + VX * q, xv[i]);
             c += wk.dc;
             q += wk.dqx;
             if (q >= g.QX) { q -= g.QX; ++c; }
@@ -211,16 +213,16 @@ __device__ __forceinline__ void row_mfma(f32x4 (&acc)[PW][9], const float* dyt, 
     if (ks < kend) mma(a0, b0);
 }
 
-template <int PW, int PRO, int VEC, int NQDY, int NQX>
+template <int PW, int PRO, int VEC, int VX, int NQDY, int NQX>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void wgrad_win_kernel(WgradArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int NB = a.NPM * MT, CB = a.NPC * MT;
     Geo g;
     g.CW = a.CW;
     g.QD = a.CW / VEC;
-    g.QX = a.CW / VEC + 2;
+    g.QX = a.CW / VX + 2;
     g.DS = pad2odd(a.CW);
-    g.XSP = pad2odd(a.CW + 2 * VEC);
+    g.XSP = pad2odd(a.CW + 2 * VX);
     g.nqd = NB * g.QD;
     g.nqx = CB * g.QX;
     g.dyslot = NB * g.DS;
@@ -257,7 +259,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
         mi[k] = p / a.NPC;
         ci[k] = p - mi[k] * a.NPC;
         ao[k] = (mi[k] * MT + li) * g.DS + kg;
-        xo[k] = (ci[k] * MT + li) * g.XSP + kg + (VEC - 1);  // image column of sample column w0 - 1
+        xo[k] = (ci[k] * MT + li) * g.XSP + kg + (VX - 1);  // image column of sample column w0 - 1
     }
     f32x4 acc[PW][9];
 #pragma unroll
@@ -278,7 +280,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
     const bool write_dy = a.dy_out != nullptr && c0 == 0;
     const int NK = a.CW / KS;
     const int t0 = slice * a.per_slice, t1 = min(a.nchunks, t0 + a.per_slice);
-    RowStage<PRO, VEC, NQDY, NQX> st;
+    RowStage<PRO, VEC, VX, NQDY, NQX> st;
     for (int task = t0; task < t1; ++task) {
         const int b = task / a.nseg;
         const int w0 = (task - b * a.nseg) * a.CW;
@@ -331,8 +333,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
             }
 }
 
-size_t win_lds(int NB, int CB, int CW, int vec) {
-    return ((size_t)2 * NB * pad2odd(CW) + (size_t)4 * CB * pad2odd(CW + 2 * vec) + 4 * (size_t)(NB + CB)) * 4;
+size_t win_lds(int NB, int CB, int CW, int vx) {
+    return ((size_t)2 * NB * pad2odd(CW) + (size_t)4 * CB * pad2odd(CW + 2 * vx) + 4 * (size_t)(NB + CB)) * 4;
 }
 
 // register prefetch capacity, in elements per thread per image, by PW (tiles per wave)
@@ -359,23 +361,26 @@ void wgrad_win_geometry(int B, int H, int W, int cin, int cout, WgradArgs* a) {
     // strip width: the next row is prefetched into registers (<= npre elements per thread and
     // image), LDS <= 78 KB so two blocks share a CU.  Cost per row step = MFMA cycles of the
     // valid k-steps + a fixed barrier / staging overhead.
-    const size_t cap = 78 * 1024;
+    const size_t cap = 80 * 1024;  // two blocks per CU
     double best = 1e300;
-    int bCW = KS;
+    int bCW = KS, bVX = vec;
+    for (int vx = vec; vx >= std::max(1, vec / 2); vx >>= 1)
     for (int cw = KS; cw <= std::max(KS, (W + KS - 1) / KS * KS); cw += KS) {
         if (cw % vec) continue;
-        if (win_lds(NB, CB, cw, vec) > cap) continue;
-        if (NB * cw > 256 * npre || CB * (cw + 2 * vec) > 256 * npre) continue;
+        if (win_lds(NB, CB, cw, vx) > cap) continue;
+        if (NB * cw > 256 * npre || CB * (cw + 2 * vx) > 256 * npre) continue;
         const int nseg = (W + cw - 1) / cw;
         double mf = 0.0;
         for (int sgm = 0; sgm < nseg; ++sgm) {
             const int valid = std::min(cw, W - sgm * cw);
             mf += (double)pw * 9 * ((valid + KS - 1) / KS) * 32.0;
         }
-        const double cost = H * (mf + nseg * 1200.0) + nseg * 2500.0;
-        if (cost < best) { best = cost; bCW = cw; }
+        // narrower x loads cost more instructions per staged element
+        const double cost = (H * (mf + nseg * 1200.0) + nseg * 2500.0) * (vx < vec ? 1.03 : 1.0);
+        if (cost < best) { best = cost; bCW = cw; bVX = vx; }
     }
     a->CW = bCW;
+    a->VX = bVX;
     a->R = 1;
     a->nseg = ceil_div(W, bCW);
     a->nrb = 1;
@@ -388,28 +393,30 @@ void wgrad_win_geometry(int B, int H, int W, int cin, int cout, WgradArgs* a) {
 }
 
 int launch_wgrad_win(int pro, WgradArgs a, hipStream_t s) {
-    const int NB = a.NPM * a.MT, CB = a.NPC * a.MT, vec = win_vec(a.W);
+    const int NB = a.NPM * a.MT, CB = a.NPC * a.MT, vec = win_vec(a.W), vx = a.VX;
+    PCX_CHECK_ARG(vx >= 1 && vx <= vec && vec % vx == 0, "wgrad_win: x vector width %d", vx);
     PCX_CHECK_ARG(a.cout % NB == 0 && a.cin % CB == 0, "wgrad_win: channels (%d,%d) vs block %dx%d", a.cout, a.cin,
                   NB, CB);
     PCX_CHECK_ARG(a.CW % KS == 0 && a.CW % vec == 0, "wgrad_win: strip width %d", a.CW);
     PCX_CHECK_ARG((int64_t)a.cout * a.H * a.W < ((int64_t)1 << 31), "wgrad_win: sample block too large");
     const int pw = a.NPM * a.NPC / 4;
     PCX_CHECK_ARG(a.MT == MT && pw * 4 == a.NPM * a.NPC && pw >= 1 && pw <= 2, "wgrad_win: bad tile split");
-    PCX_CHECK_ARG(NB * a.CW <= 256 * NPRE[pw] && CB * (a.CW + 2 * vec) <= 256 * NPRE[pw],
+    PCX_CHECK_ARG(NB * a.CW <= 256 * NPRE[pw] && CB * (a.CW + 2 * vx) <= 256 * NPRE[pw],
                   "wgrad_win: strip %d exceeds the prefetch", a.CW);
-    const size_t smem = win_lds(NB, CB, a.CW, vec);
+    const size_t smem = win_lds(NB, CB, a.CW, vx);
     PCX_CHECK_ARG(smem <= 160 * 1024, "wgrad_win: LDS %zu too large", smem);
     dim3 grid((unsigned)(((a.nslice + 7) / 8) * 8 * ((a.cout / NB) * (a.cin / CB))));
-#define PCX_WGW(PW_, P_, V_)                                                                           \
-    if (pw == PW_ && pro == P_ && vec == V_) {                                                         \
-        constexpr int nq = NPRE[PW_] / V_;                                                            \
-        (void)hipFuncSetAttribute((const void*)wgrad_win_kernel<PW_, P_, V_, nq, nq>,                  \
+#define PCX_WGW(PW_, P_, V_, VX_)                                                                      \
+    if (pw == PW_ && pro == P_ && vec == V_ && vx == VX_) {                                            \
+        constexpr int nq = NPRE[PW_] / V_, nqx = NPRE[PW_] / VX_;                                      \
+        (void)hipFuncSetAttribute((const void*)wgrad_win_kernel<PW_, P_, V_, VX_, nq, nqx>,            \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);              \
-        wgrad_win_kernel<PW_, P_, V_, nq, nq><<<grid, 256, smem, s>>>(a);                              \
+        wgrad_win_kernel<PW_, P_, V_, VX_, nq, nqx><<<grid, 256, smem, s>>>(a);                        \
         PCX_LAUNCH_CHECK("wgrad_win_kernel");                                                          \
         return PCX_OK;                                                                                 \
     }
-#define PCX_WGW_V(PW_, P_) PCX_WGW(PW_, P_, 4) PCX_WGW(PW_, P_, 2) PCX_WGW(PW_, P_, 1)
+#define PCX_WGW_V(PW_, P_) PCX_WGW(PW_, P_, 4, 4) PCX_WGW(PW_, P_, 4, 2) PCX_WGW(PW_, P_, 2, 2) PCX_WGW(PW_, P_, 2, 1) \
+    PCX_WGW(PW_, P_, 1, 1)
 #define PCX_WGW_ALL(P_) PCX_WGW_V(1, P_) PCX_WGW_V(2, P_)
     PCX_WGW_ALL(PRO_RAW)
     PCX_WGW_ALL(PRO_BNRELU)
