@@ -430,7 +430,7 @@ int launch_conv3x3(int pro, int epi, ConvArgs a, hipStream_t s) {
     a.NR = (bp - 1 + a.W - 1) / a.W + 1 + 2;
     a.RS = PADL + ((a.W + 1 + 3) / 4) * 4;
     size_t smem = ((size_t)CK * a.NR * a.RS + 9 * CK * cout_t) * sizeof(float);
-    size_t red = (size_t)4 * cout_t * 3 * sizeof(float);
+    size_t red = ((size_t)4 * cout_t * 3 + 4 * (size_t)cout_t) * sizeof(float);  // epilogue partials + cf table
     if (smem < red) smem = red;
     PCX_CHECK_ARG(smem <= 150 * 1024 && a.NR <= 160, "conv3x3: W=%d needs %zu B of LDS", a.W, smem);
     dim3 grid((unsigned)(ntile * (a.cout / cout_t)));

@@ -17,6 +17,13 @@ namespace {
 
 typedef __attribute__((address_space(3))) void lds_void;
 
+// Timing-decomposition builds only (scripts/conv_expt.sh compiles this file with
+// -DPCX_CONV_EXPT=bits into a separate library): 1 no DMA after the first chunk, 2 no MFMA,
+// 4 no epilogue, 8 no per-chunk wait / barrier, 16 no prologue / padding masks.  Results are garbage in those builds.
+#ifndef PCX_CONV_EXPT
+#define PCX_CONV_EXPT 0
+#endif
+
 __device__ __forceinline__ int fdiv(int n, int d, float inv) {  // n / d, 0 <= n < 2^22
     int q = (int)((float)n * inv);
     int r = n - q * d;
@@ -43,6 +50,27 @@ __device__ __forceinline__ void dma(const float* g, unsigned lds_byte_addr) {
         asm volatile("s_nop 0\n\tglobal_load_lds_dword %0, off" :: "v"(g), "{m0}"(m0) : "memory");
 }
 
+// Same copy in the saddr form: global address = uniform 64-bit base (SGPRs) + per-lane 32-bit
+// byte offset.  The offsets of every copy a lane issues are fixed for a tile (only the channel
+// base moves from chunk to chunk), so they are computed once and a copy costs no VALU at all.
+template <int VEC>
+__device__ __forceinline__ void dma_s(const float* sbase, unsigned voff, unsigned lds_byte_addr) {
+    const unsigned m0 = __builtin_amdgcn_readfirstlane(lds_byte_addr);
+    if constexpr (VEC == 4)
+        asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" :: "v"(voff), "s"(sbase), "{m0}"(m0) : "memory");
+    else
+        asm volatile("s_nop 0\n\tglobal_load_lds_dword %0, %1" :: "v"(voff), "s"(sbase), "{m0}"(m0) : "memory");
+}
+
+__device__ __forceinline__ const float* uniform_ptr(const float* p) {
+    const uint64_t v = (uint64_t)(uintptr_t)p;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+    return (const float*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
+
+// copies per wave and K-chunk with precomputed offsets (more fall back to per-copy addressing)
+constexpr int DMA_MAXR = 5, DMA_MAXW = 3;
 
 // raw image of one K-chunk: NSRC tensors x CK channels x NR staged rows x W columns (dense)
 template <int VEC, int NSRC>
@@ -85,8 +113,9 @@ __device__ __forceinline__ void issue_wts(const ConvArgs& a, unsigned wts, int c
 // fp32 MFMA peak where 2 reach 60 %).
 constexpr int dma_occ(int wm) { return wm == 2 ? 4 : 3; }
 
-template <int WM, int WN, int VEC, int PRO, int EPI, int CK>
+template <int WM, int WN, int VEC, int PRO, int EPI, int CK, bool PRE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_occ(WM)))) void conv3x3_dma_kernel(ConvArgs a) {
+    static_assert(!PRE || PRO != PRO_BNBWD, "precomputed copies stage one source");
     constexpr int COUT_T = 32 * WM;
     constexpr int BP = 4 * WN * 32;
     constexpr int NSRC = (PRO == PRO_BNBWD) ? 2 : 1;
@@ -155,20 +184,62 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_occ(WM)
     const int rawtotal = NSRC * CK * PL;
     const float invPL = 1.f / PL, invW = 1.f / a.W;
     const int nchunk = a.cin / CK;
-    issue_raw<VEC, NSRC>(a, rinfo, raw_lds, 0, wave, lane, rawtotal, CK, invPL, invW);
-    issue_wts<WM>(a, wts_lds, 0, n0, wave, lane, CK);
+    constexpr int WTOT = 9 * CK * COUT_T;
+    // precomputed copy offsets: raw rows relative to (first sample of the block, channel c0),
+    // weights relative to (wpack + c0 * cout + n0)
+    unsigned roff[PRE ? DMA_MAXR : 1], woff[PRE ? DMA_MAXW : 1];
+    const int bf = row0 < 0 ? 0 : (int)(row0 / a.H);
+    if constexpr (PRE) {
+#pragma unroll
+        for (int j = 0; j < DMA_MAXR; ++j) {
+            const int base = wave * 64 * VEC + j * 256 * VEC;
+            const int f = min(base + lane * VEC, rawtotal - VEC);
+            const int cl = fdiv(f, PL, invPL);
+            const int rem = f - cl * PL;
+            const int lr = fdiv(rem, a.W, invW);
+            const int w = rem - lr * a.W;
+            const int2 ri = rinfo[min(lr, a.NR - 1)];
+            const int b = ri.x < 0 ? bf : ri.x;
+            const int hh = ri.x < 0 ? 0 : ri.y;
+            roff[j] = 4u * (unsigned)((((b - bf) * a.cin + cl) * a.H + hh) * a.W + w);
+        }
+#pragma unroll
+        for (int j = 0; j < DMA_MAXW; ++j) {
+            const int f = min(wave * 256 + j * 1024 + lane * 4, WTOT - 4);
+            const int row = f / COUT_T, col = f - row * COUT_T;
+            const int tap = row / CK, cc = row - tap * CK;
+            woff[j] = 4u * (unsigned)((tap * a.cin + cc) * a.cout + col);
+        }
+    }
+    auto issue = [&](int c0, unsigned nb) {
+        if constexpr (PRE) {
+            const float* sr = uniform_ptr(a.src + ((int64_t)bf * a.cin + c0) * HW);
+            const float* sw = uniform_ptr(a.wpack + (int64_t)c0 * a.cout + n0);
+#pragma unroll
+            for (int j = 0; j < DMA_MAXR; ++j) {
+                const int base = wave * 64 * VEC + j * 256 * VEC;
+                if (base < rawtotal) dma_s<VEC>(sr, roff[j], raw_lds + nb * 4u * rawf + 4u * base);
+            }
+#pragma unroll
+            for (int j = 0; j < DMA_MAXW; ++j) {
+                const int base = wave * 256 + j * 1024;
+                if (base < WTOT) dma_s<4>(sw, woff[j], wts_lds + nb * 4u * wtsf + 4u * base);
+            }
+        } else {
+            issue_raw<VEC, NSRC>(a, rinfo, raw_lds + nb * 4u * rawf, c0, wave, lane, rawtotal, CK, invPL, invW);
+            issue_wts<WM>(a, wts_lds + nb * 4u * wtsf, c0, n0, wave, lane, CK);
+        }
+    };
+    issue(0, 0u);
     for (int k = 0; k < nchunk; ++k) {
         const int c0 = k * CK;
         float* raw = raw0 + (k & 1) * rawf;
         float* wts = wts0 + (k & 1) * wtsf;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();  // chunk k visible to all waves; chunk k-1 fully consumed
-        if (k + 1 < nchunk) {
-            const unsigned nb = (unsigned)((k + 1) & 1);
-            issue_raw<VEC, NSRC>(a, rinfo, raw_lds + nb * 4u * rawf, c0 + CK, wave, lane, rawtotal,
-                                 CK, invPL, invW);
-            issue_wts<WM>(a, wts_lds + nb * 4u * wtsf, c0 + CK, n0, wave, lane, CK);
+        if (!(PCX_CONV_EXPT & 8) || k == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();  // chunk k visible to all waves; chunk k-1 fully consumed
         }
+        if (k + 1 < nchunk && !(PCX_CONV_EXPT & 1)) issue(c0 + CK, (unsigned)((k + 1) & 1));
         float4 cf[CK / 2];
         if (PRO != PRO_RAW) {
 #pragma unroll
@@ -203,7 +274,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_occ(WM)
 #pragma unroll
             for (int ni = 0; ni < WN; ++ni) {
                 float v;
-                if (PRO == PRO_RAW) {
+                if (PRO == PRO_RAW || (PCX_CONV_EXPT & 16)) {
                     v = rv[cur][ni];
                 } else if (PRO == PRO_BNRELU) {
                     v = fmaxf(fmaf(rv[cur][ni], cf[s].x, cf[s].y), 0.f);
@@ -211,6 +282,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_occ(WM)
                     v = cf[s].x * (rv[cur][ni] - cf[s].y - (rv2[cur][ni] - cf[s].w) * cf[s].z);
                 }
                 bool ok = true;
+                if (PCX_CONV_EXPT & 16) {
+                    bv[ni] = v;
+                    continue;
+                }
                 if (dh < 0) ok = ok && vup[ni];
                 if (dh > 0) ok = ok && vdn[ni];
                 if (dw < 0) ok = ok && vl[ni];
@@ -220,11 +295,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_occ(WM)
 #pragma unroll
             for (int mi = 0; mi < WM; ++mi)
 #pragma unroll
-                for (int ni = 0; ni < WN; ++ni) acc[mi][ni] = mfma32(av[cur][mi], bv[ni], acc[mi][ni]);
+                for (int ni = 0; ni < WN; ++ni) {
+                    if (PCX_CONV_EXPT & 2) acc[mi][ni][0] = fmaf(av[cur][mi], bv[ni], acc[mi][ni][0]);
+                    else acc[mi][ni] = mfma32(av[cur][mi], bv[ni], acc[mi][ni]);
+                }
             __builtin_amdgcn_sched_barrier(0);
         }
     }
     __syncthreads();  // LDS is reused for the cross-wave statistics
+    if (PCX_CONV_EXPT & 4) {
+        float t = 0.f;
+#pragma unroll
+        for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < WN; ++ni)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) t += acc[mi][ni][r];
+        if (t == 1234.5f) a.out[tid] = t;
+        return;
+    }
     conv_epilogue<WM, WN, EPI>(a, acc, smem, tile, n0, m0, Mtot, HW, wave, tid, valid, pb, pp);
 }
 
@@ -308,15 +397,24 @@ int launch_conv3x3_dma(int pro, int epi, ConvArgs a, hipStream_t s) {
     const int rawf = ((nsrc * ck * PL + 64 * vec - 1) / (64 * vec)) * (64 * vec);
     const int wtsf = ((9 * ck * cout_t + 255) / 256) * 256;
     size_t smem = ((size_t)4 * a.cin + ((2 * a.NR + 3) & ~3) + 2 * (size_t)rawf + 2 * (size_t)wtsf) * 4;
-    size_t red = (size_t)4 * cout_t * 3 * 4;
+    size_t red = ((size_t)4 * cout_t * 3 + 4 * (size_t)cout_t) * 4;  // epilogue partials + cf table
     if (smem < red) smem = red;
     PCX_CHECK_ARG(smem <= 160 * 1024, "conv3x3_dma: W=%d needs %zu B of LDS", a.W, smem);
     dim3 grid((unsigned)(ntile * (a.cout / cout_t)));
+    // copies per wave and chunk (wave 0 issues the most): precomputed offsets when they fit
+    const bool pre = vec == 4 && ceil_div(nsrc * ck * PL, 256 * vec) <= DMA_MAXR && ceil_div(9 * ck * cout_t, 1024) <= DMA_MAXW &&
+                     (int64_t)((a.NR / a.H + 2) * a.cin) * a.H * a.W * 4 < ((int64_t)1 << 31) && nsrc == 1;
 #define PCX_DMA_CASE(WM_, WN_, V_, P_, E_, CK_)                                                   \
     if (wm == WM_ && vec == V_ && pro == P_ && epi == E_ && ck == CK_) {                         \
-        (void)hipFuncSetAttribute((const void*)conv3x3_dma_kernel<WM_, WN_, V_, P_, E_, CK_>,    \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);        \
-        conv3x3_dma_kernel<WM_, WN_, V_, P_, E_, CK_><<<grid, 256, smem, s>>>(a);                \
+        if (pre) {                                                                               \
+            (void)hipFuncSetAttribute((const void*)conv3x3_dma_kernel<WM_, WN_, V_, P_, E_, CK_, true>, \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);    \
+            conv3x3_dma_kernel<WM_, WN_, V_, P_, E_, CK_, true><<<grid, 256, smem, s>>>(a);      \
+        } else {                                                                                 \
+            (void)hipFuncSetAttribute((const void*)conv3x3_dma_kernel<WM_, WN_, V_, P_, E_, CK_, false>, \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);    \
+            conv3x3_dma_kernel<WM_, WN_, V_, P_, E_, CK_, false><<<grid, 256, smem, s>>>(a);     \
+        }                                                                                        \
         PCX_LAUNCH_CHECK("conv3x3_dma_kernel");                                                  \
         return PCX_OK;                                                                           \
     }

@@ -67,33 +67,74 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[W
             if (tid == 0 && n0 == 0) a.partn[tile] = n;
         }
     } else {
-        // backward epilogues: sums of dz and dz*xhat per channel
+        // backward epilogues: sums of dz and dz*xhat per channel.  The global loads of RB
+        // accumulator rows are issued as one batch before any of their stores: the compiler must
+        // assume a store may alias a later load, so row-by-row code paid one full memory round
+        // trip per accumulator row.  Invalid pixels were clamped to the last valid one by the
+        // caller, so every batched address is in bounds.
+#ifndef PCX_EPI_RB_RELU
+#define PCX_EPI_RB_RELU 4
+#endif
+#ifndef PCX_EPI_RB_POOL
+#define PCX_EPI_RB_POOL 2
+#endif
+        constexpr int RB = (EPI == EPI_BWD_RELU) ? PCX_EPI_RB_RELU : PCX_EPI_RB_POOL;
+        // per-channel coefficients staged in LDS once (the accumulator loop is free of them)
+        float4* cfl = reinterpret_cast<float4*>(red + 4 * COUT_T * 3);
+        if (tid < COUT_T) cfl[tid] = a.cf_out[n0 + tid];
+        __syncthreads();
+        int64_t base[WN];
+#pragma unroll
+        for (int ni = 0; ni < WN; ++ni) {
+            if (EPI == EPI_BWD_RELU) {
+                base[ni] = ((int64_t)pb[ni] * a.cout + n0) * HW + pp[ni];
+            } else {
+                const int hp = pp[ni] / a.W, wp = pp[ni] - hp * a.W;
+                base[ni] = ((int64_t)pb[ni] * a.cout + n0) * a.Hs * a.Ws + (int64_t)(2 * hp) * a.Ws + 2 * wp;
+            }
+        }
+        const int chs = (EPI == EPI_BWD_RELU) ? (int)HW : a.Hs * a.Ws;  // channel-plane stride
 #pragma unroll
         for (int mi = 0; mi < WM; ++mi)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
+            for (int rb = 0; rb < 16; rb += RB) {
+                constexpr int NY = (EPI == EPI_BWD_RELU) ? 1 : 4;
+                float yv[RB][WN][NY], dv[RB][WN];
+#pragma unroll
+                for (int j = 0; j < RB; ++j) {
+                    const int chl = mi * 32 + acc_row(rb + j, h);
+#pragma unroll
+                    for (int ni = 0; ni < WN; ++ni) {
+                        const float* yp = a.yprev + base[ni] + (int64_t)chl * chs;
+                        yv[j][ni][0] = yp[0];
+                        if (EPI == EPI_BWD_POOL) {
+                            yv[j][ni][1] = yp[1];
+                            yv[j][ni][2] = yp[a.Ws];
+                            yv[j][ni][3] = yp[a.Ws + 1];
+                            dv[j][ni] = a.drop_out ? a.drop_out[(int64_t)pb[ni] * a.cout + n0 + chl] : 1.f;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < RB; ++j) {
+                const int r = rb + j;
                 const int chl = mi * 32 + acc_row(r, h);
-                const int ch = n0 + chl;
-                const float4 cf = a.cf_out[ch];
+                const float4 cf = cfl[chl];
                 float sdz = 0.f, sdx = 0.f;
 #pragma unroll
                 for (int ni = 0; ni < WN; ++ni) {
                     if (!valid[ni]) continue;
                     const float g = acc[mi][ni][r];
+                    float* op = a.out + base[ni] + (int64_t)chl * chs;
                     if (EPI == EPI_BWD_RELU) {
-                        int64_t o = ((int64_t)pb[ni] * a.cout + ch) * HW + pp[ni];
-                        float y = a.yprev[o];
+                        const float y = yv[j][ni][0];
                         float dz = (fmaf(y, cf.x, cf.y) > 0.f) ? g : 0.f;
-                        a.out[o] = dz;
+                        op[0] = dz;
                         sdz += dz;
                         sdx = fmaf(dz, (y - cf.z) * cf.w, sdx);
                     } else {  // EPI_BWD_POOL
-                        const int hp = pp[ni] / a.W, wp = pp[ni] - hp * a.W;
-                        float gd = a.drop_out ? g * a.drop_out[(int64_t)pb[ni] * a.cout + ch] : g;
-                        int64_t o = ((int64_t)pb[ni] * a.cout + ch) * a.Hs * a.Ws +
-                                    (int64_t)(2 * hp) * a.Ws + 2 * wp;
-                        float y0 = a.yprev[o], y1 = a.yprev[o + 1];
-                        float y2 = a.yprev[o + a.Ws], y3 = a.yprev[o + a.Ws + 1];
+                        const float gd = g * dv[j][ni];
+                        const float y0 = yv[j][ni][0], y1 = yv[j][ni][1], y2 = yv[j][ni][2], y3 = yv[j][ni][3];
                         float r0 = fmaxf(fmaf(y0, cf.x, cf.y), 0.f), r1 = fmaxf(fmaf(y1, cf.x, cf.y), 0.f);
                         float r2 = fmaxf(fmaf(y2, cf.x, cf.y), 0.f), r3 = fmaxf(fmaf(y3, cf.x, cf.y), 0.f);
                         // first maximum in window scan order, as torch's max_pool2d
@@ -103,10 +144,10 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[W
                         if (r2 > best) { best = r2; arg = 2; ya = y2; }
                         if (r3 > best) { best = r3; arg = 3; ya = y3; }
                         float d = best > 0.f ? gd : 0.f;
-                        a.out[o] = arg == 0 ? d : 0.f;
-                        a.out[o + 1] = arg == 1 ? d : 0.f;
-                        a.out[o + a.Ws] = arg == 2 ? d : 0.f;
-                        a.out[o + a.Ws + 1] = arg == 3 ? d : 0.f;
+                        op[0] = arg == 0 ? d : 0.f;
+                        op[1] = arg == 1 ? d : 0.f;
+                        op[a.Ws] = arg == 2 ? d : 0.f;
+                        op[a.Ws + 1] = arg == 3 ? d : 0.f;
                         sdz += d;
                         sdx = fmaf(d, (ya - cf.z) * cf.w, sdx);
                     }
@@ -116,6 +157,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[W
                 if (l32 == 0) {
                     float* d = red + (wave * COUT_T + chl) * 2;
                     d[0] = sdz; d[1] = sdx;
+                }
                 }
             }
         __syncthreads();
