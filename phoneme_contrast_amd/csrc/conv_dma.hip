@@ -72,6 +72,12 @@ __device__ __forceinline__ const float* uniform_ptr(const float* p) {
 // copies per wave and K-chunk with precomputed offsets (more fall back to per-copy addressing)
 constexpr int DMA_MAXR = 5, DMA_MAXW = 3;
 
+// floats of the per-block tables in front of the staged image: cf [cin] float4, rinfo [NR] int2,
+// rowpos [NR] int, segments [NR] int4
+__host__ __device__ constexpr int dma_table_floats(int cin, int NR) {
+    return 4 * cin + ((2 * NR + 3) & ~3) + ((NR + 3) & ~3) + 4 * NR;
+}
+
 // raw image of one K-chunk: NSRC tensors x CK channels x NR staged rows x W columns (dense)
 template <int VEC, int NSRC>
 __device__ __forceinline__ void issue_raw(const ConvArgs& a, const int2* rinfo, unsigned raw, int c0,
@@ -120,12 +126,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_occ(WM)
     constexpr int BP = 4 * WN * 32;
     constexpr int NSRC = (PRO == PRO_BNBWD) ? 2 : 1;
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int PL = a.NR * a.W;
+    // channel-plane stride of the staged image: dense rows (NR * W), or with PRE the row segments
+    // of each sample placed at the 16-byte phase of their global address (host-computed bound)
+    const int PL = PRE ? a.RS : a.NR * a.W;
     const int rawf = ((NSRC * CK * PL + 64 * VEC - 1) / (64 * VEC)) * (64 * VEC);
     const int wtsf = ((9 * CK * COUT_T + 255) / 256) * 256;
     float4* cft = reinterpret_cast<float4*>(smem);                        // [cin]
     int2* rinfo = reinterpret_cast<int2*>(smem + 4 * a.cin);              // [NR] (padded to 4)
-    float* raw0 = smem + 4 * a.cin + ((2 * a.NR + 3) & ~3);
+    int* rowpos = reinterpret_cast<int*>(smem + 4 * a.cin + ((2 * a.NR + 3) & ~3));  // [NR]
+    int4* segt = reinterpret_cast<int4*>(rowpos + ((a.NR + 3) & ~3));    // [NR] {kstart, kend, goff, nseg}
+    float* raw0 = smem + dma_table_floats(a.cin, a.NR);
     float* wts0 = raw0 + 2 * rawf;
     // LDS byte addresses of the DMA targets (M0 operand)
     const unsigned lds0 = (unsigned)(uintptr_t)(lds_void*)smem;
@@ -153,7 +163,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_occ(WM)
         int b = ok ? (int)(gr / a.H) : -1;
         rinfo[lr] = make_int2(b, ok ? (int)(gr - (int64_t)b * a.H) : 0);
     }
-    int pixoff[WN];
+    int pixoff[WN], prow[WN];
     bool vup[WN], vdn[WN], vl[WN], vr[WN], valid[WN];
     int pb[WN], pp[WN];
 #pragma unroll
@@ -165,7 +175,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_occ(WM)
         int w = (int)(mm - gr * a.W);
         int b = (int)(gr / a.H);
         int hr = (int)(gr - (int64_t)b * a.H);
-        pixoff[ni] = (int)(gr - row0) * a.W + w;
+        prow[ni] = (int)(gr - row0);
+        pixoff[ni] = w;
         vup[ni] = hr > 0;
         vdn[ni] = hr < a.H - 1;
         vl[ni] = w > 0;
@@ -173,7 +184,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_occ(WM)
         pb[ni] = b;
         pp[ni] = hr * a.W + w;
     }
+    const int bf = row0 < 0 ? 0 : (int)(row0 / a.H);
+    if constexpr (PRE) {
+        // row segments (maximal runs of rows of one sample, or of invalid rows): a segment starts
+        // on a fresh 16-byte group, its first row at the 16-byte phase of its global address, so
+        // that every group of the image is one aligned dwordx4 copy of one segment
+        __syncthreads();
+        if (tid == 0) {
+            int pos = 0, nseg = 0, pb_ = -2, ph_ = -2;
+            for (int lr = 0; lr < a.NR; ++lr) {
+                const int2 ri = rinfo[lr];
+                if (lr == 0 || ri.x != pb_ || (ri.x >= 0 && ri.y != ph_ + 1)) {
+                    if (nseg) segt[nseg - 1].y = (pos + 3) >> 2;
+                    const int ks = (pos + 3) >> 2;
+                    const int phase = ri.x >= 0 ? (ri.y * a.W) & 3 : 0;
+                    const int goff = ri.x >= 0 ? (ri.x - bf) * a.cin * (int)HW + ri.y * a.W - phase : -1;
+                    segt[nseg++] = make_int4(ks, 0, goff, 0);
+                    pos = 4 * ks + phase;
+                }
+                rowpos[lr] = pos;
+                pos += a.W;
+                pb_ = ri.x;
+                ph_ = ri.y;
+            }
+            segt[nseg - 1].y = (pos + 3) >> 2;
+            segt[0].w = nseg;
+        }
+    }
     __syncthreads();
+#pragma unroll
+    for (int ni = 0; ni < WN; ++ni) pixoff[ni] += PRE ? rowpos[prow[ni]] : prow[ni] * a.W;
 
     f32x16 acc[WM][WN];
 #pragma unroll
@@ -188,20 +228,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_occ(WM)
     // precomputed copy offsets: raw rows relative to (first sample of the block, channel c0),
     // weights relative to (wpack + c0 * cout + n0)
     unsigned roff[PRE ? DMA_MAXR : 1], woff[PRE ? DMA_MAXW : 1];
-    const int bf = row0 < 0 ? 0 : (int)(row0 / a.H);
     if constexpr (PRE) {
+        static_assert(!PRE || VEC == 4, "segment layout copies 16-byte groups");
+        const int QP = PL / 4, nseg = segt[0].w;
+        const float invQP = 1.f / QP;
 #pragma unroll
         for (int j = 0; j < DMA_MAXR; ++j) {
-            const int base = wave * 64 * VEC + j * 256 * VEC;
-            const int f = min(base + lane * VEC, rawtotal - VEC);
-            const int cl = fdiv(f, PL, invPL);
-            const int rem = f - cl * PL;
-            const int lr = fdiv(rem, a.W, invW);
-            const int w = rem - lr * a.W;
-            const int2 ri = rinfo[min(lr, a.NR - 1)];
-            const int b = ri.x < 0 ? bf : ri.x;
-            const int hh = ri.x < 0 ? 0 : ri.y;
-            roff[j] = 4u * (unsigned)((((b - bf) * a.cin + cl) * a.H + hh) * a.W + w);
+            const int g = min(wave * 64 + j * 256 + lane, rawtotal / 4 - 1);
+            const int cl = fdiv(g, QP, invQP);
+            const int k = g - cl * QP;
+            int4 sg = segt[0];
+            for (int t = 1; t < nseg; ++t) {
+                const int4 st = segt[t];
+                if (k >= st.x) sg = st;
+            }
+            // gaps and invalid rows copy the channel's first group (in bounds, never read unmasked)
+            const int off = cl * (int)HW + ((sg.z >= 0 && k < sg.y) ? sg.z + 4 * (k - sg.x) : 0);
+            roff[j] = 4u * (unsigned)off;
         }
 #pragma unroll
         for (int j = 0; j < DMA_MAXW; ++j) {
@@ -366,15 +409,15 @@ __global__ __launch_bounds__(256) void bn_relu_pool_kernel(const float* __restri
 
 }  // namespace
 
-int conv3x3_dma_ck(int pro, int cout, int W, int NR, int cin) {
+int conv3x3_dma_ck(int pro, int cout, int PL, int NR, int cin) {
     // largest K-chunk whose double-buffered raw image + weights let dma_occ blocks share a CU
     const int nsrc = pro == PRO_BNBWD ? 2 : 1;
     const int cout_t = cout == 32 ? 32 : 64;
     for (int ck = 8; ck >= 2; ck >>= 1) {
         if (cin % ck) continue;
-        size_t raw = (size_t)nsrc * ck * NR * W + 256;
+        size_t raw = (size_t)nsrc * ck * PL + 256;
         size_t wts = (size_t)9 * ck * cout_t + 256;
-        size_t bytes = (2 * raw + 2 * wts + 4 * (size_t)cin + 2 * NR + 8) * 4;
+        size_t bytes = (2 * raw + 2 * wts + (size_t)dma_table_floats(cin, NR)) * 4;
         if (bytes <= (size_t)160 * 1024 / dma_occ(cout == 32 ? 1 : 2)) return ck;
     }
     return 2;
@@ -389,28 +432,42 @@ int launch_conv3x3_dma(int pro, int epi, ConvArgs a, hipStream_t s) {
     const int ntile = ceil_div(M, bp);
     PCX_CHECK_ARG(a.nblk == ntile, "conv3x3: partial buffer sized for %d tiles, need %d", a.nblk, ntile);
     a.NR = (bp - 1 + a.W - 1) / a.W + 1 + 2;
-    const int ck = conv3x3_dma_ck(pro, a.cout, a.W, a.NR, a.cin);
-    PCX_CHECK_ARG(a.cin % ck == 0, "conv3x3: cin %d not a multiple of %d", a.cin, ck);
-    const int vec = (a.W % 4 == 0) ? 4 : 1;
     const int nsrc = pro == PRO_BNBWD ? 2 : 1;
-    const int PL = a.NR * a.W;
+    // Preferred: segment layout (16-byte copies at any W, offsets precomputed per tile).  A tile's
+    // rows span at most NR / H + 2 samples plus an invalid run at either end; each segment costs
+    // at most 7 floats of alignment gap.
+    const int64_t HW = (int64_t)a.H * a.W;
+    const int PLseg = ((a.NR * a.W + 8 * (a.NR / a.H + 4)) + 3) & ~3;
+    int ck = conv3x3_dma_ck(pro, a.cout, PLseg, a.NR, a.cin);
+    bool pre = nsrc == 1 && HW % 4 == 0 && a.cin % ck == 0 && ceil_div(ck * PLseg, 1024) <= DMA_MAXR &&
+               ceil_div(9 * ck * cout_t, 1024) <= DMA_MAXW &&
+               (int64_t)((a.NR / a.H + 3) * a.cin) * HW * 4 < ((int64_t)1 << 31);
+    int vec = 4, PL = PLseg;
+    if (pre) {
+        a.RS = PLseg;
+    } else {
+        vec = (a.W % 4 == 0) ? 4 : 1;
+        PL = a.NR * a.W;
+        ck = conv3x3_dma_ck(pro, a.cout, PL, a.NR, a.cin);
+    }
+    PCX_CHECK_ARG(a.cin % ck == 0, "conv3x3: cin %d not a multiple of %d", a.cin, ck);
     const int rawf = ((nsrc * ck * PL + 64 * vec - 1) / (64 * vec)) * (64 * vec);
     const int wtsf = ((9 * ck * cout_t + 255) / 256) * 256;
-    size_t smem = ((size_t)4 * a.cin + ((2 * a.NR + 3) & ~3) + 2 * (size_t)rawf + 2 * (size_t)wtsf) * 4;
+    size_t smem = ((size_t)dma_table_floats(a.cin, a.NR) + 2 * (size_t)rawf + 2 * (size_t)wtsf) * 4;
     size_t red = ((size_t)4 * cout_t * 3 + 4 * (size_t)cout_t) * 4;  // epilogue partials + cf table
     if (smem < red) smem = red;
     PCX_CHECK_ARG(smem <= 160 * 1024, "conv3x3_dma: W=%d needs %zu B of LDS", a.W, smem);
     dim3 grid((unsigned)(ntile * (a.cout / cout_t)));
-    // copies per wave and chunk (wave 0 issues the most): precomputed offsets when they fit
-    const bool pre = vec == 4 && ceil_div(nsrc * ck * PL, 256 * vec) <= DMA_MAXR && ceil_div(9 * ck * cout_t, 1024) <= DMA_MAXW &&
-                     (int64_t)((a.NR / a.H + 2) * a.cin) * a.H * a.W * 4 < ((int64_t)1 << 31) && nsrc == 1;
 #define PCX_DMA_CASE(WM_, WN_, V_, P_, E_, CK_)                                                   \
     if (wm == WM_ && vec == V_ && pro == P_ && epi == E_ && ck == CK_) {                         \
-        if (pre) {                                                                               \
+        if constexpr (V_ == 4) if (pre) {                                                        \
             (void)hipFuncSetAttribute((const void*)conv3x3_dma_kernel<WM_, WN_, V_, P_, E_, CK_, true>, \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);    \
             conv3x3_dma_kernel<WM_, WN_, V_, P_, E_, CK_, true><<<grid, 256, smem, s>>>(a);      \
-        } else {                                                                                 \
+            PCX_LAUNCH_CHECK("conv3x3_dma_kernel");                                              \
+            return PCX_OK;                                                                       \
+        }                                                                                        \
+        {                                                                                        \
             (void)hipFuncSetAttribute((const void*)conv3x3_dma_kernel<WM_, WN_, V_, P_, E_, CK_, false>, \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);    \
             conv3x3_dma_kernel<WM_, WN_, V_, P_, E_, CK_, false><<<grid, 256, smem, s>>>(a);     \

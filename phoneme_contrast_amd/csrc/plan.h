@@ -97,7 +97,7 @@ struct Plan {
 
     size_t carve(const char* name, size_t bytes) {
         size_t off = total;
-        total += (bytes + 255) / 256 * 256;
+        total += (bytes + 256 + 255) / 256 * 256;  // >= 256 B slack: 16-byte conv copies may overrun a tensor end by 12 B
         regions.push_back({name, off, bytes});
         return off;
     }
