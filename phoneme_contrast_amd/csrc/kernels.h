@@ -85,6 +85,7 @@ struct WgradArgs {
     int R, CW, nseg, nrb, nchunks, per_slice, nslice;
     int MT, NPM, NPC;     // MFMA tile (16 or 32), tiles per block along cout / cin
     int VX;               // wgrad_win: vector width of the x staging
+    int KW, ntslice;      // wgrad_w32: waves splitting K on one tile, task slices (nslice = ntslice * KW)
     int expt;             // timing experiments only (PCX_WGRAD_EXPT): 1 no staging, 2 no MFMA, 4 no barrier
 };
 int launch_wgrad3x3(int pro, WgradArgs a, hipStream_t s);
@@ -94,6 +95,9 @@ int launch_wgrad_pipe(int pro, WgradArgs a, hipStream_t s);
 void wgrad_pipe_geometry(int B, int H, int W, int cin, int cout, WgradArgs* a);
 // sliding-row-window variant (wgrad_win.hip, the default): prologues PRO_RAW / PRO_BNRELU
 int launch_wgrad_win(int pro, WgradArgs a, hipStream_t s);
+// same row window on 32 x 32 tiles (wgrad_w32.hip; channels multiples of 32): false if it does not apply
+bool wgrad_w32_geometry(int B, int H, int W, int cin, int cout, WgradArgs* a);
+int launch_wgrad_w32(int pro, WgradArgs a, hipStream_t s);
 void wgrad_win_geometry(int B, int H, int W, int cin, int cout, WgradArgs* a);
 
 // first-layer (Cin = 1) weight gradient

@@ -61,7 +61,10 @@ int build_small(Plan& p) {
             L.wp = p.carve("wp", (size_t)9 * L.cin * L.cout * 4);
             L.wpd = p.carve("wpd", (size_t)9 * L.cin * L.cout * 4);
             L.nblk = (int)conv3x3_nblk(B, L.H, L.W, L.cout);
-            if (p.wgrad_impl == 0) wgrad_win_geometry(B, L.H, L.W, L.cin, L.cout, &L.wg);
+            if (p.wgrad_impl == 0) {
+                if (!wgrad_w32_geometry(B, L.H, L.W, L.cin, L.cout, &L.wg))
+                    wgrad_win_geometry(B, L.H, L.W, L.cin, L.cout, &L.wg);
+            } else if (p.wgrad_impl == 3) wgrad_win_geometry(B, L.H, L.W, L.cin, L.cout, &L.wg);
             else if (p.wgrad_impl == 1) wgrad_pipe_geometry(B, L.H, L.W, L.cin, L.cout, &L.wg);
             else wgrad3x3_geometry(B, L.H, L.W, L.cin, L.cout, &L.wg);
             wg = std::max(wg, (size_t)L.wg.nslice * L.cout * L.cin * 9);
@@ -333,7 +336,8 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
             if (const char* e = getenv("PCX_WGRAD_EXPT")) w.expt = atoi(e);
             {
                 Scope sc(&p.prof, s, "wgrad", l);
-                RC(p.wgrad_impl == 0 ? launch_wgrad_win(pro, w, s)
+                RC(p.wgrad_impl == 0 || p.wgrad_impl == 3
+                       ? (w.MT == 32 ? launch_wgrad_w32(pro, w, s) : launch_wgrad_win(pro, w, s))
                    : p.wgrad_impl == 1 ? launch_wgrad_pipe(pro, w, s) : launch_wgrad3x3(pro, w, s));
             }
             { Scope sc(&p.prof, s, "wgrad_reduce", l); RC(launch_sum_slices(wgp, w.nslice, (int64_t)L.cout * L.cin * 9, G[p_conv_w(l)], s)); }
@@ -414,7 +418,9 @@ extern "C" void* pcx_net_create(const pcx_net_config* cfg, int64_t B, int64_t F,
         const char* impl = getenv("PCX_CONV");  // A/B switch for measurements: "legacy" = conv.hip
         p->dma = !(impl && strcmp(impl, "legacy") == 0);
         const char* wg = getenv("PCX_WGRAD");  // "dma" / "legacy" for A/B measurements
-        p->wgrad_impl = (!p->dma || (wg && strcmp(wg, "legacy") == 0)) ? 2 : (wg && strcmp(wg, "pipe") == 0) ? 1 : 0;
+        p->wgrad_impl = (!p->dma || (wg && strcmp(wg, "legacy") == 0)) ? 2
+                        : (wg && strcmp(wg, "pipe") == 0) ? 1
+                        : (wg && strcmp(wg, "win16") == 0) ? 3 : 0;
     }
     int rc = PCX_EINVAL;
     if (cfg->kind == PCX_NET_CNN_SMALL) rc = build_small(*p);

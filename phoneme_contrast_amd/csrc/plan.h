@@ -92,7 +92,8 @@ struct Plan {
     std::vector<Region> regions;
     int nparams, nbn, ndrop, drop_ch[4];
     bool dma;                       // LDS-DMA conv path (default); PCX_CONV=legacy selects conv.hip
-    int wgrad_impl;                 // 0 row window (default), 1 pipelined chunks, 2 wgrad.hip (PCX_WGRAD)
+    int wgrad_impl;                 // 0 row window, 32x32 tiles where they apply (default), 1 pipelined
+                                    // chunks, 2 wgrad.hip, 3 row window on 16x16 tiles (PCX_WGRAD)
     mutable Profiler prof;
 
     size_t carve(const char* name, size_t bytes) {
