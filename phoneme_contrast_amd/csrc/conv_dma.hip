@@ -19,7 +19,8 @@ typedef __attribute__((address_space(3))) void lds_void;
 
 // Timing-decomposition builds only (scripts/conv_expt.sh compiles this file with
 // -DPCX_CONV_EXPT=bits into a separate library): 1 no DMA after the first chunk, 2 no MFMA,
-// 4 no epilogue, 8 no per-chunk wait / barrier, 16 no prologue / padding masks.  Results are garbage in those builds.
+// 4 no epilogue, 8 no per-chunk wait / barrier, 16 no prologue / padding masks, 32 no LDS reads of
+// the pixel operand.  Results are garbage in those builds.
 #ifndef PCX_CONV_EXPT
 #define PCX_CONV_EXPT 0
 #endif
@@ -301,7 +302,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_occ(WM)
 #pragma unroll
             for (int ni = 0; ni < WN; ++ni) {
                 const int o = (2 * s + h) * PL + pixoff[ni] + toff;
-                r_[ni] = raw[o];
+                r_[ni] = (PCX_CONV_EXPT & 32) ? (float)(o & 7) : raw[o];
                 if (PRO == PRO_BNBWD) r2_[ni] = raw[o + CK * PL];
             }
         };

@@ -11,6 +11,36 @@ __device__ __forceinline__ float conv_sum32(float v) {  // reduce within each 32
     return v;
 }
 
+// Transposed butterfly: v[r] (r < 16) summed over the 32 lanes of each half-wave in 16 shuffles
+// (instead of 16 x 5).  Lane l of a half returns the total of r = (l >> 1) & 15.  `sel` gets the
+// same lane-bit selection applied to a half-uniform array (no shuffles): sel = u[(l >> 1) & 15].
+__device__ __forceinline__ float xsum16(const float (&v)[16], int l32) {
+    const bool b4 = l32 & 16, b3 = l32 & 8, b2 = l32 & 4, b1 = l32 & 2;
+    float w8[8], w4[4], w2[2];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w8[j] = (b4 ? v[j + 8] : v[j]) + __shfl_xor(b4 ? v[j] : v[j + 8], 16, 64);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w4[j] = (b3 ? w8[j + 4] : w8[j]) + __shfl_xor(b3 ? w8[j] : w8[j + 4], 8, 64);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) w2[j] = (b2 ? w4[j + 2] : w4[j]) + __shfl_xor(b2 ? w4[j] : w4[j + 2], 4, 64);
+    float w1 = (b1 ? w2[1] : w2[0]) + __shfl_xor(b1 ? w2[0] : w2[1], 2, 64);
+    return w1 + __shfl_xor(w1, 1, 64);
+}
+__device__ __forceinline__ float xsel16(const float (&u)[16], int l32) {
+    const bool b4 = l32 & 16, b3 = l32 & 8, b2 = l32 & 4, b1 = l32 & 2;
+    float w8[8], w4[4], w2[2];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w8[j] = b4 ? u[j + 8] : u[j];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w4[j] = b3 ? w8[j + 4] : w8[j];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) w2[j] = b2 ? w4[j + 2] : w4[j];
+    return b1 ? w2[1] : w2[0];
+}
+__device__ __forceinline__ float readlane_f(float v, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+
 template <int WM, int WN, int EPI>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[WM][WN], float* red,
                                               int tile, int n0, int64_t m0, int64_t Mtot, int64_t HW,
@@ -20,34 +50,41 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[W
     const int lane = tid & 63, h = lane >> 5, l32 = lane & 31;
     const int cnt_w = (int)max((int64_t)0, min((int64_t)WN * 32, Mtot - (m0 + wave * WN * 32)));
     if (EPI == EPI_FWD) {
+        // store y; per (wave, channel) Chan statistics shifted by the channel's first pixel of the
+        // half-wave (K, read with v_readlane), reduced with the transposed butterfly
+        float* ob[WN];
 #pragma unroll
-        for (int mi = 0; mi < WM; ++mi)
+        for (int ni = 0; ni < WN; ++ni) ob[ni] = a.out + ((int64_t)pb[ni] * a.cout + n0 + 4 * h) * HW + pp[ni];
+#pragma unroll
+        for (int mi = 0; mi < WM; ++mi) {
+            float kv[16], s1[16], s2[16];
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int chl = mi * 32 + acc_row(r, h);
-                const int ch = n0 + chl;
-                float K = __shfl(acc[mi][0][r], h * 32, 64);
-                float s1 = 0.f, s2 = 0.f;
+                const float k0 = readlane_f(acc[mi][0][r], 0), k1 = readlane_f(acc[mi][0][r], 32);
+                kv[r] = h ? k1 : k0;
+                const int64_t co = (int64_t)(mi * 32 + (r & 3) + 8 * (r >> 2)) * HW;
+                s1[r] = 0.f;
+                s2[r] = 0.f;
 #pragma unroll
                 for (int ni = 0; ni < WN; ++ni) {
-                    float v = acc[mi][ni][r];
+                    const float v = acc[mi][ni][r];
                     if (valid[ni]) {
-                        a.out[((int64_t)pb[ni] * a.cout + ch) * HW + pp[ni]] = v;
-                        float d = v - K;
-                        s1 += d;
-                        s2 = fmaf(d, d, s2);
+                        ob[ni][co] = v;
+                        const float d = v - kv[r];
+                        s1[r] += d;
+                        s2[r] = fmaf(d, d, s2[r]);
                     }
                 }
-                s1 = conv_sum32(s1);
-                s2 = conv_sum32(s2);
-                if (l32 == 0) {
-                    float n = (float)cnt_w;
-                    float mean = cnt_w ? K + s1 / n : 0.f;
-                    float m2 = cnt_w ? fmaxf(s2 - s1 * s1 / n, 0.f) : 0.f;
-                    float* d = red + (wave * COUT_T + chl) * 3;
-                    d[0] = n; d[1] = mean; d[2] = m2;
-                }
             }
+            const float t1 = xsum16(s1, l32), t2 = xsum16(s2, l32), K = xsel16(kv, l32);
+            if (!(l32 & 1)) {
+                const float n = (float)cnt_w;
+                const float mean = cnt_w ? K + t1 / n : 0.f;
+                const float m2 = cnt_w ? fmaxf(t2 - t1 * t1 / n, 0.f) : 0.f;
+                float* d = red + (wave * COUT_T + mi * 32 + acc_row(l32 >> 1, h)) * 3;
+                d[0] = n; d[1] = mean; d[2] = m2;
+            }
+        }
         __syncthreads();
         if (tid < COUT_T) {
             float n = 0.f, mean = 0.f, m2 = 0.f;
@@ -95,7 +132,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[W
         }
         const int chs = (EPI == EPI_BWD_RELU) ? (int)HW : a.Hs * a.Ws;  // channel-plane stride
 #pragma unroll
-        for (int mi = 0; mi < WM; ++mi)
+        for (int mi = 0; mi < WM; ++mi) {
+            float sz[16], sx[16];
 #pragma unroll
             for (int rb = 0; rb < 16; rb += RB) {
                 constexpr int NY = (EPI == EPI_BWD_RELU) ? 1 : 4;
@@ -152,14 +190,16 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[W
                         sdx = fmaf(d, (ya - cf.z) * cf.w, sdx);
                     }
                 }
-                sdz = conv_sum32(sdz);
-                sdx = conv_sum32(sdx);
-                if (l32 == 0) {
-                    float* d = red + (wave * COUT_T + chl) * 2;
-                    d[0] = sdz; d[1] = sdx;
-                }
+                sz[r] = sdz;
+                sx[r] = sdx;
                 }
             }
+            const float tz = xsum16(sz, l32), tx = xsum16(sx, l32);
+            if (!(l32 & 1)) {
+                float* d = red + (wave * COUT_T + mi * 32 + acc_row(l32 >> 1, h)) * 2;
+                d[0] = tz; d[1] = tx;
+            }
+        }
         __syncthreads();
         if (tid < COUT_T) {
             float s0 = 0.f, s1 = 0.f;
