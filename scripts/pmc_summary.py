@@ -20,6 +20,7 @@ ORDER = {
     "conv3x3_dma_kernel": FWD + DGRAD,
     "wgrad_pipe_kernel": [f"wgrad_L{l}" for l in range(6, 1, -1)],
     "wgrad_win_kernel": [f"wgrad_L{l}" for l in range(6, 1, -1)],
+    "wgrad_w32_kernel": [f"wgrad_L{l}" for l in range(6, 3, -1)],
     "wgrad3x3_kernel": [f"wgrad_L{l}" for l in range(6, 1, -1)],
     "bn_relu_pool_kernel": ["bn_relu_pool_L3", "bn_relu_pool_L5"],
     "conv1_fwd_kernel": ["conv1_fwd_L1"],
@@ -28,6 +29,15 @@ ORDER = {
     "supcon_grad_partial": ["supcon_grad"],
     "adam_kernel": ["adam"],
 }
+
+
+def order_for(per):
+    """Layer labels per family; the 32x32 wgrad takes the cin >= 64 layers (L6..L4), the 16x16
+    one the rest (L3, L2) when both run."""
+    o = dict(ORDER)
+    if "wgrad_w32_kernel" in per:
+        o["wgrad_win_kernel"] = ["wgrad_L3", "wgrad_L2"]
+    return o
 
 
 def family(name):
@@ -54,8 +64,9 @@ def counters(path, counter):
         if k:
             per[k].append(float(r["Counter_Value"]))
     out = defaultdict(list)
+    order = order_for(per)
     for k, vals in per.items():
-        labs = ORDER[k]
+        labs = order[k]
         for i, v in enumerate(vals):
             out[labs[i % len(labs)]].append(v)
     return out
@@ -68,8 +79,9 @@ def durations(path):
         if k:
             per[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
     out = defaultdict(list)
+    order = order_for(per)
     for k, vals in per.items():
-        labs = ORDER[k]
+        labs = order[k]
         for i, v in enumerate(vals):
             out[labs[i % len(labs)]].append(v)
     return {k: {"avg_ms": round(sum(v) / len(v), 4), "launches": len(v)} for k, v in out.items()}
