@@ -118,6 +118,51 @@ int pcx_net_profile_read(void* plan, char* labels, size_t labels_len, float* tot
 int pcx_dropout_masks(float* out, int64_t n, float p, uint64_t seed, uint64_t offset,
                       hipStream_t stream);
 
+/* ------------------------------------------------------------------ feature path
+ * Replaces torchaudio.transforms.MFCC / MelSpectrogram + AmplitudeToDB as called by
+ * MFCCExtractor / MelSpectrogramExtractor (src/datasets/features.py:22-150), the random gain of
+ * PhonemeContrastiveDataset._augment_waveform (src/datasets/dataset.py:147-172) and the
+ * TimeMask / FrequencyMask / GaussianNoise transforms (src/datasets/transforms.py:25-97).
+ *
+ * pcx_melspec: wave [n][S] fp32, gain [n] or NULL -> mel [n][n_mels][T] (T = 1 + S / hop; periodic
+ * hann, center=True reflect padding, power 2) and tile_max [n][ceil(T/32)].  fb is the HTK mel
+ * filterbank [n_freq][n_mels] zero-padded to [fb_rows = ceil((n_fft/2+1)/32)*32][fb_cols =
+ * ceil(n_mels/32)*32].  n_fft/2+1 <= 256, n <= 65535 per call.
+ * pcx_mel_finish: dB = 10 log10(max(mel, 1e-10)), floored at (max over a group of clamp_group
+ * consecutive clips) - top_db when top_db > 0; then out[v][k][t] = sum_m dct[m][k] dB[m][t]
+ * (dct [n_mels][n_out], DCT-II ortho) or, dct == NULL, out = dB.  gmax_ws: ceil(n/clamp_group)
+ * floats.  out view stride out_stride >= n_out * T (room for delta features after the block).
+ * pcx_compute_deltas: ComputeDeltas(win_length=5, mode="replicate") of [n][F][T] blocks.
+ * pcx_specaug: in place on x [n][F][T]: t in [tband[2v], tband[2v+1]) or f in [fband[2v],
+ * fband[2v+1]) -> 0 (bands may be NULL), then + level[v] * noise (noise [n][F][T] given, or drawn
+ * from N(0,1) by a counter-based generator keyed by seed when noise == NULL). */
+int pcx_melspec(const float* wave, int64_t n, int64_t S, const float* gain, const float* fb, int n_fft,
+                int hop, int n_mels, int fb_rows, int fb_cols, float* mel, float* tile_max,
+                hipStream_t stream);
+int pcx_mel_finish(const float* mel, const float* tile_max, int64_t n, int64_t T, int n_mels,
+                   int clamp_group, float top_db, const float* dct, int n_out, float* gmax_ws,
+                   float* out, int64_t out_stride, hipStream_t stream);
+int pcx_compute_deltas(const float* in, int64_t in_stride, float* out, int64_t out_stride, int64_t n,
+                       int F, int64_t T, hipStream_t stream);
+int pcx_specaug(float* x, int64_t n, int F, int64_t T, const int* tband, const int* fband,
+                const float* level, const float* noise, uint64_t seed, hipStream_t stream);
+
+/* Host-side (no GPU) reproduction of the reference's per-view random draws, bit-exact with
+ * Python's `random` and torch's CPU generator as the reference calls them: for view v,
+ * gain[v] from seed gain_seeds[v] (dataset.py:147-172) and, from aug_seeds[v] (+1000 per enabled
+ * transform, transforms.py:139-143), the time band, frequency band ([start, end), {0, 0} when
+ * not drawn) and the noise level (0 when not drawn).  Either seed array may be NULL. */
+typedef struct pcx_aug_config {  /* probabilities and bounds are doubles, as the Python floats */
+    int time_enabled, time_width;
+    double time_prob;
+    int freq_enabled, freq_width;
+    double freq_prob;
+    int noise_enabled;
+    double noise_min, noise_max, noise_prob;
+} pcx_aug_config;
+int pcx_draw_view_params(const int64_t* gain_seeds, const int64_t* aug_seeds, int64_t n, int F, int T,
+                         const pcx_aug_config* cfg, float* gain, int* tband, int* fband, float* level);
+
 #ifdef __cplusplus
 }
 #endif

@@ -67,7 +67,28 @@ SIGNATURES = {
                                      c_int]),
     "pcx_dropout_masks": (c_int, [c_void_p, c_i64, c_float, ctypes.c_uint64, ctypes.c_uint64,
                                   c_void_p]),
+    "pcx_melspec": (c_int, [c_void_p, c_i64, c_i64, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                            c_int, c_void_p, c_void_p, c_void_p]),
+    "pcx_mel_finish": (c_int, [c_void_p, c_void_p, c_i64, c_i64, c_int, c_int, c_float, c_void_p,
+                               c_int, c_void_p, c_void_p, c_i64, c_void_p]),
+    "pcx_compute_deltas": (c_int, [c_void_p, c_i64, c_void_p, c_i64, c_i64, c_int, c_i64,
+                                   c_void_p]),
+    "pcx_specaug": (c_int, [c_void_p, c_i64, c_int, c_i64, c_void_p, c_void_p, c_void_p, c_void_p,
+                            ctypes.c_uint64, c_void_p]),
 }
+
+
+class AugConfig(ctypes.Structure):
+    """pcx_aug_config (include/pcx.h)."""
+    _fields_ = [("time_enabled", c_int), ("time_width", c_int), ("time_prob", ctypes.c_double),
+                ("freq_enabled", c_int), ("freq_width", c_int), ("freq_prob", ctypes.c_double),
+                ("noise_enabled", c_int), ("noise_min", ctypes.c_double), ("noise_max", ctypes.c_double),
+                ("noise_prob", ctypes.c_double)]
+
+
+SIGNATURES["pcx_draw_view_params"] = (c_int, [c_void_p, c_void_p, c_i64, c_int, c_int,
+                                              ctypes.POINTER(AugConfig), c_void_p, c_void_p,
+                                              c_void_p, c_void_p])
 
 
 class PcxError(RuntimeError):

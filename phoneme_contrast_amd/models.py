@@ -245,9 +245,10 @@ class _NativeNet(BaseModel):
             grads.append(flat[off:off + n].view_as(p))
             off += n
         da = _ptr_array(masks) if masks is not None else None
+        g_emb = demb.contiguous().float()  # held until the launch is enqueued
         _lib.check(lib.pcx_net_backward(plan.handle, _ptr_array([p.detach() for p in params]),
                                         _lib.ptr(x), da, _lib.ptr(emb),
-                                        _lib.ptr(demb.contiguous().float()), _ptr_array(grads),
+                                        _lib.ptr(g_emb), _ptr_array(grads),
                                         _lib.ptr(ws), plan.ws_bytes, _lib.stream_of(x)),
                    "pcx_net_backward")
         return grads
