@@ -7,6 +7,10 @@
 //  mode 1  data grad   dx[b,c,ih,iw]  = sum_{n,kh,kw} W[n,c,kh,kw] dy[b,n,(ih+p-kh)/s,(iw+p-kw)/s]
 //                      (only taps where the division is exact and in range)
 //                      GEMM  M = cin,  N = B*IH*IW, K = cout*KH*KW
+//  mode 3  data grad of a stride-2 conv for one parity class (ih % 2, iw % 2) = (ph, pw): only the
+//          taps kh = ph + p (mod 2), kw = pw + p (mod 2) reach those pixels, so the class is a dense
+//          GEMM  M = cin, N = B*ceil((IH-ph)/2)*ceil((IW-pw)/2), K = cout*(valid taps); the four
+//          classes cover dx exactly once with none of mode 1's zero taps (3/4 of its K at stride 2)
 //  mode 2  weight grad dW[n,c,kh,kw]  = sum_{b,oh,ow} dy[b,n,oh,ow] x[b,c,oh*s-p+kh,ow*s-p+kw]
 //                      GEMM  M = cout, N = cin*KH*KW, K = B*OH*OW split into slices (partials)
 //
@@ -36,9 +40,16 @@ __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
     const int64_t OHW = (int64_t)a.OH * a.OW, IHW = (int64_t)a.IH * a.IW;
     const int s = a.stride, pad = a.pad;
 
+    // parity class (mode 3): pixels (2 ihc + ph, 2 iwc + pw), taps kh0 + 2 i, kw0 + 2 j
+    const int ph = a.par >> 1, pw = a.par & 1;
+    const int kh0 = (ph + pad) & 1, kw0 = (pw + pad) & 1;
+    const int nth = (KH - kh0 + 1) / 2, ntw = (KW - kw0 + 1) / 2, KKp = nth * ntw;
+    const int IHc = (a.IH - ph + 1) / 2, IWc = (a.IW - pw + 1) / 2;
+    const int64_t CHW = (int64_t)IHc * IWc;
     int64_t M, N, K;
     if (MODE == 0) { M = a.cout; N = a.B * OHW; K = (int64_t)a.cin * KK; }
     else if (MODE == 1) { M = a.cin; N = a.B * IHW; K = (int64_t)a.cout * KK; }
+    else if (MODE == 3) { M = a.cin; N = a.B * CHW; K = (int64_t)a.cout * KKp; }
     else { M = a.cout; N = (int64_t)a.cin * KK; K = a.B * OHW; }
     const int64_t mt = (M + BM - 1) / BM, nt = (N + BN - 1) / BN;
     int64_t bid = blockIdx.x;
@@ -64,11 +75,17 @@ __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
     int64_t xbase = 0;             // mode 0: x + b*cin*IHW ; mode 1: dy + b*cout*OHW
     int ih0 = 0, iw0 = 0;          // mode 0: oh*s-p, ow*s-p ; mode 1: ih+p, iw+p
     bool bvalid = false;
-    if (MODE == 0 || MODE == 1) {
+    if (MODE == 0 || MODE == 1 || MODE == 3) {
         const int64_t m = n0 + bcol;
         bvalid = m < N;
         const int64_t mm = bvalid ? m : 0;
-        if (MODE == 0) {
+        if (MODE == 3) {
+            const int64_t b = mm / CHW, p = mm - b * CHW;
+            const int ihc = (int)(p / IWc), iwc = (int)(p - (int64_t)(p / IWc) * IWc);
+            xbase = b * a.cout * OHW;
+            ih0 = 2 * ihc + ph + pad;
+            iw0 = 2 * iwc + pw + pad;
+        } else if (MODE == 0) {
             const int64_t b = mm / OHW, p = mm - b * OHW;
             const int oh = (int)(p / a.OW), ow = (int)(p - (int64_t)(p / a.OW) * a.OW);
             xbase = b * a.cin * IHW;
@@ -141,6 +158,27 @@ __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
                         if (ok && oh < a.OH && ow < a.OW)
                             v = a.dy[xbase + ((int64_t)nn * a.OH + oh) * a.OW + ow];
                     }
+                }
+                rb[i] = v;
+            }
+        } else if (MODE == 3) {
+            const int64_t k = kbase + kq;
+            const int n = KKp ? (int)(k / KKp) : 0, r = (int)(k - (int64_t)n * KKp);
+            const int kh = kh0 + 2 * (ntw ? r / ntw : 0), kw = kw0 + 2 * (ntw ? r % ntw : 0);
+#pragma unroll
+            for (int j = 0; j < NA; ++j) {
+                const int64_t c = m0 + colq + 16 * j;
+                ra[j] = (c < M && k < K) ? a.w[(((int64_t)n * a.cin + c) * KH + kh) * KW + kw] : 0.f;
+            }
+#pragma unroll
+            for (int i = 0; i < NBv; ++i) {
+                const int64_t kb = kbase + brow + BROWS * i;
+                float v = 0.f;
+                if (bvalid && kb < K) {
+                    const int nn = (int)(kb / KKp), rr = (int)(kb - (int64_t)(kb / KKp) * KKp);
+                    const int oh = (ih0 - (kh0 + 2 * (rr / ntw))) >> 1, ow = (iw0 - (kw0 + 2 * (rr % ntw))) >> 1;
+                    if (oh >= 0 && ow >= 0 && oh < a.OH && ow < a.OW)
+                        v = a.dy[xbase + ((int64_t)nn * a.OH + oh) * a.OW + ow];
                 }
                 rb[i] = v;
             }
@@ -229,6 +267,11 @@ __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
             const int64_t b = col / IHW;
             obase = b * a.cin * IHW + (col - b * IHW);
             ostride = IHW;
+        } else if (MODE == 3) {
+            const int64_t b = col / CHW, p = col - b * CHW;
+            const int ihc = (int)(p / IWc), iwc = (int)(p - (int64_t)(p / IWc) * IWc);
+            obase = b * a.cin * IHW + (int64_t)(2 * ihc + ph) * a.IW + 2 * iwc + pw;
+            ostride = IHW;
         } else {
             obase = (int64_t)slice * M * N + col;
             ostride = N;
@@ -240,7 +283,7 @@ __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
                 const int64_t row = m0 + wr * 32 * WM + mi * 32 + acc_row(r, h);
                 if (row < M) {
                     float* o = a.out + obase + row * ostride;
-                    if (MODE == 1 && a.accumulate) *o += acc[mi][ni][r];
+                    if ((MODE == 1 || MODE == 3) && a.accumulate) *o += acc[mi][ni][r];
                     else *o = acc[mi][ni][r];
                 }
             }
@@ -367,69 +410,67 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* g, const
         dy[o + p] = k.x * (g[o + p] - k.y - (y[o + p] - k.w) * k.z);
 }
 
-// MaxPool2d(3, stride 2, pad 1) of relu(BN(y))  (reference phoneme_cnn.py:211-216)
+// MaxPool2d(3, stride 2, pad 1) of relu(BN(y))  (reference phoneme_cnn.py:211-216).  One block per
+// channel plane (32-bit index math).  Also records, per window, the tap (kh*3 + kw) of its first
+// maximum in row-major scan order (torch's tie rule), or 255 when that maximum is 0 (the ReLU then
+// passes no gradient), so the backward never re-reads y.
 __global__ __launch_bounds__(256) void maxpool3_fwd_kernel(const float* __restrict__ y, const float4* __restrict__ cf,
-                                                           float* __restrict__ out, int64_t rows, int C, int H,
-                                                           int W, int OH, int OW) {
-    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int64_t n = rows * OH * OW;
-    if (e >= n) return;
-    const int64_t row = e / ((int64_t)OH * OW);
-    const int p = (int)(e - row * OH * OW);
-    const int oh = p / OW, ow = p % OW;
+                                                           float* __restrict__ out, uint8_t* __restrict__ arg, int C,
+                                                           int H, int W, int OH, int OW) {
+    const int64_t row = blockIdx.x;
     const float4 k = cf[(int)(row % C)];
     const float* yp = y + row * H * W;
-    float m = -INFINITY;
-    for (int kh = 0; kh < 3; ++kh) {
-        const int ih = 2 * oh - 1 + kh;
-        if (ih < 0 || ih >= H) continue;
-        for (int kw = 0; kw < 3; ++kw) {
-            const int iw = 2 * ow - 1 + kw;
-            if (iw < 0 || iw >= W) continue;
-            m = fmaxf(m, fmaxf(fmaf(yp[ih * W + iw], k.x, k.y), 0.f));
+    float* op = out + row * OH * OW;
+    uint8_t* ap = arg + row * OH * OW;
+    // rows x columns walk (no per-element division): OW-wide row segments of 256 threads
+    const int segs = (OW + 255) / 256;
+    for (int q = 0; q < OH * segs; ++q) {
+        const int oh = q / segs, ow = (q - oh * segs) * 256 + threadIdx.x;
+        if (ow >= OW) continue;
+        const int p = oh * OW + ow;
+        float m = -INFINITY;
+        int best = 0;
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) {
+            const int ih = 2 * oh - 1 + kh;
+            if (ih < 0 || ih >= H) continue;
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+                const int iw = 2 * ow - 1 + kw;
+                if (iw < 0 || iw >= W) continue;
+                const float v = fmaxf(fmaf(yp[ih * W + iw], k.x, k.y), 0.f);
+                if (v > m) { m = v; best = kh * 3 + kw; }
+            }
         }
+        op[p] = m;
+        ap[p] = m > 0.f ? (uint8_t)best : (uint8_t)255;
     }
-    out[e] = m;
 }
 
-// gradient of MaxPool(3,2,1)(relu(BN(y))) w.r.t. the BN output: each input position collects the
-// windows whose first maximum (row-major scan, torch's tie rule) it is, times the ReLU mask
-__global__ __launch_bounds__(256) void maxpool3_bwd_kernel(const float* __restrict__ y, const float4* __restrict__ cf,
+// gradient of MaxPool(3,2,1)(relu(BN(y))) w.r.t. the BN output: each input position collects
+// dout of the (at most 2 x 2) windows whose recorded first maximum it is
+__global__ __launch_bounds__(256) void maxpool3_bwd_kernel(const uint8_t* __restrict__ arg,
                                                            const float* __restrict__ dout, float* __restrict__ dz,
-                                                           int64_t rows, int C, int H, int W, int OH, int OW) {
-    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int64_t n = rows * H * W;
-    if (e >= n) return;
-    const int64_t row = e / ((int64_t)H * W);
-    const int p = (int)(e - row * H * W);
-    const int ih = p / W, iw = p % W;
-    const float4 k = cf[(int)(row % C)];
-    const float* yp = y + row * H * W;
-    const float z = fmaf(yp[p], k.x, k.y);
-    float g = 0.f;
-    if (z > 0.f) {
-        const int oh_lo = max(0, ih / 2), oh_hi = min(OH - 1, (ih + 1) / 2);
-        const int ow_lo = max(0, iw / 2), ow_hi = min(OW - 1, (iw + 1) / 2);
+                                                           int H, int W, int OH, int OW) {
+    const int64_t row = blockIdx.x;
+    const uint8_t* ap = arg + row * OH * OW;
+    const float* dp = dout + row * OH * OW;
+    float* zp = dz + row * H * W;
+    const int segs = (W + 255) / 256;
+    for (int q = 0; q < H * segs; ++q) {
+        const int ih = q / segs, iw = (q - ih * segs) * 256 + threadIdx.x;
+        if (iw >= W) continue;
+        const int p = ih * W + iw;
+        const int oh_lo = ih / 2, oh_hi = min(OH - 1, (ih + 1) / 2);
+        const int ow_lo = iw / 2, ow_hi = min(OW - 1, (iw + 1) / 2);
+        float g = 0.f;
         for (int oh = oh_lo; oh <= oh_hi; ++oh)
             for (int ow = ow_lo; ow <= ow_hi; ++ow) {
-                // window rows 2oh-1..2oh+1 / cols 2ow-1..2ow+1 must contain (ih, iw)
-                if (ih < 2 * oh - 1 || ih > 2 * oh + 1 || iw < 2 * ow - 1 || iw > 2 * ow + 1) continue;
-                float m = -INFINITY;
-                int arg = -1;
-                for (int kh = 0; kh < 3; ++kh) {
-                    const int hh = 2 * oh - 1 + kh;
-                    if (hh < 0 || hh >= H) continue;
-                    for (int kw = 0; kw < 3; ++kw) {
-                        const int ww = 2 * ow - 1 + kw;
-                        if (ww < 0 || ww >= W) continue;
-                        const float v = fmaxf(fmaf(yp[hh * W + ww], k.x, k.y), 0.f);
-                        if (v > m) { m = v; arg = hh * W + ww; }
-                    }
-                }
-                if (arg == p) g += dout[row * OH * OW + oh * OW + ow];
+                const int kh = ih - (2 * oh - 1), kw = iw - (2 * ow - 1);
+                if (ap[oh * OW + ow] == kh * 3 + kw) g += dp[oh * OW + ow];
             }
+        zp[p] = g;
     }
-    dz[e] = g;
 }
 
 __global__ void fill_cf_kernel(float4* cf, int C, float4 v) {
@@ -462,11 +503,24 @@ int convg_nslice(const ConvGArgs& a, int64_t* kslice) {
 int launch_convg(ConvGArgs a, hipStream_t s) {
     PCX_CHECK_ARG(a.stride == 1 || a.stride == 2, "convg: stride %d unsupported", a.stride);
     PCX_CHECK_ARG(a.B > 0 && a.cin > 0 && a.cout > 0, "convg: empty tensor");
+    if (a.mode == 1 && a.stride == 2 && !getenv("PCX_CONVG_NOPARITY")) {
+        for (int par = 0; par < 4; ++par) {  // each parity class of dx written exactly once
+            ConvGArgs c = a;
+            c.mode = 3;
+            c.par = par;
+            const int rc = launch_convg(c, s);
+            if (rc != PCX_OK) return rc;
+        }
+        return PCX_OK;
+    }
     const int64_t IHW = (int64_t)a.IH * a.IW, OHW = (int64_t)a.OH * a.OW;
     int64_t M, N;
     if (a.mode == 0) { M = a.cout; N = a.B * OHW; }
     else if (a.mode == 1) { M = a.cin; N = a.B * IHW; }
-    else { M = a.cout; N = (int64_t)a.cin * a.KH * a.KW; }
+    else if (a.mode == 3) {
+        M = a.cin;
+        N = a.B * (int64_t)((a.IH - (a.par >> 1) + 1) / 2) * ((a.IW - (a.par & 1) + 1) / 2);
+    } else { M = a.cout; N = (int64_t)a.cin * a.KH * a.KW; }
     const int wm = M >= 128 ? 2 : 1, wn = 2;
     const int64_t mt = ceil_div(M, 64 * wm), nt = ceil_div(N, 64 * wn);
     const int64_t nblocks = mt * nt * (a.mode == 2 ? a.nslice : 1);
@@ -485,6 +539,7 @@ int launch_convg(ConvGArgs a, hipStream_t s) {
     PCX_CG_K(1)
     PCX_CG_K(3)
     PCX_CG_K(7)
+    PCX_CG(3, 1, 1) PCX_CG(3, 1, 2) PCX_CG(3, 3, 1) PCX_CG(3, 3, 2)
 #undef PCX_CG_K
 #undef PCX_CG
     set_error("convg: kernel size %d unsupported", a.KH);
@@ -533,18 +588,20 @@ int launch_bn_bwd_apply(const float* g, const float* y, const float4* cf, float*
     return PCX_OK;
 }
 
-int launch_maxpool3_fwd(const float* y, const float4* cf, float* out, int B, int C, int H, int W, int OH, int OW,
-                        hipStream_t s) {
+int launch_maxpool3_fwd(const float* y, const float4* cf, float* out, uint8_t* arg, int B, int C, int H, int W,
+                        int OH, int OW, hipStream_t s) {
+    PCX_CHECK_ARG(OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1, "maxpool3: output %dx%d for input %dx%d", OH, OW,
+                  H, W);
     const int64_t rows = (int64_t)B * C;
-    maxpool3_fwd_kernel<<<ceil_div(rows * OH * OW, 256), 256, 0, s>>>(y, cf, out, rows, C, H, W, OH, OW);
+    maxpool3_fwd_kernel<<<(unsigned)rows, 256, 0, s>>>(y, cf, out, arg, C, H, W, OH, OW);
     PCX_LAUNCH_CHECK("maxpool3_fwd_kernel");
     return PCX_OK;
 }
 
-int launch_maxpool3_bwd(const float* y, const float4* cf, const float* dout, float* dz, int B, int C, int H, int W,
-                        int OH, int OW, hipStream_t s) {
+int launch_maxpool3_bwd(const uint8_t* arg, const float* dout, float* dz, int B, int C, int H, int W, int OH, int OW,
+                        hipStream_t s) {
     const int64_t rows = (int64_t)B * C;
-    maxpool3_bwd_kernel<<<ceil_div(rows * H * W, 256), 256, 0, s>>>(y, cf, dout, dz, rows, C, H, W, OH, OW);
+    maxpool3_bwd_kernel<<<(unsigned)rows, 256, 0, s>>>(arg, dout, dz, H, W, OH, OW);
     PCX_LAUNCH_CHECK("maxpool3_bwd_kernel");
     return PCX_OK;
 }

@@ -28,7 +28,7 @@ struct DeepPlan {
     bool residual;
     int h[4];
     int H0, W0, H1, W1;
-    size_t y0, a0, cf0, cfb0, dz0;
+    size_t y0, a0, cf0, cfb0, dz0, mparg;
     DeepBlock blk[4];
     size_t g, dyA, dyB, dd, hdz;   // backward scratch
     size_t stat, wgp, ident;
@@ -58,6 +58,7 @@ int build_deep(Plan& p) {
     d.y0 = p.carve("y0", planes(B, C0, d.H0, d.W0) * 4);
     d.dz0 = p.carve("dz0", planes(B, C0, d.H0, d.W0) * 4);
     d.a0 = p.carve("a0", planes(B, C0, d.H1, d.W1) * 4);
+    d.mparg = p.carve("maxpool_arg", planes(B, C0, d.H1, d.W1));  // first-max tap per window (uint8)
     d.cf0 = p.carve("cf0", C0 * 16);
     d.cfb0 = p.carve("cfb0", C0 * 16);
     int pidx = 4, bnidx = 1, cin = C0, H = d.H1, W = d.W1;
@@ -246,8 +247,8 @@ int deep_forward(const Plan& p, const float* const* P, float* const* bnstat, int
                    P[1], bnp(0, 0), bnp(0, 1), nb(0), train, c.w<float4>(d.cf0)));
     {
         Scope sc(&p.prof, s, "maxpool_fwd");
-        RC(launch_maxpool3_fwd(c.w<float>(d.y0), c.w<float4>(d.cf0), c.w<float>(d.a0), B, C0, d.H0, d.W0, d.H1,
-                               d.W1, s));
+        RC(launch_maxpool3_fwd(c.w<float>(d.y0), c.w<float4>(d.cf0), c.w<float>(d.a0), c.w<uint8_t>(d.mparg), B, C0,
+                               d.H0, d.W0, d.H1, d.W1, s));
     }
     const float* a = c.w<float>(d.a0);
     for (int i = 0; i < 4; ++i) {
@@ -481,7 +482,7 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
     float* dz0 = c.w<float>(d.dz0);
     {
         Scope sc(&p.prof, s, "maxpool_bwd");
-        RC(launch_maxpool3_bwd(c.w<float>(d.y0), c.w<float4>(d.cf0), dout, dz0, B, C0, d.H0, d.W0, d.H1, d.W1, s));
+        RC(launch_maxpool3_bwd(c.w<uint8_t>(d.mparg), dout, dz0, B, C0, d.H0, d.W0, d.H1, d.W1, s));
     }
     {
         BwdPrepArgs b{};

@@ -227,7 +227,8 @@ struct ConvGArgs {
     const float* w;       // modes 0, 1: [cout][cin][KH][KW] (reference layout)
     const float* dy;      // modes 1, 2: [B][cout][OH][OW]
     float* out;           // 0: y [B][cout][OH][OW]; 1: dx [B][cin][IH][IW]; 2: [nslice][cout][cin*KH*KW]
-    int accumulate;       // mode 1: dx += result
+    int accumulate;       // modes 1, 3: dx += result
+    int par;              // mode 3 (internal): parity class (ih % 2) * 2 + (iw % 2)
     int64_t kslice;       // mode 2: pixels per slice (multiple of 16)
     int nslice;
 };
@@ -262,10 +263,10 @@ int launch_bn_act(const float* y, const float4* cf, const float* res, const floa
                   float* out, int B, int C, int64_t P, hipStream_t s);
 int launch_bn_bwd_apply(const float* g, const float* y, const float4* cf, float* dy, int B, int C, int64_t P,
                         hipStream_t s);
-int launch_maxpool3_fwd(const float* y, const float4* cf, float* out, int B, int C, int H, int W, int OH, int OW,
-                        hipStream_t s);
-int launch_maxpool3_bwd(const float* y, const float4* cf, const float* dout, float* dz, int B, int C, int H, int W,
+int launch_maxpool3_fwd(const float* y, const float4* cf, float* out, uint8_t* arg, int B, int C, int H, int W,
                         int OH, int OW, hipStream_t s);
+int launch_maxpool3_bwd(const uint8_t* arg, const float* dout, float* dz, int B, int C, int H, int W, int OH, int OW,
+                        hipStream_t s);
 int launch_fill_cf(float4* cf, int C, float4 v, hipStream_t s);
 
 }  // namespace pcx
