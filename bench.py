@@ -183,6 +183,7 @@ def main():
     rank, world, local = ddp.init_from_env()
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}")
+    local = local % max(1, torch.cuda.device_count())  # == LOCAL_RANK on a full node
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     B, F, T, D = args.batch, 40, args.T, 128

@@ -26,8 +26,8 @@ def init_from_env(backend=None):
     lr = int(os.environ.get("LOCAL_RANK", "0"))
     if ws <= 1:
         return 0, 1, lr
-    if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend is None:  # PCX_DIST_BACKEND=gloo rehearses N ranks on one GPU (tests only)
+        backend = os.environ.get("PCX_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     if backend == "nccl":
         torch.cuda.set_device(lr)
     if not dist.is_initialized():
