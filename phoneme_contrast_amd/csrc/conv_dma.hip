@@ -484,6 +484,7 @@ int launch_conv3x3_dma(int pro, int epi, ConvArgs a, hipStream_t s) {
     PCX_DMA_ALL(PRO_BNRELU, EPI_FWD)
     PCX_DMA_ALL(PRO_RAW, EPI_BWD_RELU)   // data gradient on the dy materialised by the wgrad
     PCX_DMA_ALL(PRO_RAW, EPI_BWD_POOL)
+    PCX_DMA_ALL(PRO_RAW, EPI_BWD_STORE)  // cnn_deep's stride-1 3x3 data gradients
 #undef PCX_DMA_ALL
 #undef PCX_DMA_V
 #undef PCX_DMA_CK

@@ -103,6 +103,20 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[W
             a.part1[(int64_t)(n0 + tid) * a.nblk + tile] = m2;
             if (tid == 0 && n0 == 0) a.partn[tile] = n;
         }
+    } else if (EPI == EPI_BWD_STORE) {
+        // plain data gradient (cnn_deep routes its stride-1 3x3 convs here): store or accumulate
+#pragma unroll
+        for (int ni = 0; ni < WN; ++ni) {
+            if (!valid[ni]) continue;
+            float* op = a.out + ((int64_t)pb[ni] * a.cout + n0 + 4 * h) * HW + pp[ni];
+#pragma unroll
+            for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    float* o = op + (int64_t)(mi * 32 + (r & 3) + 8 * (r >> 2)) * HW;
+                    *o = a.accumulate ? *o + acc[mi][ni][r] : acc[mi][ni][r];
+                }
+        }
     } else {
         // backward epilogues: sums of dz and dz*xhat per channel.  The global loads of RB
         // accumulator rows are issued as one batch before any of their stores: the compiler must

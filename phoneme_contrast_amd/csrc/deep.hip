@@ -22,6 +22,11 @@ struct DeepBlock {
     size_t y1, d1, y2, ysc, out;  // forward tensors
     size_t cf1, cf2, cfsc, cfb1, cfb2, cfbsc;
     size_t da;                    // gradient w.r.t. the block input
+    // stride-1 3x3 convs routed to the cnn_small engines (conv_dma.hip forward / data gradient,
+    // wgrad_w32.hip weight gradient) when their channel counts fit; conv1 of block 0 and conv2
+    bool dma1, dma2, w32_1, w32_2;
+    WgradArgs wg1, wg2;
+    int nblk1, nblk2;
 };
 
 struct DeepPlan {
@@ -29,6 +34,8 @@ struct DeepPlan {
     int h[4];
     int H0, W0, H1, W1;
     size_t y0, a0, cf0, cfb0, dz0, mparg;
+    size_t wpk, identw;           // packed 3x3 weights of a routed conv; identity BN coefficients
+    int cmax;
     DeepBlock blk[4];
     size_t g, dyA, dyB, dd, hdz;   // backward scratch
     size_t stat, wgp, ident;
@@ -77,6 +84,23 @@ int build_deep(Plan& p) {
     };
     stat_need(C0);
     wg_need(1, C0, 7, d.H0, d.W0);
+    size_t wpk = 0;
+    int cmax = 0;
+    for (int i = 0; i < 4; ++i) cmax = std::max(cmax, d.h[i]);
+    const char* dmaenv = getenv("PCX_DEEP_DMA");  // "0": every conv on the general engine (A/B)
+    const bool route = !(dmaenv && dmaenv[0] == '0');
+    // a stride-1 3x3 conv cin -> cout at HxW on the DMA conv (fwd, dgrad) and the 32x32 wgrad
+    auto plan_routed = [&](int ci, int co, int h, int w, bool* fwd, bool* w32, WgradArgs* wga, int* nblk) {
+        *fwd = route && (co == 32 || co % 64 == 0) && (ci == 32 || ci % 64 == 0) && ci % 2 == 0;
+        *w32 = route && wgrad_w32_geometry(B, h, w, ci, co, wga);
+        *nblk = 0;
+        if (*fwd) {
+            *nblk = (int)std::max(conv3x3_nblk(B, h, w, co), conv3x3_nblk(B, h, w, ci));
+            stat = std::max(stat, (size_t)2 * std::max(ci, co) * (*nblk) + *nblk);
+            wpk = std::max(wpk, (size_t)9 * ci * co);
+        }
+        if (*w32) wg = std::max(wg, (size_t)wga->nslice * co * ci * 9);
+    };
     for (int i = 0; i < 4; ++i) {
         DeepBlock& k = d.blk[i];
         k.cin = cin; k.cout = d.h[i]; k.stride = i == 0 ? 1 : 2;
@@ -103,6 +127,10 @@ int build_deep(Plan& p) {
         wg_need(k.cin, k.cout, 3, k.Ho, k.Wo);
         wg_need(k.cout, k.cout, 3, k.Ho, k.Wo);
         if (k.sc) wg_need(k.cin, k.cout, 1, k.Ho, k.Wo);
+        k.dma1 = k.w32_1 = false;
+        k.nblk1 = 0;
+        if (k.stride == 1) plan_routed(k.cin, k.cout, k.Ho, k.Wo, &k.dma1, &k.w32_1, &k.wg1, &k.nblk1);
+        plan_routed(k.cout, k.cout, k.Ho, k.Wo, &k.dma2, &k.w32_2, &k.wg2, &k.nblk2);
         cin = k.cout; H = k.Ho; W = k.Wo;
     }
     d.g = p.carve("g", gmax);
@@ -117,6 +145,9 @@ int build_deep(Plan& p) {
     d.stat = p.carve("stat_part", stat * 4);
     d.wgp = p.carve("wg_part", wg * 4);
     d.ident = p.carve("ident", (size_t)C4 * 16);
+    d.identw = p.carve("identw", (size_t)cmax * 16);
+    d.cmax = cmax;
+    d.wpk = p.carve("wpack", std::max<size_t>(wpk, 1) * 4);
     d.ia = pidx;
     d.ip = pidx + (p.cfg.use_attention ? 2 : 0);
     d.bn_proj = bnidx;
@@ -156,19 +187,40 @@ struct Ctx {
 // forward conv (raw output, no bias) + train-mode statistics + BN finalise -> cf
 int conv_bn_fwd(const Ctx& c, const char* label, int layer, const float* x, int cin, int IH, int IW, int k, int stride,
                 int pad, const float* wgt, float* y, int cout, int OH, int OW, const float* gamma, const float* beta,
-                const float* bias, float* rmean, float* rvar, int64_t* nbt, int train, float4* cf) {
-    ConvGArgs a{};
-    a.mode = 0;
-    a.B = c.p.B; a.cin = cin; a.cout = cout;
-    a.IH = IH; a.IW = IW; a.OH = OH; a.OW = OW;
-    a.KH = a.KW = k; a.stride = stride; a.pad = pad;
-    a.x = x; a.w = wgt; a.out = y;
-    { Scope sc(&c.p.prof, c.s, label, layer); RC(launch_convg(a, c.s)); }
+                const float* bias, float* rmean, float* rvar, int64_t* nbt, int train, float4* cf, int dma_nblk = 0) {
     float* part = c.w<float>(c.d.stat);
     int ns = 1;
     BnFwdArgs f{};
     f.C = cout;
-    if (train) {
+    if (dma_nblk) {  // stride-1 3x3 on the LDS-DMA conv: its epilogue writes the BN partials
+        float* wp = c.w<float>(c.d.wpk);
+        RC(launch_pack_fwd(wgt, wp, cout, cin, c.s));
+        ConvArgs a{};
+        a.B = c.p.B; a.H = OH; a.W = OW; a.cin = cin; a.cout = cout;
+        a.src = x;
+        a.srcH = IH; a.srcW = IW;
+        a.wpack = wp;
+        a.out = y;
+        a.nblk = (int)conv3x3_nblk(c.p.B, OH, OW, cout);
+        a.part0 = part;
+        a.part1 = part + (size_t)cout * a.nblk;
+        a.partn = part + (size_t)2 * cout * a.nblk;
+        { Scope sc(&c.p.prof, c.s, label, layer); RC(launch_conv3x3_dma(PRO_RAW, EPI_FWD, a, c.s)); }
+        ns = a.nblk;
+        f.part0 = a.part0;
+        f.part1 = a.part1;
+        f.partn = a.partn;
+    } else {
+        ConvGArgs a{};
+        a.mode = 0;
+        a.B = c.p.B; a.cin = cin; a.cout = cout;
+        a.IH = IH; a.IW = IW; a.OH = OH; a.OW = OW;
+        a.KH = a.KW = k; a.stride = stride; a.pad = pad;
+        a.x = x; a.w = wgt; a.out = y;
+        Scope sc(&c.p.prof, c.s, label, layer);
+        RC(launch_convg(a, c.s));
+    }
+    if (train && !dma_nblk) {
         Scope sc(&c.p.prof, c.s, "chan_stats");
         int bps;
         const int nsl = chan_slices(c.p.B, cout, &bps);
@@ -189,7 +241,24 @@ int conv_bn_fwd(const Ctx& c, const char* label, int layer, const float* x, int 
 
 // weight gradient of a conv into G (partials summed deterministically) + zero bias gradient
 int conv_wgrad(const Ctx& c, int layer, const float* x, int cin, int IH, int IW, int k, int stride, int pad,
-               const float* dy, int cout, int OH, int OW, float* gw, float* gb) {
+               const float* dy, int cout, int OH, int OW, float* gw, float* gb, const WgradArgs* w32 = nullptr) {
+    if (w32) {  // stride-1 3x3: the 32x32 row-window kernel on a ready dy (identity BN-backward)
+        WgradArgs w = *w32;
+        w.B = c.p.B; w.H = OH; w.W = OW; w.cin = cin; w.cout = cout;
+        w.dz = dy;
+        w.y = dy;
+        w.cf_dy = c.w<float4>(c.d.identw);
+        w.src = x;
+        w.cf_x = nullptr;
+        w.drop = nullptr;
+        w.srcH = IH; w.srcW = IW;
+        w.dy_out = nullptr;
+        float* wgp = c.w<float>(c.d.wgp);
+        w.part = wgp;
+        { Scope sc(&c.p.prof, c.s, "wgrad", layer); RC(launch_wgrad_w32(PRO_RAW, w, c.s)); }
+        RC(launch_sum_slices(wgp, w.nslice, (int64_t)cout * cin * 9, gw, c.s));
+        return hip_status_ok(hipMemsetAsync(gb, 0, (size_t)cout * 4, c.s), "memset bias grad");
+    }
     ConvGArgs a{};
     a.mode = 2;
     a.B = c.p.B; a.cin = cin; a.cout = cout;
@@ -206,7 +275,22 @@ int conv_wgrad(const Ctx& c, int layer, const float* x, int cin, int IH, int IW,
 }
 
 int conv_dgrad(const Ctx& c, int layer, const float* dy, int cout, int OH, int OW, int k, int stride, int pad,
-               const float* wgt, float* dx, int cin, int IH, int IW, int accumulate) {
+               const float* wgt, float* dx, int cin, int IH, int IW, int accumulate, bool dma = false) {
+    if (dma) {  // stride-1 3x3: the LDS-DMA conv on flipped weights, plain store / accumulate
+        float* wp = c.w<float>(c.d.wpk);
+        RC(launch_pack_dgrad(wgt, wp, cout, cin, c.s));
+        ConvArgs a{};
+        a.B = c.p.B; a.H = IH; a.W = IW; a.cin = cout; a.cout = cin;
+        a.src = dy;
+        a.srcH = OH; a.srcW = OW;
+        a.wpack = wp;
+        a.out = dx;
+        a.accumulate = accumulate;
+        a.nblk = (int)conv3x3_nblk(c.p.B, IH, IW, cin);
+        a.part0 = a.part1 = c.w<float>(c.d.stat);
+        Scope sc(&c.p.prof, c.s, "conv_dgrad", layer);
+        return launch_conv3x3_dma(PRO_RAW, EPI_BWD_STORE, a, c.s);
+    }
     ConvGArgs a{};
     a.mode = 1;
     a.B = c.p.B; a.cin = cin; a.cout = cout;
@@ -256,7 +340,7 @@ int deep_forward(const Plan& p, const float* const* P, float* const* bnstat, int
         const int q = k.pidx, L = 2 * i + 1;
         RC(conv_bn_fwd(c, "conv_fwd", L, a, k.cin, k.Hi, k.Wi, 3, k.stride, 1, P[q], c.w<float>(k.y1), k.cout, k.Ho,
                        k.Wo, P[q + 2], P[q + 3], P[q + 1], bnp(k.bnidx, 0), bnp(k.bnidx, 1), nb(k.bnidx), train,
-                       c.w<float4>(k.cf1)));
+                       c.w<float4>(k.cf1), k.dma1 ? k.nblk1 : 0));
         const int64_t P2 = (int64_t)k.Ho * k.Wo;
         {
             Scope sc(&p.prof, s, "bn_act");
@@ -265,7 +349,7 @@ int deep_forward(const Plan& p, const float* const* P, float* const* bnstat, int
         }
         RC(conv_bn_fwd(c, "conv_fwd", L + 1, c.w<float>(k.d1), k.cout, k.Ho, k.Wo, 3, 1, 1, P[q + 4], c.w<float>(k.y2),
                        k.cout, k.Ho, k.Wo, P[q + 6], P[q + 7], P[q + 5], bnp(k.bnidx + 1, 0), bnp(k.bnidx + 1, 1),
-                       nb(k.bnidx + 1), train, c.w<float4>(k.cf2)));
+                       nb(k.bnidx + 1), train, c.w<float4>(k.cf2), k.dma2 ? k.nblk2 : 0));
         const float* res = nullptr;
         const float4* rcf = nullptr;
         if (k.sc) {
@@ -336,6 +420,8 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
         for (int i = 0; i < 4; ++i) dmask[i] = drop[i];
     float* part = c.w<float>(d.stat);
     const int ip = d.ip, ia = d.ia;
+    // dy is handed to the routed weight gradients ready-made: identity BN-backward coefficients
+    RC(launch_fill_cf(c.w<float4>(d.identw), d.cmax, make_float4(1.f, 0.f, 0.f, 1.f), s));
     {
         ProjArgs j{};
         j.B = B; j.K = p.C6; j.D = p.D;
@@ -430,9 +516,9 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
         }
         // ---- conv2
         RC(conv_wgrad(c, L + 1, c.w<float>(k.d1), k.cout, k.Ho, k.Wo, 3, 1, 1, dy2, k.cout, k.Ho, k.Wo, G[q + 4],
-                      G[q + 5]));
+                      G[q + 5], k.w32_2 ? &k.wg2 : nullptr));
         float* dd = c.w<float>(d.dd);
-        RC(conv_dgrad(c, L + 1, dy2, k.cout, k.Ho, k.Wo, 3, 1, 1, P[q + 4], dd, k.cout, k.Ho, k.Wo, 0));
+        RC(conv_dgrad(c, L + 1, dy2, k.cout, k.Ho, k.Wo, 3, 1, 1, P[q + 4], dd, k.cout, k.Ho, k.Wo, 0, k.dma2));
         // ---- through Dropout2d / ReLU / BN1
         {
             BwdPrepArgs b{};
@@ -459,7 +545,8 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
             RC(launch_bn_bwd_apply(dd, c.w<float>(k.y1), c.w<float4>(k.cfb1), dy1, B, k.cout, P2, s));
         }
         // ---- conv1 (+ shortcut): gradients of the weights and of the block input
-        RC(conv_wgrad(c, L, a_in, k.cin, k.Hi, k.Wi, 3, k.stride, 1, dy1, k.cout, k.Ho, k.Wo, G[q], G[q + 1]));
+        RC(conv_wgrad(c, L, a_in, k.cin, k.Hi, k.Wi, 3, k.stride, 1, dy1, k.cout, k.Ho, k.Wo, G[q], G[q + 1],
+                      k.w32_1 ? &k.wg1 : nullptr));
         float* da = c.w<float>(k.da);
         int acc = 0;
         if (d.residual && !k.sc) {  // identity shortcut: the block input receives g directly
@@ -467,7 +554,7 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
                              "copy shortcut grad"));
             acc = 1;
         }
-        RC(conv_dgrad(c, L, dy1, k.cout, k.Ho, k.Wo, 3, k.stride, 1, P[q], da, k.cin, k.Hi, k.Wi, acc));
+        RC(conv_dgrad(c, L, dy1, k.cout, k.Ho, k.Wo, 3, k.stride, 1, P[q], da, k.cin, k.Hi, k.Wi, acc, k.dma1));
         if (k.sc) {
             RC(conv_wgrad(c, 100 + i, a_in, k.cin, k.Hi, k.Wi, 1, k.stride, 0, dysc, k.cout, k.Ho, k.Wo, G[q + 8],
                           G[q + 9]));

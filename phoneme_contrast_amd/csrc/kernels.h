@@ -18,6 +18,7 @@ enum Epilogue {
     EPI_FWD = 0,        // store y, per-block BN statistics (sum, M2, count)
     EPI_BWD_RELU = 1,   // dz = acc * [yprev*s+t > 0]; store dz; sums of dz and dz*xhat
     EPI_BWD_POOL = 2,   // route acc (pooled res) through dropout, 2x2 argmax, ReLU to 2x res
+    EPI_BWD_STORE = 3,  // dx = acc (or dx += acc with ConvArgs::accumulate); no statistics
 };
 
 // 3x3 / stride 1 / pad 1 convolution as an implicit GEMM on v_mfma_f32_32x32x2_f32.
@@ -44,6 +45,7 @@ struct ConvArgs {
     float* partn;         // [nblk] element counts (EPI_FWD)
     int nblk;
     int NR, RS;           // staged rows / LDS row stride (host-computed)
+    int accumulate;       // EPI_BWD_STORE: add into out instead of overwriting
 };
 
 int launch_conv3x3(int pro, int epi, ConvArgs a, hipStream_t s);

@@ -97,17 +97,22 @@ def _torch_reference(m, x, masks):
     return F.normalize(x, p=2, dim=1)
 
 
-@pytest.mark.parametrize("residual,T", [(False, 200), (False, 201), (True, 57)])
-def test_deep_matches_float64_torch(residual, T):
+FULL = [64, 128, 256, 512]  # the benchmarked widths: stride-1 3x3 convs on the LDS-DMA / 32x32 engines
+
+
+@pytest.mark.parametrize("residual,T,dims,B", [(False, 200, None, 8), (False, 201, None, 8), (True, 57, None, 8),
+                                               (True, 200, FULL, 4), (True, 57, FULL, 5)])
+def test_deep_matches_float64_torch(residual, T, dims, B):
     from phoneme_contrast_amd.losses import SupervisedContrastiveLoss
     torch.manual_seed(3)
     cfg = dict(DEEP, use_residual=residual)
+    if dims:
+        cfg["hidden_dims"] = dims
     from phoneme_contrast_amd.models import PhonemeNetDeep
     m = PhonemeNetDeep(cfg)
     ref = PhonemeNetDeep(cfg).double()
     ref.load_state_dict(m.state_dict())
     m = m.cuda().train()
-    B = 8
     x = torch.randn(B, 1, 40, T)
     labels = torch.arange(B) % 4
     masks = [(torch.rand(B, c) > 0.2).float() / 0.8 for c in cfg["hidden_dims"]]
@@ -121,7 +126,13 @@ def test_deep_matches_float64_torch(residual, T):
     from oracle import torch_port as tp
     lr_ = tp.supcon(er, labels, 0.15, 0.07)
     lr_.backward()
-    assert (e.detach().cpu().double() - er.detach()).abs().max() < 1e-5
+    emb_err = (e.detach().cpu().double() - er.detach()).abs().max().item()
+    print(f"deep residual={residual} T={T} dims={dims} B={B}: max |d emb| {emb_err:.2e}, "
+          f"|d loss| {abs(loss.item() - lr_.item()):.2e}")
+    # full widths (512 channels through 4 train-mode BN layers over B = 4 samples) condition the
+    # fp32 forward worse: the general implicit-GEMM engine alone measures 1.26e-5 on (200, FULL, 4),
+    # the routed engines 1.41e-5 -- float32 rounding, not a layout error, so the bound is 5e-5 there
+    assert emb_err < (5e-5 if dims == FULL else 1e-5)
     assert abs(loss.item() - lr_.item()) < 1e-4
     for (k, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
         g, r = p.grad.cpu().double(), q.grad
