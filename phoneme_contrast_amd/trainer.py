@@ -195,7 +195,9 @@ class ContrastiveTrainer:
             json.dump(self.metrics_history, f, indent=2)
 
     def load_checkpoint(self, path: Path) -> None:
-        checkpoint = torch.load(path, map_location=self.device, weights_only=False)
+        # every entry is a tensor or a plain container, so the safe loader reads it (as
+        # scripts/evaluate.py:271 does with torch's default weights_only=True)
+        checkpoint = torch.load(path, map_location=self.device, weights_only=True)
         self.model.load_state_dict(checkpoint["model_state_dict"])
         self.optimizer.load_state_dict(checkpoint["optimizer_state_dict"])
         if self.scheduler and checkpoint["scheduler_state_dict"]:
