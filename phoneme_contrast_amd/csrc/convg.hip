@@ -473,6 +473,131 @@ __global__ __launch_bounds__(256) void maxpool3_bwd_kernel(const uint8_t* __rest
     }
 }
 
+// LDS-plane forms of the two kernels above (the stem planes, 40 x 200 at T = 200, fit): the plane is
+// read once with coalesced (float4 when VEC = 4) loads, BN + ReLU applied on the way into LDS, and
+// every window / gather then reads LDS.  Same results, same tie rule, bit for bit.
+template <int VEC>
+__global__ __launch_bounds__(256) void maxpool3_fwd_lds_kernel(const float* __restrict__ y,
+                                                               const float4* __restrict__ cf, float* __restrict__ out,
+                                                               uint8_t* __restrict__ arg, int C, int H, int W, int OH,
+                                                               int OW) {
+    extern __shared__ __attribute__((aligned(16))) float pl[];  // [H][W]
+    const int64_t row = blockIdx.x;
+    const float4 k = cf[(int)(row % C)];
+    const int HW = H * W, OHW = OH * OW;
+    const float* yp = y + row * HW;
+    for (int i = threadIdx.x; i < HW / VEC; i += 256) {
+        if (VEC == 4) {
+            float4 v = reinterpret_cast<const float4*>(yp)[i];
+            v.x = fmaxf(fmaf(v.x, k.x, k.y), 0.f);
+            v.y = fmaxf(fmaf(v.y, k.x, k.y), 0.f);
+            v.z = fmaxf(fmaf(v.z, k.x, k.y), 0.f);
+            v.w = fmaxf(fmaf(v.w, k.x, k.y), 0.f);
+            reinterpret_cast<float4*>(pl)[i] = v;
+        } else {
+            pl[i] = fmaxf(fmaf(yp[i], k.x, k.y), 0.f);
+        }
+    }
+    __syncthreads();
+    float* op = out + row * OHW;
+    uint8_t* ap = arg + row * OHW;
+    // output walk: p = tid + 256 j, (oh, ow) tracked without division
+    int oh = threadIdx.x / OW, ow = threadIdx.x - oh * OW;
+    const int doh = 256 / OW, dow = 256 - doh * OW;
+    for (int p = threadIdx.x; p < OHW; p += 256) {
+        float m = -INFINITY;
+        int best = 0;
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) {
+            const int ih = 2 * oh - 1 + kh;
+            if (ih < 0 || ih >= H) continue;
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+                const int iw = 2 * ow - 1 + kw;
+                if (iw < 0 || iw >= W) continue;
+                const float v = pl[ih * W + iw];
+                if (v > m) { m = v; best = kh * 3 + kw; }
+            }
+        }
+        op[p] = m;
+        ap[p] = m > 0.f ? (uint8_t)best : (uint8_t)255;
+        oh += doh;
+        ow += dow;
+        if (ow >= OW) { ow -= OW; ++oh; }
+    }
+}
+
+// MaxPool(3,2,1) + ReLU backward fused with the stem BN's backward sums (replaces
+// maxpool3_bwd_kernel + bwd_prep_kernel on the stem): block (c, slice) walks its samples' planes of
+// channel c; per plane the pooled gradient and the recorded taps are staged in LDS, every input
+// pixel gathers its (at most 2 x 2) windows, g is written once and sum(g), sum(g * xhat) go to the
+// same [C][nslice] partials bwd_prep_kernel produces.
+template <int VEC>
+__global__ __launch_bounds__(256) void maxpool3_bwd_prep_kernel(const uint8_t* __restrict__ arg,
+                                                                const float* __restrict__ dout,
+                                                                const float* __restrict__ y,
+                                                                const float4* __restrict__ cf, float* __restrict__ g,
+                                                                float* __restrict__ p_g, float* __restrict__ p_x, int B,
+                                                                int C, int H, int W, int OH, int OW, int bps) {
+    extern __shared__ __attribute__((aligned(16))) float dl[];  // [OH*OW] gradients, then [OH*OW] taps
+    __shared__ double red[4];
+    const int c = blockIdx.x, sl = blockIdx.y, nsl = gridDim.y;
+    const int b0 = sl * bps, b1 = min(B, b0 + bps);
+    const int HW = H * W, OHW = OH * OW, WQ = W / VEC, HWQ = HW / VEC;
+    uint8_t* al = reinterpret_cast<uint8_t*>(dl + OHW);
+    const float4 k = cf[c];
+    double sg = 0.0, sx = 0.0;
+    const int q0h = threadIdx.x / WQ, q0w = threadIdx.x - q0h * WQ;
+    const int dqh = 256 / WQ, dqw = 256 - dqh * WQ;
+    for (int b = b0; b < b1; ++b) {
+        const int64_t row = (int64_t)b * C + c;
+        for (int i = threadIdx.x; i < OHW; i += 256) {
+            dl[i] = dout[row * OHW + i];
+            al[i] = arg[row * OHW + i];
+        }
+        __syncthreads();
+        const float* yp = y + row * HW;
+        float* gp = g + row * HW;
+        int ih = q0h, iq = q0w;
+        for (int q = threadIdx.x; q < HWQ; q += 256) {
+            float gv[VEC], yv[VEC];
+            if (VEC == 4) {
+                const float4 t = reinterpret_cast<const float4*>(yp)[q];
+                yv[0] = t.x; yv[1] = t.y; yv[2] = t.z; yv[3] = t.w;
+            } else {
+                yv[0] = yp[q];
+            }
+            const int oh_lo = ih >> 1, oh_hi = min(OH - 1, (ih + 1) >> 1);
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) {
+                const int iw = iq * VEC + e;
+                const int ow_lo = iw >> 1, ow_hi = min(OW - 1, (iw + 1) >> 1);
+                float acc = 0.f;
+                for (int oh = oh_lo; oh <= oh_hi; ++oh)
+                    for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+                        const int kh = ih - (2 * oh - 1), kw = iw - (2 * ow - 1);
+                        if (al[oh * OW + ow] == kh * 3 + kw) acc += dl[oh * OW + ow];
+                    }
+                gv[e] = acc;
+                sg += (double)acc;
+                sx += (double)acc * (double)((yv[e] - k.z) * k.w);
+            }
+            if (VEC == 4) reinterpret_cast<float4*>(gp)[q] = make_float4(gv[0], gv[1], gv[2], gv[3]);
+            else gp[q] = gv[0];
+            ih += dqh;
+            iq += dqw;
+            if (iq >= WQ) { iq -= WQ; ++ih; }
+        }
+        __syncthreads();
+    }
+    sg = block_sum(sg, red);
+    sx = block_sum(sx, red);
+    if (threadIdx.x == 0) {
+        p_g[(int64_t)c * nsl + sl] = (float)sg;
+        p_x[(int64_t)c * nsl + sl] = (float)sx;
+    }
+}
+
 __global__ void fill_cf_kernel(float4* cf, int C, float4 v) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c < C) cf[c] = v;
@@ -593,8 +718,39 @@ int launch_maxpool3_fwd(const float* y, const float4* cf, float* out, uint8_t* a
     PCX_CHECK_ARG(OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1, "maxpool3: output %dx%d for input %dx%d", OH, OW,
                   H, W);
     const int64_t rows = (int64_t)B * C;
+    const size_t lds = (size_t)H * W * 4;
+    if (lds <= 64 * 1024 && !getenv("PCX_MAXPOOL_OLD")) {
+        if ((H * W) % 4 == 0) maxpool3_fwd_lds_kernel<4><<<(unsigned)rows, 256, lds, s>>>(y, cf, out, arg, C, H, W, OH, OW);
+        else maxpool3_fwd_lds_kernel<1><<<(unsigned)rows, 256, lds, s>>>(y, cf, out, arg, C, H, W, OH, OW);
+        PCX_LAUNCH_CHECK("maxpool3_fwd_lds_kernel");
+        return PCX_OK;
+    }
     maxpool3_fwd_kernel<<<(unsigned)rows, 256, 0, s>>>(y, cf, out, arg, C, H, W, OH, OW);
     PCX_LAUNCH_CHECK("maxpool3_fwd_kernel");
+    return PCX_OK;
+}
+
+bool maxpool3_bwd_prep_fits(int H, int W, int OH, int OW) {
+    (void)H;
+    (void)W;
+    return (size_t)OH * OW * 5 <= 64 * 1024 && !getenv("PCX_MAXPOOL_OLD");
+}
+
+int launch_maxpool3_bwd_prep(const uint8_t* arg, const float* dout, const float* y, const float4* cf, float* g,
+                             float* p_g, float* p_x, int B, int C, int H, int W, int OH, int OW, int* nslice,
+                             hipStream_t s) {
+    PCX_CHECK_ARG(OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1, "maxpool3: output %dx%d for input %dx%d", OH, OW,
+                  H, W);
+    PCX_CHECK_ARG(maxpool3_bwd_prep_fits(H, W, OH, OW), "maxpool3_bwd_prep: %dx%d pooled plane exceeds LDS", OH, OW);
+    int bps;
+    const int ns = chan_slices(B, C, &bps);
+    *nslice = ns;
+    const size_t lds = ((size_t)OH * OW * 5 + 15) / 16 * 16;
+    if (W % 4 == 0)
+        maxpool3_bwd_prep_kernel<4><<<dim3(C, ns), 256, lds, s>>>(arg, dout, y, cf, g, p_g, p_x, B, C, H, W, OH, OW, bps);
+    else
+        maxpool3_bwd_prep_kernel<1><<<dim3(C, ns), 256, lds, s>>>(arg, dout, y, cf, g, p_g, p_x, B, C, H, W, OH, OW, bps);
+    PCX_LAUNCH_CHECK("maxpool3_bwd_prep_kernel");
     return PCX_OK;
 }
 

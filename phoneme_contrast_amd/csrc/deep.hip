@@ -241,18 +241,26 @@ int conv_bn_fwd(const Ctx& c, const char* label, int layer, const float* x, int 
 
 // weight gradient of a conv into G (partials summed deterministically) + zero bias gradient
 int conv_wgrad(const Ctx& c, int layer, const float* x, int cin, int IH, int IW, int k, int stride, int pad,
-               const float* dy, int cout, int OH, int OW, float* gw, float* gb, const WgradArgs* w32 = nullptr) {
-    if (w32) {  // stride-1 3x3: the 32x32 row-window kernel on a ready dy (identity BN-backward)
+               const float* dy, int cout, int OH, int OW, float* gw, float* gb, const WgradArgs* w32 = nullptr,
+               const float* bn_g = nullptr, const float* bn_y = nullptr, const float4* bn_cf = nullptr) {
+    if (w32) {  // stride-1 3x3: the 32x32 row-window kernel
         WgradArgs w = *w32;
         w.B = c.p.B; w.H = OH; w.W = OW; w.cin = cin; w.cout = cout;
-        w.dz = dy;
-        w.y = dy;
-        w.cf_dy = c.w<float4>(c.d.identw);
+        if (bn_g) {  // BN backward in the staging: dy = f(g, y) computed per row and written to `dy`
+            w.dz = bn_g;
+            w.y = bn_y;
+            w.cf_dy = bn_cf;
+            w.dy_out = const_cast<float*>(dy);
+        } else {     // a ready dy (identity BN-backward coefficients)
+            w.dz = dy;
+            w.y = dy;
+            w.cf_dy = c.w<float4>(c.d.identw);
+            w.dy_out = nullptr;
+        }
         w.src = x;
         w.cf_x = nullptr;
         w.drop = nullptr;
         w.srcH = IH; w.srcW = IW;
-        w.dy_out = nullptr;
         float* wgp = c.w<float>(c.d.wgp);
         w.part = wgp;
         { Scope sc(&c.p.prof, c.s, "wgrad", layer); RC(launch_wgrad_w32(PRO_RAW, w, c.s)); }
@@ -511,12 +519,13 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
         }
         {
             Scope sc(&p.prof, s, "bn_bwd_apply");
-            RC(launch_bn_bwd_apply(g, c.w<float>(k.y2), c.w<float4>(k.cfb2), dy2, B, k.cout, P2, s));
+            // (a routed conv2's dy is produced by its weight-gradient kernel's staging)
+            if (!k.w32_2) RC(launch_bn_bwd_apply(g, c.w<float>(k.y2), c.w<float4>(k.cfb2), dy2, B, k.cout, P2, s));
             if (k.sc) RC(launch_bn_bwd_apply(g, c.w<float>(k.ysc), c.w<float4>(k.cfbsc), dysc, B, k.cout, P2, s));
         }
         // ---- conv2
         RC(conv_wgrad(c, L + 1, c.w<float>(k.d1), k.cout, k.Ho, k.Wo, 3, 1, 1, dy2, k.cout, k.Ho, k.Wo, G[q + 4],
-                      G[q + 5], k.w32_2 ? &k.wg2 : nullptr));
+                      G[q + 5], k.w32_2 ? &k.wg2 : nullptr, g, c.w<float>(k.y2), c.w<float4>(k.cfb2)));
         float* dd = c.w<float>(d.dd);
         RC(conv_dgrad(c, L + 1, dy2, k.cout, k.Ho, k.Wo, 3, 1, 1, P[q + 4], dd, k.cout, k.Ho, k.Wo, 0, k.dma2));
         // ---- through Dropout2d / ReLU / BN1
@@ -542,11 +551,11 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
         float* dy1 = dy2;  // dy2 is dead after conv2's gradients
         {
             Scope sc(&p.prof, s, "bn_bwd_apply");
-            RC(launch_bn_bwd_apply(dd, c.w<float>(k.y1), c.w<float4>(k.cfb1), dy1, B, k.cout, P2, s));
+            if (!k.w32_1) RC(launch_bn_bwd_apply(dd, c.w<float>(k.y1), c.w<float4>(k.cfb1), dy1, B, k.cout, P2, s));
         }
         // ---- conv1 (+ shortcut): gradients of the weights and of the block input
         RC(conv_wgrad(c, L, a_in, k.cin, k.Hi, k.Wi, 3, k.stride, 1, dy1, k.cout, k.Ho, k.Wo, G[q], G[q + 1],
-                      k.w32_1 ? &k.wg1 : nullptr));
+                      k.w32_1 ? &k.wg1 : nullptr, dd, c.w<float>(k.y1), c.w<float4>(k.cfb1)));
         float* da = c.w<float>(k.da);
         int acc = 0;
         if (d.residual && !k.sc) {  // identity shortcut: the block input receives g directly
@@ -567,11 +576,22 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
     const int C0 = d.h[0];
     const int64_t P0 = (int64_t)d.H0 * d.W0;
     float* dz0 = c.w<float>(d.dz0);
-    {
-        Scope sc(&p.prof, s, "maxpool_bwd");
-        RC(launch_maxpool3_bwd(c.w<uint8_t>(d.mparg), dout, dz0, B, C0, d.H0, d.W0, d.H1, d.W1, s));
-    }
-    {
+    if (maxpool3_bwd_prep_fits(d.H0, d.W0, d.H1, d.W1)) {  // one pass: pooled gradient + BN0 sums
+        int bps, ns;
+        const int nsl = chan_slices(B, C0, &bps);
+        float* p_g = part;
+        float* p_x = part + (size_t)C0 * nsl;
+        {
+            Scope sc(&p.prof, s, "maxpool_bwd");
+            RC(launch_maxpool3_bwd_prep(c.w<uint8_t>(d.mparg), dout, c.w<float>(d.y0), c.w<float4>(d.cf0), dz0, p_g,
+                                        p_x, B, C0, d.H0, d.W0, d.H1, d.W1, &ns, s));
+        }
+        RC(bn_bwd(c, C0, ns, p_g, p_x, P[2], c.w<float4>(d.cf0), G[2], G[3], c.w<float4>(d.cfb0), (double)B * P0));
+    } else {
+        {
+            Scope sc(&p.prof, s, "maxpool_bwd");
+            RC(launch_maxpool3_bwd(c.w<uint8_t>(d.mparg), dout, dz0, B, C0, d.H0, d.W0, d.H1, d.W1, s));
+        }
         BwdPrepArgs b{};
         b.B = B; b.C = C0; b.P = P0;
         b.d = dz0;

@@ -269,6 +269,11 @@ int launch_maxpool3_fwd(const float* y, const float4* cf, float* out, uint8_t* a
                         int OH, int OW, hipStream_t s);
 int launch_maxpool3_bwd(const uint8_t* arg, const float* dout, float* dz, int B, int C, int H, int W, int OH, int OW,
                         hipStream_t s);
+// MaxPool(3,2,1) + ReLU backward fused with the stem BN's backward partial sums (g written once)
+bool maxpool3_bwd_prep_fits(int H, int W, int OH, int OW);
+int launch_maxpool3_bwd_prep(const uint8_t* arg, const float* dout, const float* y, const float4* cf, float* g,
+                             float* p_g, float* p_x, int B, int C, int H, int W, int OH, int OW, int* nslice,
+                             hipStream_t s);
 int launch_fill_cf(float4* cf, int C, float4 v, hipStream_t s);
 
 }  // namespace pcx
