@@ -26,7 +26,11 @@ namespace {
 
 constexpr int KC = 16;
 
-template <int MODE, int KH, int KW, int WM, int WN>
+// K order (modes 0, 1, 3) is tap-major: k = tap * CK + channel, CK = cin (mode 0) or cout (modes 1,
+// 3).  With CK % 16 == 0 (FK) every K-chunk then shares one tap, so a thread's B gathers of a chunk
+// are one bounds check and NBv loads at a fixed channel stride -- no per-element index arithmetic.
+// Mode 2's N index is (tap, cin) likewise, its per-column decomposition hoisted out of the K loop.
+template <int MODE, int KH, int KW, int WM, int WN, bool FK>
 __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
     constexpr int KK = KH * KW;
     constexpr int BM = 64 * WM, BN = 64 * WN;
@@ -39,6 +43,7 @@ __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
     const int wave = tid >> 6, wr = wave >> 1, wc = wave & 1;
     const int64_t OHW = (int64_t)a.OH * a.OW, IHW = (int64_t)a.IH * a.IW;
     const int s = a.stride, pad = a.pad;
+    const int CK = MODE == 0 ? a.cin : a.cout;
 
     // parity class (mode 3): pixels (2 ihc + ph, 2 iwc + pw), taps kh0 + 2 i, kw0 + 2 j
     const int ph = a.par >> 1, pw = a.par & 1;
@@ -68,12 +73,12 @@ __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
     // ---- per-thread staging state
     const int kq = tid & 15;       // k-fast mapping: k offset within the chunk
     const int colq = tid >> 4;     // k-fast mapping: first column
-    // column-fast mapping (B of modes 0/1): fixed pixel per thread
+    // column-fast mapping (B of modes 0/1/3): fixed pixel per thread
     const int bcol = tid % BN;
     const int brow = tid / BN;     // first k row; rows advance by 256/BN
     constexpr int BROWS = 256 / BN;
-    int64_t xbase = 0;             // mode 0: x + b*cin*IHW ; mode 1: dy + b*cout*OHW
-    int ih0 = 0, iw0 = 0;          // mode 0: oh*s-p, ow*s-p ; mode 1: ih+p, iw+p
+    int64_t xbase = 0;             // mode 0: x + b*cin*IHW ; modes 1, 3: dy + b*cout*OHW
+    int ih0 = 0, iw0 = 0;          // mode 0: oh*s-p, ow*s-p ; modes 1, 3: ih+p, iw+p
     bool bvalid = false;
     if (MODE == 0 || MODE == 1 || MODE == 3) {
         const int64_t m = n0 + bcol;
@@ -99,88 +104,125 @@ __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
             iw0 = iw + pad;
         }
     }
-    // mode 2: pixel tracker of k = k_begin + chunk*KC + kq
+    // mode 2: pixel tracker of k = k_begin + chunk*KC + kq, and the fixed (tap, channel) of each
+    // staged B column
     int64_t pb = 0;
     int poh = 0, pow_ = 0;
+    int wkh[MODE == 2 ? NBv : 1], wkw[MODE == 2 ? NBv : 1];
+    int64_t wco[MODE == 2 ? NBv : 1];
     if (MODE == 2) {
         const int64_t q = k_begin + kq;
         pb = q / OHW;
         const int64_t p = q - pb * OHW;
         poh = (int)(p / a.OW);
         pow_ = (int)(p - (int64_t)poh * a.OW);
+#pragma unroll
+        for (int i = 0; i < NBv; ++i) {
+            const int64_t jj = n0 + colq + 16 * i;
+            const int tap = (int)(jj / a.cin), c = (int)(jj - (int64_t)tap * a.cin);
+            const bool jv = jj < N;
+            wkh[i] = jv ? tap / KW - pad : -(1 << 28);  // out of range: never loads
+            wkw[i] = tap % KW - pad;
+            wco[i] = (int64_t)c * IHW;
+        }
     }
 
     float ra[NA], rb[NBv];
     auto gather = [&](int chunk) {
         const int64_t kbase = k_begin + (int64_t)chunk * KC;
-        if (MODE == 0) {
+        if (MODE == 0 || MODE == 1 || MODE == 3) {
+            // A: weights, k = kbase + kq -> (tap, channel)
             const int64_t k = kbase + kq;
+            const int tap = (int)(k / CK), ch = (int)(k - (int64_t)tap * CK);
+            const bool kv = k < K;
 #pragma unroll
             for (int j = 0; j < NA; ++j) {
-                const int64_t n = m0 + colq + 16 * j;
-                ra[j] = (n < M && k < K) ? a.w[n * K + k] : 0.f;
-            }
-#pragma unroll
-            for (int i = 0; i < NBv; ++i) {
-                const int64_t kb = kbase + brow + BROWS * i;
+                const int64_t m = m0 + colq + 16 * j;
                 float v = 0.f;
-                if (bvalid && kb < K) {
-                    const int c = (int)(kb / KK), r = (int)(kb - (int64_t)(kb / KK) * KK);
-                    const int ih = ih0 + r / KW, iw = iw0 + r % KW;
-                    if (ih >= 0 && ih < a.IH && iw >= 0 && iw < a.IW)
-                        v = a.x[xbase + ((int64_t)c * a.IH + ih) * a.IW + iw];
+                if (kv && m < M) {
+                    if (MODE == 0) v = a.w[(m * a.cin + ch) * KK + tap];
+                    else if (MODE == 1) v = a.w[((int64_t)ch * a.cin + m) * KK + tap];
+                    else v = a.w[(((int64_t)ch * a.cin + m) * KH + kh0 + 2 * (tap / ntw)) * KW + kw0 + 2 * (tap % ntw)];
                 }
-                rb[i] = v;
+                ra[j] = v;
+            }
+        }
+        if (MODE == 0) {
+            if (FK) {  // one tap per chunk
+                const int tap = (int)(kbase / CK), c0 = (int)(kbase - (int64_t)tap * CK);
+                const int ih = ih0 + tap / KW, iw = iw0 + tap % KW;
+                const bool ok = bvalid && ih >= 0 && ih < a.IH && iw >= 0 && iw < a.IW;
+                const float* p = a.x + xbase + (int64_t)(c0 + brow) * IHW + (int64_t)ih * a.IW + iw;
+#pragma unroll
+                for (int i = 0; i < NBv; ++i) rb[i] = ok ? p[(int64_t)i * BROWS * IHW] : 0.f;
+            } else {
+#pragma unroll
+                for (int i = 0; i < NBv; ++i) {
+                    const int64_t kb = kbase + brow + BROWS * i;
+                    float v = 0.f;
+                    if (bvalid && kb < K) {
+                        const int tap = (int)(kb / CK), c = (int)(kb - (int64_t)tap * CK);
+                        const int ih = ih0 + tap / KW, iw = iw0 + tap % KW;
+                        if (ih >= 0 && ih < a.IH && iw >= 0 && iw < a.IW)
+                            v = a.x[xbase + ((int64_t)c * a.IH + ih) * a.IW + iw];
+                    }
+                    rb[i] = v;
+                }
             }
         } else if (MODE == 1) {
-            const int64_t k = kbase + kq;
-            const int n = (int)(k / KK), r = (int)(k - (int64_t)(k / KK) * KK);
-#pragma unroll
-            for (int j = 0; j < NA; ++j) {
-                const int64_t c = m0 + colq + 16 * j;
-                ra[j] = (c < M && k < K) ? a.w[((int64_t)n * a.cin + c) * KK + r] : 0.f;
-            }
-#pragma unroll
-            for (int i = 0; i < NBv; ++i) {
-                const int64_t kb = kbase + brow + BROWS * i;
-                float v = 0.f;
-                if (bvalid && kb < K) {
-                    const int nn = (int)(kb / KK), rr = (int)(kb - (int64_t)(kb / KK) * KK);
-                    const int th = ih0 - rr / KW, tw = iw0 - rr % KW;
-                    if (th >= 0 && tw >= 0) {
-                        int oh = th, ow = tw;
-                        bool ok = true;
-                        if (s == 2) {
-                            ok = ((th | tw) & 1) == 0;
-                            oh = th >> 1;
-                            ow = tw >> 1;
-                        }
-                        if (ok && oh < a.OH && ow < a.OW)
-                            v = a.dy[xbase + ((int64_t)nn * a.OH + oh) * a.OW + ow];
-                    }
+            auto src = [&](int tap, int& oh, int& ow) {
+                const int th = ih0 - tap / KW, tw = iw0 - tap % KW;
+                oh = th;
+                ow = tw;
+                bool ok = th >= 0 && tw >= 0;
+                if (s == 2) {
+                    ok = ok && ((th | tw) & 1) == 0;
+                    oh = th >> 1;
+                    ow = tw >> 1;
                 }
-                rb[i] = v;
+                return ok && oh < a.OH && ow < a.OW;
+            };
+            if (FK) {
+                const int tap = (int)(kbase / CK), c0 = (int)(kbase - (int64_t)tap * CK);
+                int oh, ow;
+                const bool ok = bvalid && src(tap, oh, ow);
+                const float* p = a.dy + xbase + (int64_t)(c0 + brow) * OHW + (int64_t)oh * a.OW + ow;
+#pragma unroll
+                for (int i = 0; i < NBv; ++i) rb[i] = ok ? p[(int64_t)i * BROWS * OHW] : 0.f;
+            } else {
+#pragma unroll
+                for (int i = 0; i < NBv; ++i) {
+                    const int64_t kb = kbase + brow + BROWS * i;
+                    float v = 0.f;
+                    if (bvalid && kb < K) {
+                        const int tap = (int)(kb / CK), nn = (int)(kb - (int64_t)tap * CK);
+                        int oh, ow;
+                        if (src(tap, oh, ow)) v = a.dy[xbase + ((int64_t)nn * a.OH + oh) * a.OW + ow];
+                    }
+                    rb[i] = v;
+                }
             }
         } else if (MODE == 3) {
-            const int64_t k = kbase + kq;
-            const int n = KKp ? (int)(k / KKp) : 0, r = (int)(k - (int64_t)n * KKp);
-            const int kh = kh0 + 2 * (ntw ? r / ntw : 0), kw = kw0 + 2 * (ntw ? r % ntw : 0);
+            if (FK) {
+                const int tap = (int)(kbase / CK), c0 = (int)(kbase - (int64_t)tap * CK);
+                const int oh = (ih0 - (kh0 + 2 * (tap / ntw))) >> 1, ow = (iw0 - (kw0 + 2 * (tap % ntw))) >> 1;
+                const bool ok = bvalid && oh >= 0 && ow >= 0 && oh < a.OH && ow < a.OW;
+                const float* p = a.dy + xbase + (int64_t)(c0 + brow) * OHW + (int64_t)oh * a.OW + ow;
 #pragma unroll
-            for (int j = 0; j < NA; ++j) {
-                const int64_t c = m0 + colq + 16 * j;
-                ra[j] = (c < M && k < K) ? a.w[(((int64_t)n * a.cin + c) * KH + kh) * KW + kw] : 0.f;
-            }
+                for (int i = 0; i < NBv; ++i) rb[i] = ok ? p[(int64_t)i * BROWS * OHW] : 0.f;
+            } else {
 #pragma unroll
-            for (int i = 0; i < NBv; ++i) {
-                const int64_t kb = kbase + brow + BROWS * i;
-                float v = 0.f;
-                if (bvalid && kb < K) {
-                    const int nn = (int)(kb / KKp), rr = (int)(kb - (int64_t)(kb / KKp) * KKp);
-                    const int oh = (ih0 - (kh0 + 2 * (rr / ntw))) >> 1, ow = (iw0 - (kw0 + 2 * (rr % ntw))) >> 1;
-                    if (oh >= 0 && ow >= 0 && oh < a.OH && ow < a.OW)
-                        v = a.dy[xbase + ((int64_t)nn * a.OH + oh) * a.OW + ow];
+                for (int i = 0; i < NBv; ++i) {
+                    const int64_t kb = kbase + brow + BROWS * i;
+                    float v = 0.f;
+                    if (bvalid && kb < K) {
+                        const int tap = (int)(kb / CK), nn = (int)(kb - (int64_t)tap * CK);
+                        const int oh = (ih0 - (kh0 + 2 * (tap / ntw))) >> 1, ow = (iw0 - (kw0 + 2 * (tap % ntw))) >> 1;
+                        if (oh >= 0 && ow >= 0 && oh < a.OH && ow < a.OW)
+                            v = a.dy[xbase + ((int64_t)nn * a.OH + oh) * a.OW + ow];
+                    }
+                    rb[i] = v;
                 }
-                rb[i] = v;
             }
         } else {
             const bool kval = (kbase + kq) < k_end;
@@ -190,17 +232,13 @@ __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
                 const int64_t n = m0 + colq + 16 * j;
                 ra[j] = (kval && n < M) ? a.dy[(pb * a.cout + n) * OHW + pofs] : 0.f;
             }
+            const float* xb = a.x + pb * a.cin * IHW;
+            const int ihb = poh * s, iwb = pow_ * s;
 #pragma unroll
             for (int i = 0; i < NBv; ++i) {
-                const int64_t jj = n0 + colq + 16 * i;
-                float v = 0.f;
-                if (kval && jj < N) {
-                    const int c = (int)(jj / KK), r = (int)(jj - (int64_t)(jj / KK) * KK);
-                    const int ih = poh * s - pad + r / KW, iw = pow_ * s - pad + r % KW;
-                    if (ih >= 0 && ih < a.IH && iw >= 0 && iw < a.IW)
-                        v = a.x[((pb * a.cin + c) * a.IH + ih) * a.IW + iw];
-                }
-                rb[i] = v;
+                const int ih = ihb + wkh[i], iw = iwb + wkw[i];
+                rb[i] = (kval && ih >= 0 && ih < a.IH && iw >= 0 && iw < a.IW) ? xb[wco[i] + (int64_t)ih * a.IW + iw]
+                                                                              : 0.f;
             }
             // advance the pixel tracker by KC
             pow_ += KC;
@@ -272,8 +310,9 @@ __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
             const int ihc = (int)(p / IWc), iwc = (int)(p - (int64_t)(p / IWc) * IWc);
             obase = b * a.cin * IHW + (int64_t)(2 * ihc + ph) * a.IW + 2 * iwc + pw;
             ostride = IHW;
-        } else {
-            obase = (int64_t)slice * M * N + col;
+        } else {  // column (tap, c) -> the reference weight layout [cout][cin][KH][KW]
+            const int tap = (int)(col / a.cin), c = (int)(col - (int64_t)tap * a.cin);
+            obase = (int64_t)slice * M * N + (int64_t)c * KK + tap;
             ostride = N;
         }
 #pragma unroll
@@ -652,11 +691,14 @@ int launch_convg(ConvGArgs a, hipStream_t s) {
     PCX_CHECK_ARG(nblocks < ((int64_t)1 << 31), "convg: grid too large");
     if (a.mode == 2) PCX_CHECK_ARG(a.kslice % KC == 0 && a.nslice >= 1, "convg: bad weight-gradient split");
     dim3 grid((unsigned)nblocks);
-#define PCX_CG(MODE_, KH_, WM_)                                                  \
-    if (a.mode == MODE_ && a.KH == KH_ && wm == WM_) {                           \
-        convg_kernel<MODE_, KH_, KH_, WM_, 2><<<grid, 256, 0, s>>>(a);           \
-        PCX_LAUNCH_CHECK("convg_kernel");                                        \
-        return PCX_OK;                                                           \
+    // tap-uniform K chunks: the K channel count (cin forward, cout data gradient) a multiple of 16
+    const bool fk = a.mode == 2 || (a.mode == 0 ? a.cin : a.cout) % KC == 0;
+#define PCX_CG(MODE_, KH_, WM_)                                                                      \
+    if (a.mode == MODE_ && a.KH == KH_ && wm == WM_) {                                               \
+        if (fk) convg_kernel<MODE_, KH_, KH_, WM_, 2, true><<<grid, 256, 0, s>>>(a);                 \
+        else convg_kernel<MODE_, KH_, KH_, WM_, 2, false><<<grid, 256, 0, s>>>(a);                   \
+        PCX_LAUNCH_CHECK("convg_kernel");                                                            \
+        return PCX_OK;                                                                               \
     }
 #define PCX_CG_K(KH_) PCX_CG(0, KH_, 1) PCX_CG(0, KH_, 2) PCX_CG(1, KH_, 1) PCX_CG(1, KH_, 2) \
                       PCX_CG(2, KH_, 1) PCX_CG(2, KH_, 2)

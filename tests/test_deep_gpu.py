@@ -78,19 +78,34 @@ def test_deep_two_steps_with_fused_adam_track_reference():
         assert diff.max() <= tol, (k, diff.max())
 
 
-def _torch_reference(m, x, masks):
+def _torch_reference(m, x, masks, margins=None):
     """float64 evaluation of PhonemeNetDeep built from the model's own nn modules (a reference
-    layer-for-layer restatement of phoneme_cnn.py:274-304 with explicit Dropout2d masks)."""
-    x = m.init_conv(x)
+    layer-for-layer restatement of phoneme_cnn.py:274-304 with explicit Dropout2d masks).
+    `margins` (a list) collects min |pre-activation| of every ReLU: how far the case sits from a
+    kink where float32 rounding may legitimately flip a ReLU mask."""
+    def relu(v):
+        if margins is not None:
+            margins.append(v.detach().abs().min().item())
+        return F.relu(v)
+
+    def seq(mod, v):
+        for layer in mod:
+            v = relu(v) if isinstance(layer, nn.ReLU) else layer(v)
+        return v
+
+    x = seq(m.init_conv, x) if isinstance(m.init_conv, nn.Sequential) else m.init_conv(x)
     for blk, mk in zip(m.conv_blocks, masks):
         if isinstance(blk, nn.Sequential):  # use_residual = false
             for layer in blk:
-                x = x * mk[:, :, None, None] if isinstance(layer, nn.Dropout2d) else layer(x)
+                if isinstance(layer, nn.Dropout2d):
+                    x = x * mk[:, :, None, None]
+                else:
+                    x = relu(x) if isinstance(layer, nn.ReLU) else layer(x)
         else:
-            out = F.relu(blk.bn1(blk.conv1(x))) * mk[:, :, None, None]
+            out = relu(blk.bn1(blk.conv1(x))) * mk[:, :, None, None]
             out = blk.bn2(blk.conv2(out))
             sc = blk.shortcut(x) if len(blk.shortcut) else x
-            x = F.relu(out + sc)
+            x = relu(out + sc)
     if m.use_attention:
         x = x * torch.sigmoid(m.attention.conv(x))
     x = m.projection(x.mean(dim=(2, 3)))
@@ -100,11 +115,16 @@ def _torch_reference(m, x, masks):
 FULL = [64, 128, 256, 512]  # the benchmarked widths: stride-1 3x3 convs on the LDS-DMA / 32x32 engines
 
 
-@pytest.mark.parametrize("residual,T,dims,B", [(False, 200, None, 8), (False, 201, None, 8), (True, 57, None, 8),
-                                               (True, 200, FULL, 4), (True, 57, FULL, 5)])
-def test_deep_matches_float64_torch(residual, T, dims, B):
+# (False, 201) uses seed 5: with seed 3 one block-3 pre-activation sits 2.8e-7 from the ReLU kink
+# (float64 reference, 312 values per channel there), so float32 summation order alone decides that
+# mask bit and with it ~5 % of block 3's BN1 beta gradient -- measured: the forward matches to 6e-7
+# and only beta (not gamma: xhat = 0 at the kink with beta = 0) moves.  Not a property of the kernels.
+@pytest.mark.parametrize("residual,T,dims,B,seed", [(False, 200, None, 8, 3), (False, 201, None, 8, 5),
+                                                    (True, 57, None, 8, 3), (True, 200, FULL, 4, 3),
+                                                    (True, 57, FULL, 5, 3)])
+def test_deep_matches_float64_torch(residual, T, dims, B, seed):
     from phoneme_contrast_amd.losses import SupervisedContrastiveLoss
-    torch.manual_seed(3)
+    torch.manual_seed(seed)
     cfg = dict(DEEP, use_residual=residual)
     if dims:
         cfg["hidden_dims"] = dims
@@ -122,13 +142,14 @@ def test_deep_matches_float64_torch(residual, T, dims, B):
     loss.backward()
     ref.train()
     xr = x.double().requires_grad_(False)
-    er = _torch_reference(ref, xr, [k.double() for k in masks])
+    margins = []
+    er = _torch_reference(ref, xr, [k.double() for k in masks], margins)
     from oracle import torch_port as tp
     lr_ = tp.supcon(er, labels, 0.15, 0.07)
     lr_.backward()
     emb_err = (e.detach().cpu().double() - er.detach()).abs().max().item()
     print(f"deep residual={residual} T={T} dims={dims} B={B}: max |d emb| {emb_err:.2e}, "
-          f"|d loss| {abs(loss.item() - lr_.item()):.2e}")
+          f"|d loss| {abs(loss.item() - lr_.item()):.2e}, min ReLU margin {min(margins):.1e}")
     # full widths (512 channels through 4 train-mode BN layers over B = 4 samples) condition the
     # fp32 forward worse: the general implicit-GEMM engine alone measures 1.26e-5 on (200, FULL, 4),
     # the routed engines 1.41e-5 -- float32 rounding, not a layout error, so the bound is 5e-5 there
