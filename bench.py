@@ -25,6 +25,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 FP32_PEAK_TFLOPS = 157.3     # MI355X vector == matrix fp32 (MI355X_MICROARCH.md)
+BF16_PEAK_TFLOPS = 2500.0    # dense bf16 MFMA (MI355X_MICROARCH.md: ~2.5 PF dense, no sparsity)
 HBM_PEAK_GBS = 8000.0        # HBM3E spec
 METRIC = "MFCC-samples/sec per train step (cnn_small, batch 4096) at 1/2/4/8 MI355X"
 DEEP_DIMS = [64, 128, 256, 512]
@@ -171,6 +172,8 @@ def main():
     ap.add_argument("--T", type=int, default=200)
     ap.add_argument("--model", choices=["cnn_small", "cnn_deep"], default="cnn_small",
                     help="cnn_small is the north-star workload; cnn_deep is reported as a side line")
+    ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
+                    help="cnn_deep conv operand precision (bf16: float32 accumulation, float32 elsewhere)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     args = ap.parse_args()
@@ -193,7 +196,8 @@ def main():
     if deep:
         model = model_registry.create("phoneme_cnn_deep", {"in_channels": 1, "embedding_dim": D,
                                                            "use_attention": True, "dropout_rate": 0.2,
-                                                           "hidden_dims": DEEP_DIMS})
+                                                           "hidden_dims": DEEP_DIMS,
+                                                           "precision": args.precision})
     else:
         model = model_registry.create("phoneme_cnn", {"in_channels": 1, "embedding_dim": D,
                                                       "use_attention": True, "dropout_rate": 0.1})
@@ -252,6 +256,8 @@ def main():
     ms_step = 1000.0 * el / args.steps
     value = world * B * args.steps / el
     costs = deep_kernel_costs(B, F, T) if deep else kernel_costs(B, F, T, D)
+    bf16 = deep and args.precision == "bf16"
+    peak = BF16_PEAK_TFLOPS if bf16 else FP32_PEAK_TFLOPS
     roof = None
     kernels = {}
     if prof:
@@ -263,10 +269,10 @@ def main():
         avg_s = tot / cnt / 1000.0
         fl, by = costs[dom]
         ai = fl / by
-        if ai > FP32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9):
+        if ai > peak * 1e12 / (HBM_PEAK_GBS * 1e9):
             ach = fl / avg_s / 1e12
-            roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": FP32_PEAK_TFLOPS,
-                    "unit": "TFLOP/s", "frac": round(ach / FP32_PEAK_TFLOPS, 4)}
+            roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": peak,
+                    "unit": "TFLOP/s", "frac": round(ach / peak, 4)}
         else:
             ach = by / avg_s / 1e9
             roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
@@ -277,7 +283,7 @@ def main():
         roof["avg_launch_ms"] = round(avg_s * 1000.0, 4)
     sf, sb = deep_step_cost(B, F, T, D) if deep else step_cost(B, F, T, D)
     step_roof = {"flops_per_step": sf, "bytes_per_step": sb,
-                 "mfma_fraction": round(sf / (el / args.steps) / (FP32_PEAK_TFLOPS * 1e12), 4),
+                 "mfma_fraction": round(sf / (el / args.steps) / (peak * 1e12), 4),
                  "hbm_fraction": round(sb / (el / args.steps) / (HBM_PEAK_GBS * 1e9), 4)}
 
     cpu = None
@@ -288,7 +294,7 @@ def main():
             cpu = {"error": repr(exc)}
 
     out = {
-        "metric": METRIC if not deep else f"MFCC-samples/sec per train step (cnn_deep, batch {B})",
+        "metric": METRIC if not deep else f"MFCC-samples/sec per train step (cnn_deep{', bf16 convs' if bf16 else ''}, batch {B})",
         "value": round(value, 1),
         "unit": "samples/s",
         "n_gpus": world,
@@ -298,7 +304,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": "bf16 conv operands, fp32 accumulate/elsewhere" if bf16 else "fp32",
         "data": f"synthetic N(0,1) MFCC [B,1,40,T], random-init {args.model} (seed 42)",
         "config": {"workload": f"{args.model} contrastive train step: fwd + SupCon(T=0.15) + bwd + "
                                "grad all-reduce + Adam(lr 3e-4, wd 1e-4)",

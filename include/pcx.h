@@ -88,7 +88,18 @@ typedef struct pcx_net_config {
     int use_attention;
     int hidden_dims[4];   /* deep only */
     int use_residual;     /* deep only */
+    int conv_bf16;        /* deep only: conv operands rounded to bf16, float32 accumulation (0: fp32) */
 } pcx_net_config;
+
+/* The cnn_deep convolution engine as a standalone op (src/models/phoneme_cnn.py:146-304 convs):
+ * mode 0  out = conv2d(x, w)                      x [B][cin][IH][IW], w [cout][cin][k][k], out [B][cout][OH][OW]
+ * mode 1  out (+)= d conv2d / d x  applied to dy  dy [B][cout][OH][OW], out [B][cin][IH][IW] (+= if accumulate)
+ * mode 2  out = d conv2d / d w  applied to dy     out [cout][cin][k][k]; ws >= pcx_conv2d_workspace_bytes
+ * precision 0: float32 operands; 1: operands rounded to bf16, float32 accumulation.  Deterministic. */
+size_t pcx_conv2d_workspace_bytes(int mode, int precision, int B, int cin, int cout, int OH, int OW, int k);
+int pcx_conv2d(int mode, int precision, int B, int cin, int cout, int IH, int IW, int OH, int OW, int k, int stride,
+               int pad, const float* x, const float* w, const float* dy, float* out, int accumulate, void* ws,
+               size_t ws_bytes, hipStream_t stream);
 
 void* pcx_net_create(const pcx_net_config* cfg, int64_t B, int64_t F, int64_t T);
 void pcx_net_destroy(void* plan);

@@ -35,7 +35,8 @@ class NetConfig(ctypes.Structure):
     """pcx_net_config (include/pcx.h)."""
     _fields_ = [("kind", ctypes.c_int), ("in_channels", ctypes.c_int),
                 ("embedding_dim", ctypes.c_int), ("use_attention", ctypes.c_int),
-                ("hidden_dims", ctypes.c_int * 4), ("use_residual", ctypes.c_int)]
+                ("hidden_dims", ctypes.c_int * 4), ("use_residual", ctypes.c_int),
+                ("conv_bf16", ctypes.c_int)]
 
 
 _pp = ctypes.POINTER(ctypes.c_void_p)
@@ -75,6 +76,8 @@ SIGNATURES = {
                                    c_void_p]),
     "pcx_specaug": (c_int, [c_void_p, c_i64, c_int, c_i64, c_void_p, c_void_p, c_void_p, c_void_p,
                             ctypes.c_uint64, c_void_p]),
+    "pcx_conv2d_workspace_bytes": (c_size, [c_int] * 8),
+    "pcx_conv2d": (c_int, [c_int] * 12 + [c_void_p] * 4 + [c_int, c_void_p, c_size, c_void_p]),
 }
 
 

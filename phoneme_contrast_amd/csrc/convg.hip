@@ -659,7 +659,7 @@ int convg_nslice(const ConvGArgs& a, int64_t* kslice) {
     int64_t want = std::max<int64_t>(1, 2048 / (mt * nt));
     int64_t ks = (K + want - 1) / want;
     ks = std::max<int64_t>(ks, 256);
-    ks = (ks + KC - 1) / KC * KC;
+    ks = (ks + 31) / 32 * 32;  // the bf16 form advances 32 pixels per chunk
     *kslice = ks;
     return (int)((K + ks - 1) / ks);
 }
@@ -677,6 +677,7 @@ int launch_convg(ConvGArgs a, hipStream_t s) {
         }
         return PCX_OK;
     }
+    if (a.bf16) return launch_convg_bf16(a, s);
     const int64_t IHW = (int64_t)a.IH * a.IW, OHW = (int64_t)a.OH * a.OW;
     int64_t M, N;
     if (a.mode == 0) { M = a.cout; N = a.B * OHW; }

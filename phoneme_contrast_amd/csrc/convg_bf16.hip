@@ -1,0 +1,429 @@
+// bf16-operand form of the general implicit-GEMM convolution (convg.hip), for PhonemeNetDeep with
+// precision "bf16" (SURVEY 8(f) row 2): operands are rounded to bf16 (round-to-nearest-even) when
+// they are staged into LDS and multiplied on v_mfma_f32_32x32x16_bf16 with float32 accumulation;
+// activations, BN statistics, gradients and the optimizer stay float32 in HBM.
+//
+// Same GEMM views (modes 0 forward, 1 / 3 data gradient, 2 weight gradient), tap-major K order and
+// deterministic epilogue as convg_kernel.  What changes is the staging: an MFMA lane consumes 8
+// consecutive k of one row (A[m][8h .. 8h+7], B[8h .. 8h+7][n]), so every thread gathers whole
+// k-runs of ONE row and writes them to LDS as one 16-byte store, rows stored k-contiguous (80-byte
+// stride: conflict-free ds_read_b128).  K advances 32 per chunk (two MFMAs per tile, one barrier).
+#include "kernels.h"
+
+namespace pcx {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int KB = 32;  // k per chunk
+constexpr int RS = 40;  // LDS row stride in bf16 (32 k + 8 pad = 80 B)
+
+struct Pix {  // (sample, row, column) of an output pixel index, advanced without division
+    int64_t b;
+    int oh, ow;
+};
+
+__device__ __forceinline__ void pix_step(Pix& p, int n, int OH, int OW) {
+    p.ow += n;
+    while (p.ow >= OW) {
+        p.ow -= OW;
+        if (++p.oh == OH) { p.oh = 0; ++p.b; }
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void store_bf16(__bf16* dst, const float (&v)[N]) {
+    static_assert(N % 4 == 0, "runs of 4 / 8 / 16");
+#pragma unroll
+    for (int q = 0; q < N / 8; ++q) {
+        bf16x8 t;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t[j] = (__bf16)v[8 * q + j];
+        *reinterpret_cast<bf16x8*>(dst + 8 * q) = t;
+    }
+    if constexpr (N % 8) {
+        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+        bf16x4 t;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) t[j] = (__bf16)v[N - 4 + j];
+        *reinterpret_cast<bf16x4*>(dst + N - 4) = t;
+    }
+}
+
+template <int MODE, int KH, int KW, int WM, bool FK>
+__global__ __launch_bounds__(256) void convg_bf16_kernel(ConvGArgs a) {
+    constexpr int KK = KH * KW;
+    constexpr int WN = 2;
+    constexpr int BM = 64 * WM, BN = 64 * WN;
+    constexpr int NA = KB * BM / 256, NB = KB * BN / 256;  // k per thread: 8 / 16, 16
+    __shared__ __attribute__((aligned(16))) __bf16 As[2][BM][RS];
+    __shared__ __attribute__((aligned(16))) __bf16 Bs[2][BN][RS];
+
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+    const int wave = tid >> 6, wr = wave >> 1, wc = wave & 1;
+    const int64_t OHW = (int64_t)a.OH * a.OW, IHW = (int64_t)a.IH * a.IW;
+    const int s = a.stride, pad = a.pad;
+    const int CK = MODE == 0 ? a.cin : a.cout;
+
+    const int ph = a.par >> 1, pw = a.par & 1;
+    const int kh0 = (ph + pad) & 1, kw0 = (pw + pad) & 1;
+    const int nth = (KH - kh0 + 1) / 2, ntw = (KW - kw0 + 1) / 2, KKp = nth * ntw;
+    const int IHc = (a.IH - ph + 1) / 2, IWc = (a.IW - pw + 1) / 2;
+    const int64_t CHW = (int64_t)IHc * IWc;
+    int64_t M, N, K;
+    if (MODE == 0) { M = a.cout; N = a.B * OHW; K = (int64_t)a.cin * KK; }
+    else if (MODE == 1) { M = a.cin; N = a.B * IHW; K = (int64_t)a.cout * KK; }
+    else if (MODE == 3) { M = a.cin; N = a.B * CHW; K = (int64_t)a.cout * KKp; }
+    else { M = a.cout; N = (int64_t)a.cin * KK; K = a.B * OHW; }
+    const int64_t mt = (M + BM - 1) / BM, nt = (N + BN - 1) / BN;
+    int64_t bid = blockIdx.x;
+    const int64_t tm = bid % mt;
+    bid /= mt;
+    const int64_t tn = bid % nt;
+    const int slice = (int)(bid / nt);
+    const int64_t m0 = tm * BM, n0 = tn * BN;
+    int64_t k_begin = 0, k_end = K;
+    if (MODE == 2) {
+        k_begin = (int64_t)slice * a.kslice;
+        k_end = min(K, k_begin + a.kslice);
+    }
+    const int nch = (int)((k_end - k_begin + KB - 1) / KB);
+
+    // staging roles: A row am with k-run akg*NA.., B row bn with k-run bkg*NB..
+    const int am = tid % BM, akg = tid / BM;
+    const int bn = tid % BN, bkg = tid / BN;
+    const int64_t arow = m0 + am, brow = n0 + bn;
+    const bool avalid = arow < M, bvalid = brow < N;
+
+    // modes 0/1/3: the B row is an output (or input-gradient) pixel
+    int64_t xbase = 0;
+    int ih0 = 0, iw0 = 0;
+    if (MODE == 0 || MODE == 1 || MODE == 3) {
+        const int64_t mm = bvalid ? brow : 0;
+        if (MODE == 3) {
+            const int64_t b = mm / CHW, p = mm - b * CHW;
+            const int ihc = (int)(p / IWc), iwc = (int)(p - (int64_t)(p / IWc) * IWc);
+            xbase = b * a.cout * OHW;
+            ih0 = 2 * ihc + ph + pad;
+            iw0 = 2 * iwc + pw + pad;
+        } else if (MODE == 0) {
+            const int64_t b = mm / OHW, p = mm - b * OHW;
+            const int oh = (int)(p / a.OW), ow = (int)(p - (int64_t)(p / a.OW) * a.OW);
+            xbase = b * a.cin * IHW;
+            ih0 = oh * s - pad;
+            iw0 = ow * s - pad;
+        } else {
+            const int64_t b = mm / IHW, p = mm - b * IHW;
+            const int ih = (int)(p / a.IW), iw = (int)(p - (int64_t)(p / a.IW) * a.IW);
+            xbase = b * a.cout * OHW;
+            ih0 = ih + pad;
+            iw0 = iw + pad;
+        }
+    }
+    // mode 2: pixel trackers of the two k-runs; the B row's fixed (tap, channel)
+    Pix pa{0, 0, 0}, pbx{0, 0, 0};
+    int wkh = 0, wkw = 0;
+    int64_t wco = 0;
+    if (MODE == 2) {
+        auto init = [&](Pix& p, int64_t q) {
+            p.b = q / OHW;
+            const int64_t r = q - p.b * OHW;
+            p.oh = (int)(r / a.OW);
+            p.ow = (int)(r - (int64_t)p.oh * a.OW);
+        };
+        init(pa, k_begin + (int64_t)akg * NA);
+        init(pbx, k_begin + (int64_t)bkg * NB);
+        const int tap = (int)(brow / a.cin), c = (int)(brow - (int64_t)tap * a.cin);
+        wkh = bvalid ? tap / KW - pad : -(1 << 28);
+        wkw = tap % KW - pad;
+        wco = (int64_t)c * IHW;
+    }
+
+    float ra[NA], rb[NB];
+    auto gather = [&](int chunk) {
+        const int64_t kbase = k_begin + (int64_t)chunk * KB;
+        if (MODE == 0 || MODE == 1 || MODE == 3) {
+            // ---- A: weights of row m = arow, k-run kbase + akg*NA + j
+            const int64_t k0 = kbase + akg * NA;
+            if (FK) {
+                const int tap = (int)(kbase / CK), ch0 = (int)(k0 - (int64_t)tap * CK);
+                const float* wp;
+                int64_t wst;
+                if (MODE == 0) { wp = a.w + (arow * a.cin + ch0) * KK + tap; wst = KK; }
+                else if (MODE == 1) { wp = a.w + ((int64_t)ch0 * a.cin + arow) * KK + tap; wst = (int64_t)a.cin * KK; }
+                else {
+                    wp = a.w + (((int64_t)ch0 * a.cin + arow) * KH + kh0 + 2 * (tap / ntw)) * KW + kw0 + 2 * (tap % ntw);
+                    wst = (int64_t)a.cin * KK;
+                }
+#pragma unroll
+                for (int j = 0; j < NA; ++j) ra[j] = avalid ? wp[j * wst] : 0.f;
+            } else {
+#pragma unroll
+                for (int j = 0; j < NA; ++j) {
+                    const int64_t k = k0 + j;
+                    float v = 0.f;
+                    if (avalid && k < K) {
+                        const int tap = (int)(k / CK), ch = (int)(k - (int64_t)tap * CK);
+                        if (MODE == 0) v = a.w[(arow * a.cin + ch) * KK + tap];
+                        else if (MODE == 1) v = a.w[((int64_t)ch * a.cin + arow) * KK + tap];
+                        else
+                            v = a.w[(((int64_t)ch * a.cin + arow) * KH + kh0 + 2 * (tap / ntw)) * KW + kw0 +
+                                    2 * (tap % ntw)];
+                    }
+                    ra[j] = v;
+                }
+            }
+            // ---- B: activations (mode 0) / output gradients (modes 1, 3) of pixel brow
+            const int64_t kb0 = kbase + bkg * NB;
+            if (FK) {
+                const int tap = (int)(kbase / CK), c0 = (int)(kb0 - (int64_t)tap * CK);
+                int ih, iw;
+                bool ok;
+                const float* src;
+                int64_t cst;
+                if (MODE == 0) {
+                    ih = ih0 + tap / KW;
+                    iw = iw0 + tap % KW;
+                    ok = bvalid && ih >= 0 && ih < a.IH && iw >= 0 && iw < a.IW;
+                    src = a.x + xbase + (int64_t)c0 * IHW + (int64_t)ih * a.IW + iw;
+                    cst = IHW;
+                } else {
+                    int oh, ow;
+                    if (MODE == 3) {
+                        oh = (ih0 - (kh0 + 2 * (tap / ntw))) >> 1;
+                        ow = (iw0 - (kw0 + 2 * (tap % ntw))) >> 1;
+                        ok = true;
+                    } else {
+                        const int th = ih0 - tap / KW, tw = iw0 - tap % KW;
+                        ok = th >= 0 && tw >= 0;
+                        oh = th;
+                        ow = tw;
+                        if (s == 2) {
+                            ok = ok && ((th | tw) & 1) == 0;
+                            oh = th >> 1;
+                            ow = tw >> 1;
+                        }
+                    }
+                    ok = ok && bvalid && oh >= 0 && ow >= 0 && oh < a.OH && ow < a.OW;
+                    src = a.dy + xbase + (int64_t)c0 * OHW + (int64_t)oh * a.OW + ow;
+                    cst = OHW;
+                }
+#pragma unroll
+                for (int i = 0; i < NB; ++i) rb[i] = ok ? src[i * cst] : 0.f;
+            } else {
+#pragma unroll
+                for (int i = 0; i < NB; ++i) {
+                    const int64_t k = kb0 + i;
+                    float v = 0.f;
+                    if (bvalid && k < K) {
+                        const int tap = (int)(k / CK), ch = (int)(k - (int64_t)tap * CK);
+                        if (MODE == 0) {
+                            const int ih = ih0 + tap / KW, iw = iw0 + tap % KW;
+                            if (ih >= 0 && ih < a.IH && iw >= 0 && iw < a.IW)
+                                v = a.x[xbase + (int64_t)ch * IHW + (int64_t)ih * a.IW + iw];
+                        } else {
+                            int oh, ow;
+                            bool ok;
+                            if (MODE == 3) {
+                                oh = (ih0 - (kh0 + 2 * (tap / ntw))) >> 1;
+                                ow = (iw0 - (kw0 + 2 * (tap % ntw))) >> 1;
+                                ok = true;
+                            } else {
+                                const int th = ih0 - tap / KW, tw = iw0 - tap % KW;
+                                ok = th >= 0 && tw >= 0;
+                                oh = th;
+                                ow = tw;
+                                if (s == 2) {
+                                    ok = ok && ((th | tw) & 1) == 0;
+                                    oh = th >> 1;
+                                    ow = tw >> 1;
+                                }
+                            }
+                            if (ok && oh >= 0 && ow >= 0 && oh < a.OH && ow < a.OW)
+                                v = a.dy[xbase + (int64_t)ch * OHW + (int64_t)oh * a.OW + ow];
+                        }
+                    }
+                    rb[i] = v;
+                }
+            }
+        } else {
+            // ---- mode 2: A = dy[b][n = arow][pixel], B = x[b][c][pixel*s + tap] over a k-run of pixels
+            const int64_t qa = kbase + akg * NA, qb = kbase + bkg * NB;
+            Pix p = pa;
+#pragma unroll
+            for (int j = 0; j < NA; ++j) {
+                ra[j] = (avalid && qa + j < k_end) ? a.dy[(p.b * a.cout + arow) * OHW + (int64_t)p.oh * a.OW + p.ow]
+                                                   : 0.f;
+                pix_step(p, 1, a.OH, a.OW);
+            }
+            p = pbx;
+#pragma unroll
+            for (int i = 0; i < NB; ++i) {
+                const int ih = p.oh * s + wkh, iw = p.ow * s + wkw;
+                rb[i] = (qb + i < k_end && ih >= 0 && ih < a.IH && iw >= 0 && iw < a.IW)
+                            ? a.x[p.b * a.cin * IHW + wco + (int64_t)ih * a.IW + iw]
+                            : 0.f;
+                pix_step(p, 1, a.OH, a.OW);
+            }
+            pix_step(pa, KB, a.OH, a.OW);
+            pix_step(pbx, KB, a.OH, a.OW);
+        }
+    };
+    auto stash = [&](int buf) {
+        store_bf16<NA>(&As[buf][am][akg * NA], ra);
+        store_bf16<NB>(&Bs[buf][bn][bkg * NB], rb);
+    };
+
+    f32x16 acc[WM][WN];
+#pragma unroll
+    for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < WN; ++ni) acc[mi][ni] = f32x16{0.f};
+
+    if (nch > 0) {
+        gather(0);
+        stash(0);
+    }
+    __syncthreads();
+    for (int ch = 0; ch < nch; ++ch) {
+        const int buf = ch & 1;
+        if (ch + 1 < nch) gather(ch + 1);
+#pragma unroll
+        for (int ks = 0; ks < KB / 16; ++ks) {
+            bf16x8 av[WM], bv[WN];
+#pragma unroll
+            for (int mi = 0; mi < WM; ++mi)
+                av[mi] = *reinterpret_cast<const bf16x8*>(&As[buf][wr * 32 * WM + mi * 32 + l32][16 * ks + 8 * h]);
+#pragma unroll
+            for (int ni = 0; ni < WN; ++ni)
+                bv[ni] = *reinterpret_cast<const bf16x8*>(&Bs[buf][wc * 32 * WN + ni * 32 + l32][16 * ks + 8 * h]);
+#pragma unroll
+            for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < WN; ++ni)
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[mi], bv[ni], acc[mi][ni], 0, 0, 0);
+        }
+        if (ch + 1 < nch) stash(buf ^ 1);
+        __syncthreads();
+    }
+
+    // ---- epilogue (as convg_kernel)
+#pragma unroll
+    for (int ni = 0; ni < WN; ++ni) {
+        const int64_t col = n0 + wc * 32 * WN + ni * 32 + l32;
+        if (col >= N) continue;
+        int64_t obase, ostride;
+        if (MODE == 0) {
+            const int64_t b = col / OHW;
+            obase = b * a.cout * OHW + (col - b * OHW);
+            ostride = OHW;
+        } else if (MODE == 1) {
+            const int64_t b = col / IHW;
+            obase = b * a.cin * IHW + (col - b * IHW);
+            ostride = IHW;
+        } else if (MODE == 3) {
+            const int64_t b = col / CHW, p = col - b * CHW;
+            const int ihc = (int)(p / IWc), iwc = (int)(p - (int64_t)(p / IWc) * IWc);
+            obase = b * a.cin * IHW + (int64_t)(2 * ihc + ph) * a.IW + 2 * iwc + pw;
+            ostride = IHW;
+        } else {
+            const int tap = (int)(col / a.cin), c = (int)(col - (int64_t)tap * a.cin);
+            obase = (int64_t)slice * M * N + (int64_t)c * KK + tap;
+            ostride = N;
+        }
+#pragma unroll
+        for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int64_t row = m0 + wr * 32 * WM + mi * 32 + acc_row(r, h);
+                if (row < M) {
+                    float* o = a.out + obase + row * ostride;
+                    if ((MODE == 1 || MODE == 3) && a.accumulate) *o += acc[mi][ni][r];
+                    else *o = acc[mi][ni][r];
+                }
+            }
+    }
+}
+
+}  // namespace
+
+int launch_convg_bf16(ConvGArgs a, hipStream_t s) {
+    const int64_t IHW = (int64_t)a.IH * a.IW, OHW = (int64_t)a.OH * a.OW;
+    int64_t M, N;
+    if (a.mode == 0) { M = a.cout; N = a.B * OHW; }
+    else if (a.mode == 1) { M = a.cin; N = a.B * IHW; }
+    else if (a.mode == 3) {
+        M = a.cin;
+        N = a.B * (int64_t)((a.IH - (a.par >> 1) + 1) / 2) * ((a.IW - (a.par & 1) + 1) / 2);
+    } else { M = a.cout; N = (int64_t)a.cin * a.KH * a.KW; }
+    const int wm = M >= 128 ? 2 : 1;
+    const int64_t mt = ceil_div(M, 64 * wm), nt = ceil_div(N, 128);
+    const int64_t nblocks = mt * nt * (a.mode == 2 ? a.nslice : 1);
+    PCX_CHECK_ARG(nblocks < ((int64_t)1 << 31), "convg_bf16: grid too large");
+    if (a.mode == 2) PCX_CHECK_ARG(a.kslice % KB == 0 && a.nslice >= 1, "convg_bf16: bad weight-gradient split");
+    const bool fk = a.mode == 2 || (a.mode == 0 ? a.cin : a.cout) % KB == 0;
+    dim3 grid((unsigned)nblocks);
+#define PCX_CB(MODE_, KH_, WM_)                                                                 \
+    if (a.mode == MODE_ && a.KH == KH_ && wm == WM_) {                                          \
+        if (fk) convg_bf16_kernel<MODE_, KH_, KH_, WM_, true><<<grid, 256, 0, s>>>(a);          \
+        else convg_bf16_kernel<MODE_, KH_, KH_, WM_, false><<<grid, 256, 0, s>>>(a);            \
+        PCX_LAUNCH_CHECK("convg_bf16_kernel");                                                  \
+        return PCX_OK;                                                                          \
+    }
+#define PCX_CB_K(KH_) PCX_CB(0, KH_, 1) PCX_CB(0, KH_, 2) PCX_CB(1, KH_, 1) PCX_CB(1, KH_, 2) \
+                      PCX_CB(2, KH_, 1) PCX_CB(2, KH_, 2)
+    PCX_CB_K(1)
+    PCX_CB_K(3)
+    PCX_CB_K(7)
+    PCX_CB(3, 1, 1) PCX_CB(3, 1, 2) PCX_CB(3, 3, 1) PCX_CB(3, 3, 2)
+#undef PCX_CB_K
+#undef PCX_CB
+    set_error("convg_bf16: kernel size %d unsupported", a.KH);
+    return PCX_EINVAL;
+}
+
+}  // namespace pcx
+
+// ---------------------------------------------------------------------------------------------
+// The cnn_deep convolution engine as a standalone operation (include/pcx.h: pcx_conv2d): used by
+// the kernel-level parity tests of both precisions and by micro-benchmarks.
+extern "C" size_t pcx_conv2d_workspace_bytes(int mode, int precision, int B, int cin, int cout, int OH, int OW,
+                                             int k) {
+    (void)precision;
+    if (mode != 2) return 0;
+    pcx::ConvGArgs a{};
+    a.B = B; a.cin = cin; a.cout = cout; a.OH = OH; a.OW = OW; a.KH = a.KW = k;
+    int64_t ks;
+    const int ns = pcx::convg_nslice(a, &ks);
+    return (size_t)ns * cout * cin * k * k * 4;
+}
+
+extern "C" int pcx_conv2d(int mode, int precision, int B, int cin, int cout, int IH, int IW, int OH, int OW, int k,
+                          int stride, int pad, const float* x, const float* w, const float* dy, float* out,
+                          int accumulate, void* ws, size_t ws_bytes, hipStream_t stream) {
+    using namespace pcx;
+    PCX_CHECK_ARG(mode >= 0 && mode <= 2, "pcx_conv2d: mode %d (0 forward, 1 data gradient, 2 weight gradient)", mode);
+    PCX_CHECK_ARG(precision == 0 || precision == 1, "pcx_conv2d: precision %d (0 fp32, 1 bf16)", precision);
+    PCX_CHECK_ARG(B > 0 && cin > 0 && cout > 0 && k > 0 && IH > 0 && IW > 0, "pcx_conv2d: empty shape");
+    PCX_CHECK_ARG(OH == (IH + 2 * pad - k) / stride + 1 && OW == (IW + 2 * pad - k) / stride + 1,
+                  "pcx_conv2d: output %dx%d inconsistent with input %dx%d, k %d, stride %d, pad %d", OH, OW, IH, IW,
+                  k, stride, pad);
+    PCX_CHECK_ARG(out && (mode == 2 ? (x && dy) : mode == 1 ? (w && dy) : (x && w)), "pcx_conv2d: NULL operand");
+    ConvGArgs a{};
+    a.mode = mode;
+    a.B = B; a.cin = cin; a.cout = cout;
+    a.IH = IH; a.IW = IW; a.OH = OH; a.OW = OW;
+    a.KH = a.KW = k; a.stride = stride; a.pad = pad;
+    a.x = x; a.w = w; a.dy = dy; a.out = out;
+    a.accumulate = accumulate;
+    a.bf16 = precision;
+    if (mode != 2) return launch_convg(a, stream);
+    a.nslice = convg_nslice(a, &a.kslice);
+    const size_t need = pcx_conv2d_workspace_bytes(mode, precision, B, cin, cout, OH, OW, k);
+    PCX_CHECK_ARG(ws && ws_bytes >= need, "pcx_conv2d: weight gradient needs %zu workspace bytes, got %zu", need,
+                  ws_bytes);
+    a.out = static_cast<float*>(ws);
+    const int rc = launch_convg(a, stream);
+    if (rc != PCX_OK) return rc;
+    return launch_sum_slices(a.out, a.nslice, (int64_t)cout * cin * k * k, out, stream);
+}

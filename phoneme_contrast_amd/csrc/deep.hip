@@ -31,6 +31,7 @@ struct DeepBlock {
 
 struct DeepPlan {
     bool residual;
+    bool bf16;                     // every conv on convg_bf16 (bf16 operands, float32 accumulation)
     int h[4];
     int H0, W0, H1, W1;
     size_t y0, a0, cf0, cfb0, dz0, mparg;
@@ -54,6 +55,7 @@ int build_deep(Plan& p) {
     DeepPlan& d = *dp;
     const int B = p.B;
     d.residual = p.cfg.use_residual != 0;
+    d.bf16 = p.cfg.conv_bf16 != 0;
     for (int i = 0; i < 4; ++i) {
         d.h[i] = p.cfg.hidden_dims[i];
         PCX_CHECK_ARG(d.h[i] >= 1 && d.h[i] <= 4096, "PhonemeNetDeep: hidden_dims[%d] = %d unsupported", i, d.h[i]);
@@ -88,7 +90,7 @@ int build_deep(Plan& p) {
     int cmax = 0;
     for (int i = 0; i < 4; ++i) cmax = std::max(cmax, d.h[i]);
     const char* dmaenv = getenv("PCX_DEEP_DMA");  // "0": every conv on the general engine (A/B)
-    const bool route = !(dmaenv && dmaenv[0] == '0');
+    const bool route = !d.bf16 && !(dmaenv && dmaenv[0] == '0');
     // a stride-1 3x3 conv cin -> cout at HxW on the DMA conv (fwd, dgrad) and the 32x32 wgrad
     auto plan_routed = [&](int ci, int co, int h, int w, bool* fwd, bool* w32, WgradArgs* wga, int* nblk) {
         *fwd = route && (co == 32 || co % 64 == 0) && (ci == 32 || ci % 64 == 0) && ci % 2 == 0;
@@ -217,6 +219,7 @@ int conv_bn_fwd(const Ctx& c, const char* label, int layer, const float* x, int 
         a.IH = IH; a.IW = IW; a.OH = OH; a.OW = OW;
         a.KH = a.KW = k; a.stride = stride; a.pad = pad;
         a.x = x; a.w = wgt; a.out = y;
+        a.bf16 = c.d.bf16;
         Scope sc(&c.p.prof, c.s, label, layer);
         RC(launch_convg(a, c.s));
     }
@@ -273,6 +276,7 @@ int conv_wgrad(const Ctx& c, int layer, const float* x, int cin, int IH, int IW,
     a.IH = IH; a.IW = IW; a.OH = OH; a.OW = OW;
     a.KH = a.KW = k; a.stride = stride; a.pad = pad;
     a.x = x; a.dy = dy;
+    a.bf16 = c.d.bf16;
     a.nslice = convg_nslice(a, &a.kslice);
     float* wgp = c.w<float>(c.d.wgp);
     a.out = wgp;
@@ -305,6 +309,7 @@ int conv_dgrad(const Ctx& c, int layer, const float* dy, int cout, int OH, int O
     a.IH = IH; a.IW = IW; a.OH = OH; a.OW = OW;
     a.KH = a.KW = k; a.stride = stride; a.pad = pad;
     a.w = wgt; a.dy = dy; a.out = dx; a.accumulate = accumulate;
+    a.bf16 = c.d.bf16;
     Scope sc(&c.p.prof, c.s, "conv_dgrad", layer);
     return launch_convg(a, c.s);
 }

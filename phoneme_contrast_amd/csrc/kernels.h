@@ -231,10 +231,12 @@ struct ConvGArgs {
     float* out;           // 0: y [B][cout][OH][OW]; 1: dx [B][cin][IH][IW]; 2: [nslice][cout][cin*KH*KW]
     int accumulate;       // modes 1, 3: dx += result
     int par;              // mode 3 (internal): parity class (ih % 2) * 2 + (iw % 2)
-    int64_t kslice;       // mode 2: pixels per slice (multiple of 16)
+    int64_t kslice;       // mode 2: pixels per slice (multiple of 32)
     int nslice;
+    int bf16;             // operands rounded to bf16, float32 accumulation (convg_bf16.hip)
 };
 int launch_convg(ConvGArgs a, hipStream_t s);
+int launch_convg_bf16(ConvGArgs a, hipStream_t s);
 int convg_nslice(const ConvGArgs& a, int64_t* kslice);
 
 enum MaskMode { MASK_NONE = 0, MASK_OUT = 1, MASK_BN = 2 };

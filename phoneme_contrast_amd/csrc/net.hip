@@ -423,7 +423,9 @@ extern "C" void* pcx_net_create(const pcx_net_config* cfg, int64_t B, int64_t F,
                         : (wg && strcmp(wg, "win16") == 0) ? 3 : 0;
     }
     int rc = PCX_EINVAL;
-    if (cfg->kind == PCX_NET_CNN_SMALL) rc = build_small(*p);
+    if (cfg->kind == PCX_NET_CNN_SMALL && cfg->conv_bf16)
+        set_error("pcx_net_create: conv_bf16 is a PhonemeNetDeep option (cnn_small is float32)");
+    else if (cfg->kind == PCX_NET_CNN_SMALL) rc = build_small(*p);
     else if (cfg->kind == PCX_NET_CNN_DEEP) rc = build_deep(*p);
     else set_error("pcx_net_create: network kind %d not supported", cfg->kind);
     if (rc) { delete p; return nullptr; }

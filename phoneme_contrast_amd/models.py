@@ -356,6 +356,11 @@ class PhonemeNetDeep(_NativeNet):
         self.dropout_rate = config.get("dropout_rate", 0.2)
         self.hidden_dims = list(config.get("hidden_dims", [64, 128, 256, 512]))
         self.use_residual = config.get("use_residual", True)
+        # MI355X addition: "bf16" runs every convolution on bf16 operands with float32 accumulation
+        # (SURVEY 8(f) row 2); parameters, activations, statistics and gradients stay float32
+        self.precision = config.get("precision", "fp32")
+        if self.precision not in ("fp32", "bf16"):
+            raise ValueError(f"PhonemeNetDeep: precision {self.precision!r} (fp32 | bf16)")
         self._build_network()
         self._initialize_weights()
 
@@ -391,4 +396,5 @@ class PhonemeNetDeep(_NativeNet):
         for i, d in enumerate(self.hidden_dims[:4]):
             cfg.hidden_dims[i] = d
         cfg.use_residual = 1 if self.use_residual else 0
+        cfg.conv_bf16 = 1 if self.precision == "bf16" else 0
         return cfg

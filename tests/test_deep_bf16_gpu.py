@@ -1,0 +1,148 @@
+"""PhonemeNetDeep with precision "bf16" (SURVEY 8(f) row 2): every convolution multiplies bf16-rounded
+operands on v_mfma_f32_32x32x16_bf16 with float32 accumulation; everything else is float32.
+
+Per case the GPU step is compared with a float64 evaluation in which every conv's three GEMMs see
+bf16-rounded operands, as the engine's do (kernel-level exactness of that rounding model is
+tests/test_conv2d_gpu.py): embeddings within 1e-2 (unit-norm rows; float32 vs float64 activations
+round to different bf16 values near rounding boundaries, and those flips cascade), loss within 5e-2
+of the exact float64 loss, every gradient tensor at cosine > 0.98 to the rounded reference's
+(measured >= 0.995),
+running statistics within 1e-2 relative.  bf16 is a throughput option, not fp32 parity.
+Reference: src/models/phoneme_cnn.py:146-304 (the reference trains in float32; bf16 is an MI355X
+addition)."""
+import pytest
+import torch
+import torch.nn as nn
+
+from golden_util import bn_fed_bias
+from test_deep_gpu import DEEP, FULL, _torch_reference
+
+pytestmark = pytest.mark.gpu
+
+
+def _rd(t):
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
+class _Bf16Conv(torch.autograd.Function):
+    """conv2d whose three GEMMs see bf16-rounded operands, as the MI355X engine's do: forward
+    (x, w), data gradient (dy, w), weight gradient (dy, x); float64 arithmetic otherwise."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pad):
+        xr, wr = _rd(x), _rd(w)
+        ctx.save_for_backward(xr, wr)
+        ctx.conf = (stride, pad, x.shape, w.shape)
+        return torch.nn.functional.conv2d(xr, wr, b, stride, pad)
+
+    @staticmethod
+    def backward(ctx, gy):
+        xr, wr = ctx.saved_tensors
+        stride, pad, xs, ws = ctx.conf
+        gr = _rd(gy)
+        dx = torch.nn.grad.conv2d_input(xs, wr, gr, stride=stride, padding=pad)
+        dw = torch.nn.grad.conv2d_weight(xr, ws, gr, stride=stride, padding=pad)
+        return dx, dw, gy.sum(dim=(0, 2, 3)), None, None
+
+
+def _round_conv_operands(model):
+    """Every trunk Conv2d computes through _Bf16Conv (the attention's 1x1 conv runs in float32 in
+    the head kernel, as in the fp32 path)."""
+    for name, mod in model.named_modules():
+        if isinstance(mod, nn.Conv2d) and not name.startswith("attention"):
+            mod.forward = (lambda m: (lambda x: _Bf16Conv.apply(x, m.weight, m.bias, m.stride, m.padding)))(mod)
+
+
+@pytest.mark.parametrize("residual,T,dims,B", [(True, 200, None, 32), (False, 57, None, 32),
+                                               (True, 100, [16, 32, 64, 128], 32), (True, 100, FULL, 16)])
+def test_deep_bf16_step(residual, T, dims, B):
+    from oracle import torch_port as tp
+    from phoneme_contrast_amd.losses import SupervisedContrastiveLoss
+    from phoneme_contrast_amd.models import PhonemeNetDeep
+    torch.manual_seed(11)
+    cfg = dict(DEEP, use_residual=residual, precision="bf16")
+    if dims:
+        cfg["hidden_dims"] = dims
+    m = PhonemeNetDeep(cfg)
+    ref = PhonemeNetDeep(dict(cfg, precision="fp32")).double()
+    ref.load_state_dict(m.state_dict())
+    rnd = PhonemeNetDeep(dict(cfg, precision="fp32")).double()
+    rnd.load_state_dict(m.state_dict())
+    _round_conv_operands(rnd)
+    m = m.cuda().train()
+    x = torch.randn(B, 1, 40, T)
+    labels = torch.arange(B) % 4
+    masks = [(torch.rand(B, c) > 0.2).float() / 0.8 for c in cfg["hidden_dims"]]
+    m.set_dropout_masks(masks)
+    e = m(x.cuda())
+    loss = SupervisedContrastiveLoss(temperature=0.15)(e, labels.cuda())
+    loss.backward()
+    md = [k.double() for k in masks]
+    ref.train()
+    rnd.train()
+    e_rnd = _torch_reference(rnd, x.double(), md)
+    tp.supcon(e_rnd, labels, 0.15, 0.07).backward()
+    e_ref = _torch_reference(ref, x.double(), md)
+    l_ref = tp.supcon(e_ref, labels, 0.15, 0.07)
+    l_ref.backward()
+    e64 = e.detach().cpu().double()
+    exact = (e64 - e_rnd.detach()).abs().max().item()
+    rerr = {}
+    for (k, p), (_, q) in zip(m.named_parameters(), rnd.named_parameters()):
+        if not bn_fed_bias(k, None):
+            rerr[k] = ((p.grad.cpu().double() - q.grad).abs().max() / max(q.grad.abs().max().item(), 1e-30)).item()
+    rworst = max(rerr, key=rerr.get)
+    # the float64 references themselves: how far bf16 rounding alone moves the gradients
+    f64gap = {}
+    for (k, p), (_, q) in zip(rnd.named_parameters(), ref.named_parameters()):
+        if not bn_fed_bias(k, None):
+            f64gap[k] = ((p.grad - q.grad).abs().max() / max(q.grad.abs().max().item(), 1e-30)).item()
+    vs_f64 = (e64 - e_ref.detach()).abs().max().item()
+    # gradients: per tensor, cosine similarity with the rounded-operand float64 gradient (max-norm
+    # errors are not informative here: bf16 rounding alone moves the float64 gradient of this
+    # random-init net by up to 1.0 x max|g| at B = 32, measured, because its parameter gradients
+    # are small differences of large sums; the flips of the rounding boundary between float32 and
+    # float64 activations then decorrelate individual elements, not the tensors)
+    cos = {}
+    for (k, p), (_, q) in zip(m.named_parameters(), rnd.named_parameters()):
+        if bn_fed_bias(k, None) or k.startswith("attention"):
+            continue
+        g, r = p.grad.cpu().double().flatten(), q.grad.flatten()
+        cos[k] = (g @ r / (g.norm() * r.norm() + 1e-300)).item()
+    worst = min(cos, key=cos.get)
+    print(f"bf16 residual={residual} T={T} dims={dims} B={B}: emb vs rounded-operand f64 {exact:.2e}, "
+          f"vs f64 {vs_f64:.2e}, |d loss| {abs(loss.item() - l_ref.item()):.2e}, min grad cosine {worst} {cos[worst]:.4f}")
+    assert exact < 1e-2
+    assert vs_f64 < 5e-2
+    assert abs(loss.item() - l_ref.item()) < 5e-2
+    assert cos[worst] > 0.98, (worst, cos[worst])
+    for (k, v), (_, w) in zip(m.state_dict().items(), rnd.state_dict().items()):
+        if "running" in k:
+            assert torch.allclose(v.cpu().double(), w, rtol=1e-2, atol=1e-3), k
+
+
+def test_deep_bf16_full_size_properties():
+    """config 3's batch (B = 4096, T = 200, widths 64..512) in bf16: unit-norm finite embeddings,
+    finite gradients, bit-identical repeat (no atomics on the path)."""
+    from phoneme_contrast_amd.losses import SupervisedContrastiveLoss
+    from phoneme_contrast_amd.models import PhonemeNetDeep
+    torch.manual_seed(0)
+    m = PhonemeNetDeep({"embedding_dim": 128, "precision": "bf16"}).cuda().train()
+    B = 4096
+    x = torch.randn(B, 1, 40, 200, generator=torch.Generator().manual_seed(1)).cuda()
+    labels = (torch.arange(B) // 4).cuda()
+    masks = [(torch.rand(B, c) > 0.2).float() / 0.8 for c in m.hidden_dims]
+    fn = SupervisedContrastiveLoss(temperature=0.15)
+    outs = []
+    for _ in range(2):
+        m.zero_grad(set_to_none=True)
+        m.set_dropout_masks(masks)
+        e = m(x)
+        loss = fn(e, labels)
+        loss.backward()
+        outs.append((e.detach().clone(), loss.item(), [p.grad.clone() for p in m.parameters()]))
+    e, l, g = outs[0]
+    assert torch.allclose(e.norm(dim=1), torch.ones(B, device=e.device), atol=1e-5)
+    assert torch.isfinite(torch.tensor(l)) and all(torch.isfinite(t).all() for t in g)
+    e2, l2, g2 = outs[1]
+    assert torch.equal(e, e2) and l == l2 and all(torch.equal(a, b) for a, b in zip(g, g2))

@@ -126,3 +126,12 @@ def test_native_plan_geometry_on_cpu():
     assert 25e9 < p.ws_bytes < 40e9
     with pytest.raises(ValueError):
         m._plan(4, 2, 2)
+
+
+def test_deep_precision_option():
+    """PhonemeNetDeep's MI355X "precision" option: fp32 (default) | bf16 conv operands."""
+    from src.models import PhonemeNetDeep
+    assert PhonemeNetDeep({}).precision == "fp32"
+    assert PhonemeNetDeep({"precision": "bf16"})._net_config().conv_bf16 == 1
+    with pytest.raises(ValueError):
+        PhonemeNetDeep({"precision": "fp8"})
