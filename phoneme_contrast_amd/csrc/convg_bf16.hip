@@ -50,6 +50,33 @@ __device__ __forceinline__ void store_bf16(__bf16* dst, const float (&v)[N]) {
     }
 }
 
+// A operand of modes 0 / 1 / 3 packed once per launch: Wp[m][k] (bf16, tap-major k, rows padded
+// with zeros to Kp = K rounded up to 32), so a thread's k-run is one or two 16-byte loads
+__global__ __launch_bounds__(256) void pack_wbf16_kernel(const float* __restrict__ w, __bf16* __restrict__ wp,
+                                                         int mode, int cin, int cout, int KH, int KW, int par,
+                                                         int pad, int64_t M, int64_t Kp, int64_t K) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= M * Kp) return;
+    const int64_t m = i / Kp, k = i - m * Kp;
+    float v = 0.f;
+    if (k < K) {
+        const int KK = KH * KW;
+        if (mode == 0) {
+            const int tap = (int)(k / cin), c = (int)(k - (int64_t)tap * cin);
+            v = w[(m * cin + c) * KK + tap];
+        } else if (mode == 1) {
+            const int tap = (int)(k / cout), n = (int)(k - (int64_t)tap * cout);
+            v = w[((int64_t)n * cin + m) * KK + tap];
+        } else {
+            const int ph = par >> 1, pw = par & 1;
+            const int kh0 = (ph + pad) & 1, kw0 = (pw + pad) & 1, ntw = (KW - kw0 + 1) / 2;
+            const int tp = (int)(k / cout), n = (int)(k - (int64_t)tp * cout);
+            v = w[(((int64_t)n * cin + m) * KH + kh0 + 2 * (tp / ntw)) * KW + kw0 + 2 * (tp % ntw)];
+        }
+    }
+    wp[i] = (__bf16)v;
+}
+
 template <int MODE, int KH, int KW, int WM, bool FK>
 __global__ __launch_bounds__(256) void convg_bf16_kernel(ConvGArgs a) {
     constexpr int KK = KH * KW;
@@ -120,32 +147,42 @@ __global__ __launch_bounds__(256) void convg_bf16_kernel(ConvGArgs a) {
             iw0 = iw + pad;
         }
     }
-    // mode 2: pixel trackers of the two k-runs; the B row's fixed (tap, channel)
-    Pix pa{0, 0, 0}, pbx{0, 0, 0};
-    int wkh = 0, wkw = 0;
-    int64_t wco = 0;
+    // mode 2 (k-fast): a thread stages the pixel pair 2 kq2, 2 kq2 + 1 of each chunk for rows
+    // rq + 16 j (A: output channels; B: (tap, input channel) columns), written as one bf16 pair
+    constexpr int MA2 = BM / 16, MB2 = BN / 16;  // rows per thread
+    const int kq2 = tid & 15, rq = tid >> 4;
+    Pix p2{0, 0, 0};
+    int boff[MODE == 2 ? MB2 : 1], bkhw[MODE == 2 ? MB2 : 1];
     if (MODE == 2) {
-        auto init = [&](Pix& p, int64_t q) {
-            p.b = q / OHW;
-            const int64_t r = q - p.b * OHW;
-            p.oh = (int)(r / a.OW);
-            p.ow = (int)(r - (int64_t)p.oh * a.OW);
-        };
-        init(pa, k_begin + (int64_t)akg * NA);
-        init(pbx, k_begin + (int64_t)bkg * NB);
-        const int tap = (int)(brow / a.cin), c = (int)(brow - (int64_t)tap * a.cin);
-        wkh = bvalid ? tap / KW - pad : -(1 << 28);
-        wkw = tap % KW - pad;
-        wco = (int64_t)c * IHW;
+        const int64_t q = k_begin + 2 * kq2;
+        p2.b = q / OHW;
+        const int64_t r = q - p2.b * OHW;
+        p2.oh = (int)(r / a.OW);
+        p2.ow = (int)(r - (int64_t)p2.oh * a.OW);
+#pragma unroll
+        for (int i = 0; i < MB2; ++i) {
+            const int64_t jj = n0 + rq + 16 * i;
+            const int tap = (int)(jj / a.cin), c = (int)(jj - (int64_t)tap * a.cin);
+            const int kh = tap / KW - pad, kw = tap % KW - pad;
+            boff[i] = (int)(c * IHW) + kh * a.IW + kw;
+            // (kh, kw) for the bounds test; columns past N get kh far out of range (never load)
+            bkhw[i] = jj < N ? ((kh + 16384) << 16) | (kw + 16384) : 0;
+        }
     }
 
     float ra[NA], rb[NB];
+    bf16x8 rap[NA / 8];
+    const int64_t Kp = (K + KB - 1) / KB * KB;
     auto gather = [&](int chunk) {
         const int64_t kbase = k_begin + (int64_t)chunk * KB;
         if (MODE == 0 || MODE == 1 || MODE == 3) {
             // ---- A: weights of row m = arow, k-run kbase + akg*NA + j
             const int64_t k0 = kbase + akg * NA;
-            if (FK) {
+            if (a.wpack) {  // packed bf16 rows: the run is NA / 8 aligned 16-byte loads
+                const bf16x8* src = reinterpret_cast<const bf16x8*>(static_cast<const __bf16*>(a.wpack) + arow * Kp + k0);
+#pragma unroll
+                for (int q = 0; q < NA / 8; ++q) rap[q] = avalid ? src[q] : bf16x8{};
+            } else if (FK) {
                 const int tap = (int)(kbase / CK), ch0 = (int)(k0 - (int64_t)tap * CK);
                 const float* wp;
                 int64_t wst;
@@ -247,31 +284,53 @@ __global__ __launch_bounds__(256) void convg_bf16_kernel(ConvGArgs a) {
                 }
             }
         } else {
-            // ---- mode 2: A = dy[b][n = arow][pixel], B = x[b][c][pixel*s + tap] over a k-run of pixels
-            const int64_t qa = kbase + akg * NA, qb = kbase + bkg * NB;
-            Pix p = pa;
+            // ---- mode 2: A = dy[b][n][pixel], B = x[b][c][pixel*s + tap] for the thread's pixel pair
+            Pix q1 = p2;
+            pix_step(q1, 1, a.OH, a.OW);
+            const int64_t kq = kbase + 2 * kq2;
+            const bool v0 = kq < k_end, v1 = kq + 1 < k_end;
+            const int64_t pofs0 = (int64_t)p2.oh * a.OW + p2.ow, pofs1 = (int64_t)q1.oh * a.OW + q1.ow;
+            const float* dy0 = a.dy + p2.b * a.cout * OHW + pofs0;
+            const float* dy1 = a.dy + q1.b * a.cout * OHW + pofs1;
 #pragma unroll
-            for (int j = 0; j < NA; ++j) {
-                ra[j] = (avalid && qa + j < k_end) ? a.dy[(p.b * a.cout + arow) * OHW + (int64_t)p.oh * a.OW + p.ow]
-                                                   : 0.f;
-                pix_step(p, 1, a.OH, a.OW);
+            for (int j = 0; j < MA2; ++j) {
+                const int64_t n = m0 + rq + 16 * j;
+                const bool nv = n < M;
+                ra[2 * j] = (nv && v0) ? dy0[n * OHW] : 0.f;
+                ra[2 * j + 1] = (nv && v1) ? dy1[n * OHW] : 0.f;
             }
-            p = pbx;
+            const float* x0 = a.x + p2.b * a.cin * IHW + (int64_t)p2.oh * s * a.IW + p2.ow * s;
+            const float* x1 = a.x + q1.b * a.cin * IHW + (int64_t)q1.oh * s * a.IW + q1.ow * s;
+            const int ih0b = p2.oh * s, iw0b = p2.ow * s, ih1b = q1.oh * s, iw1b = q1.ow * s;
 #pragma unroll
-            for (int i = 0; i < NB; ++i) {
-                const int ih = p.oh * s + wkh, iw = p.ow * s + wkw;
-                rb[i] = (qb + i < k_end && ih >= 0 && ih < a.IH && iw >= 0 && iw < a.IW)
-                            ? a.x[p.b * a.cin * IHW + wco + (int64_t)ih * a.IW + iw]
-                            : 0.f;
-                pix_step(p, 1, a.OH, a.OW);
+            for (int i = 0; i < MB2; ++i) {
+                const int kh = (bkhw[i] >> 16) - 16384, kw = (bkhw[i] & 0xffff) - 16384;
+                const bool ok0 = v0 && ih0b + kh >= 0 && ih0b + kh < a.IH && iw0b + kw >= 0 && iw0b + kw < a.IW;
+                const bool ok1 = v1 && ih1b + kh >= 0 && ih1b + kh < a.IH && iw1b + kw >= 0 && iw1b + kw < a.IW;
+                rb[2 * i] = ok0 ? x0[boff[i]] : 0.f;
+                rb[2 * i + 1] = ok1 ? x1[boff[i]] : 0.f;
             }
-            pix_step(pa, KB, a.OH, a.OW);
-            pix_step(pbx, KB, a.OH, a.OW);
+            pix_step(p2, KB, a.OH, a.OW);
         }
     };
     auto stash = [&](int buf) {
-        store_bf16<NA>(&As[buf][am][akg * NA], ra);
-        store_bf16<NB>(&Bs[buf][bn][bkg * NB], rb);
+        if (MODE == 2) {
+            typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+            for (int j = 0; j < MA2; ++j)
+                *reinterpret_cast<bf16x2*>(&As[buf][rq + 16 * j][2 * kq2]) = bf16x2{(__bf16)ra[2 * j], (__bf16)ra[2 * j + 1]};
+#pragma unroll
+            for (int i = 0; i < MB2; ++i)
+                *reinterpret_cast<bf16x2*>(&Bs[buf][rq + 16 * i][2 * kq2]) = bf16x2{(__bf16)rb[2 * i], (__bf16)rb[2 * i + 1]};
+        } else {
+            if (a.wpack) {
+#pragma unroll
+                for (int q = 0; q < NA / 8; ++q) *reinterpret_cast<bf16x8*>(&As[buf][am][akg * NA + 8 * q]) = rap[q];
+            } else {
+                store_bf16<NA>(&As[buf][am][akg * NA], ra);
+            }
+            store_bf16<NB>(&Bs[buf][bn][bkg * NB], rb);
+        }
     };
 
     f32x16 acc[WM][WN];
@@ -362,6 +421,20 @@ int launch_convg_bf16(ConvGArgs a, hipStream_t s) {
     PCX_CHECK_ARG(nblocks < ((int64_t)1 << 31), "convg_bf16: grid too large");
     if (a.mode == 2) PCX_CHECK_ARG(a.kslice % KB == 0 && a.nslice >= 1, "convg_bf16: bad weight-gradient split");
     const bool fk = a.mode == 2 || (a.mode == 0 ? a.cin : a.cout) % KB == 0;
+    if (a.mode != 2 && a.wpack) {
+        const int64_t KK = (int64_t)a.KH * a.KW;
+        int64_t K = a.mode == 0 ? a.cin * KK : a.cout * KK;
+        if (a.mode == 3) {
+            const int kh0 = ((a.par >> 1) + a.pad) & 1, kw0 = ((a.par & 1) + a.pad) & 1;
+            K = (int64_t)a.cout * ((a.KH - kh0 + 1) / 2) * ((a.KW - kw0 + 1) / 2);
+        }
+        const int64_t Kp = (K + KB - 1) / KB * KB;
+        if (M * Kp > 0)  // (a 1x1 stride-2 class without taps has K = 0: zero output, nothing to pack)
+            pack_wbf16_kernel<<<(unsigned)ceil_div(M * Kp, 256), 256, 0, s>>>(a.w, static_cast<__bf16*>(a.wpack), a.mode,
+                                                                           a.cin, a.cout, a.KH, a.KW, a.par, a.pad, M,
+                                                                           Kp, K);
+        PCX_LAUNCH_CHECK("pack_wbf16_kernel");
+    }
     dim3 grid((unsigned)nblocks);
 #define PCX_CB(MODE_, KH_, WM_)                                                                 \
     if (a.mode == MODE_ && a.KH == KH_ && wm == WM_) {                                          \
@@ -384,13 +457,20 @@ int launch_convg_bf16(ConvGArgs a, hipStream_t s) {
 
 }  // namespace pcx
 
+namespace pcx {
+size_t convg_bf16_wpack_bytes(int mode, int cin, int cout, int k) {
+    if (mode == 2) return 0;
+    const int64_t M = mode == 0 ? cout : cin, K = (int64_t)(mode == 0 ? cin : cout) * k * k;
+    return (size_t)M * ((K + KB - 1) / KB * KB) * 2;
+}
+}  // namespace pcx
+
 // ---------------------------------------------------------------------------------------------
 // The cnn_deep convolution engine as a standalone operation (include/pcx.h: pcx_conv2d): used by
 // the kernel-level parity tests of both precisions and by micro-benchmarks.
 extern "C" size_t pcx_conv2d_workspace_bytes(int mode, int precision, int B, int cin, int cout, int OH, int OW,
                                              int k) {
-    (void)precision;
-    if (mode != 2) return 0;
+    if (mode != 2) return precision ? (pcx::convg_bf16_wpack_bytes(mode, cin, cout, k) + 255) / 256 * 256 : 0;
     pcx::ConvGArgs a{};
     a.B = B; a.cin = cin; a.cout = cout; a.OH = OH; a.OW = OW; a.KH = a.KW = k;
     int64_t ks;
@@ -417,9 +497,14 @@ extern "C" int pcx_conv2d(int mode, int precision, int B, int cin, int cout, int
     a.x = x; a.w = w; a.dy = dy; a.out = out;
     a.accumulate = accumulate;
     a.bf16 = precision;
-    if (mode != 2) return launch_convg(a, stream);
-    a.nslice = convg_nslice(a, &a.kslice);
     const size_t need = pcx_conv2d_workspace_bytes(mode, precision, B, cin, cout, OH, OW, k);
+    PCX_CHECK_ARG(need == 0 || (ws && ws_bytes >= need), "pcx_conv2d: needs %zu workspace bytes, got %zu", need,
+                  ws_bytes);
+    if (mode != 2) {
+        a.wpack = precision ? ws : nullptr;
+        return launch_convg(a, stream);
+    }
+    a.nslice = convg_nslice(a, &a.kslice);
     PCX_CHECK_ARG(ws && ws_bytes >= need, "pcx_conv2d: weight gradient needs %zu workspace bytes, got %zu", need,
                   ws_bytes);
     a.out = static_cast<float*>(ws);

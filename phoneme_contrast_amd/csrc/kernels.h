@@ -234,7 +234,9 @@ struct ConvGArgs {
     int64_t kslice;       // mode 2: pixels per slice (multiple of 32)
     int nslice;
     int bf16;             // operands rounded to bf16, float32 accumulation (convg_bf16.hip)
+    void* wpack;          // bf16, modes 0/1/3: scratch for the weights packed as [M][K rounded to 32]
 };
+size_t convg_bf16_wpack_bytes(int mode, int cin, int cout, int k);
 int launch_convg(ConvGArgs a, hipStream_t s);
 int launch_convg_bf16(ConvGArgs a, hipStream_t s);
 int convg_nslice(const ConvGArgs& a, int64_t* kslice);
