@@ -340,22 +340,50 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
     return red[0] + red[1] + red[2] + red[3];
 }
 
+// Walk of the elements e = tid + 256 j of the planes (b, c) for b in [b0, b1): every lane busy
+// whatever the plane size (the deep net's planes go down to 3 x 13 pixels), no per-element division.
+struct PlaneWalk {
+    int b, p, db, dp;
+    __device__ __forceinline__ PlaneWalk(int b0, int P) {
+        b = b0 + (int)threadIdx.x / P;
+        p = (int)threadIdx.x % P;
+        db = 256 / P;
+        dp = 256 % P;
+    }
+    __device__ __forceinline__ void next(int P) {
+        b += db;
+        p += dp;
+        if (p >= P) { p -= P; ++b; }
+    }
+};
+
 // Forward BN partials of y [B][C][P]: block (c, slice) -> (sum, M2 about the block mean, count),
 // accumulated in float64 about a shift (first element) — consumed by launch_bn_fwd_finalize.
-__global__ __launch_bounds__(256) void chan_stats_kernel(const float* __restrict__ y, int B, int C, int64_t P,
+__global__ __launch_bounds__(256) void chan_stats_kernel(const float* __restrict__ y, int B, int C, int64_t P64,
                                                          int bps, float* part0, float* part1, float* partn) {
     __shared__ double red[4];
     const int c = blockIdx.x, sl = blockIdx.y, nsl = gridDim.y;
     const int b0 = sl * bps, b1 = min(B, b0 + bps);
+    const int P = (int)P64;
     const double K = b0 < B ? (double)y[((int64_t)b0 * C + c) * P] : 0.0;
     double s1 = 0.0, s2 = 0.0;
-    for (int b = b0; b < b1; ++b) {
-        const float* yc = y + ((int64_t)b * C + c) * P;
-        for (int64_t p = threadIdx.x; p < P; p += 256) {
-            const double d = (double)yc[p] - K;
-            s1 += d;
-            s2 += d * d;
+    PlaneWalk w(b0, P);
+    while (w.b < b1) {  // 4 independent loads in flight per thread
+        float v[4];
+        bool ok[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            ok[u] = w.b < b1;
+            v[u] = ok[u] ? y[((int64_t)w.b * C + c) * P + w.p] : 0.f;
+            w.next(P);
         }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (ok[u]) {
+                const double d = (double)v[u] - K;
+                s1 += d;
+                s2 += d * d;
+            }
     }
     s1 = block_sum(s1, red);
     s2 = block_sum(s2, red);
@@ -373,25 +401,44 @@ __global__ __launch_bounds__(256) void bwd_prep_kernel(BwdPrepArgs a) {
     __shared__ double red[4];
     const int c = blockIdx.x, sl = blockIdx.y, nsl = gridDim.y;
     const int b0 = sl * a.bps, b1 = min(a.B, b0 + a.bps);
+    const int P = (int)a.P;
     const float4 mc = a.mask_cf ? a.mask_cf[c] : make_float4(1.f, 0.f, 0.f, 1.f);
     const float4 c1 = a.cf1 ? a.cf1[c] : make_float4(0.f, 0.f, 0.f, 0.f);
     const float4 c2 = a.cf2 ? a.cf2[c] : make_float4(0.f, 0.f, 0.f, 0.f);
     double sg = 0.0, sx1 = 0.0, sx2 = 0.0;
-    for (int b = b0; b < b1; ++b) {
-        const int64_t o = ((int64_t)b * a.C + c) * a.P;
-        const float dr = a.drop ? a.drop[(int64_t)b * a.C + c] : 1.f;
-        for (int64_t p = threadIdx.x; p < a.P; p += 256) {
-            float g = a.d[o + p];
-            if (a.d2) g += a.d2[o + p];
+    PlaneWalk w(b0, P);
+    while (w.b < b1) {  // 2 elements per iteration: their loads are issued together
+        int64_t o[2], bc[2];
+        bool ok[2];
+        float g[2], m[2], y1v[2], y2v[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            ok[u] = w.b < b1;
+            bc[u] = (int64_t)(ok[u] ? w.b : b0) * a.C + c;
+            o[u] = bc[u] * P + (ok[u] ? w.p : 0);
+            w.next(P);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            g[u] = a.d[o[u]];
+            if (a.d2) g[u] += a.d2[o[u]];
+            m[u] = a.mask_mode != MASK_NONE ? a.mask_src[o[u]] : 0.f;
+            y1v[u] = a.y1 ? a.y1[o[u]] : 0.f;
+            y2v[u] = a.y2 ? a.y2[o[u]] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            if (!ok[u]) continue;
+            float gv = g[u];
             if (a.mask_mode == MASK_OUT) {
-                g = a.mask_src[o + p] > 0.f ? g : 0.f;
+                gv = m[u] > 0.f ? gv : 0.f;
             } else if (a.mask_mode == MASK_BN) {
-                g = fmaf(a.mask_src[o + p], mc.x, mc.y) > 0.f ? g * dr : 0.f;
+                gv = fmaf(m[u], mc.x, mc.y) > 0.f ? gv * (a.drop ? a.drop[bc[u]] : 1.f) : 0.f;
             }
-            a.g[o + p] = g;
-            sg += (double)g;
-            if (a.y1) sx1 += (double)g * (double)((a.y1[o + p] - c1.z) * c1.w);
-            if (a.y2) sx2 += (double)g * (double)((a.y2[o + p] - c2.z) * c2.w);
+            a.g[o[u]] = gv;
+            sg += (double)gv;
+            if (a.y1) sx1 += (double)gv * (double)((y1v[u] - c1.z) * c1.w);
+            if (a.y2) sx2 += (double)gv * (double)((y2v[u] - c2.z) * c2.w);
         }
     }
     sg = block_sum(sg, red);
