@@ -230,7 +230,17 @@ __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
 #pragma unroll
             for (int j = 0; j < NA; ++j) {
                 const int64_t n = m0 + colq + 16 * j;
-                ra[j] = (kval && n < M) ? a.dy[(pb * a.cout + n) * OHW + pofs] : 0.f;
+                float v = 0.f;
+                if (kval && n < M) {
+                    const int64_t o = (pb * a.cout + n) * OHW + pofs;
+                    if (!FK) {  // mode 2: FK = false selects the BN-fused dy (launch_convg)
+                        const float4 k = a.bn_cf[n];
+                        v = k.x * (a.bn_g[o] - k.y - (a.bn_y[o] - k.w) * k.z);
+                    } else {
+                        v = a.dy[o];
+                    }
+                }
+                ra[j] = v;
             }
             const float* xb = a.x + pb * a.cin * IHW;
             const int ihb = poh * s, iwb = pow_ * s;
@@ -740,7 +750,8 @@ int launch_convg(ConvGArgs a, hipStream_t s) {
     if (a.mode == 2) PCX_CHECK_ARG(a.kslice % KC == 0 && a.nslice >= 1, "convg: bad weight-gradient split");
     dim3 grid((unsigned)nblocks);
     // tap-uniform K chunks: the K channel count (cin forward, cout data gradient) a multiple of 16
-    const bool fk = a.mode == 2 || (a.mode == 0 ? a.cin : a.cout) % KC == 0;
+    // (mode 2 reuses the flag: false = dy computed as the BN backward of (bn_g, bn_y) while staging)
+    const bool fk = a.mode == 2 ? a.bn_g == nullptr : (a.mode == 0 ? a.cin : a.cout) % KC == 0;
 #define PCX_CG(MODE_, KH_, WM_)                                                                      \
     if (a.mode == MODE_ && a.KH == KH_ && wm == WM_) {                                               \
         if (fk) convg_kernel<MODE_, KH_, KH_, WM_, 2, true><<<grid, 256, 0, s>>>(a);                 \

@@ -296,8 +296,15 @@ __global__ __launch_bounds__(256) void convg_bf16_kernel(ConvGArgs a) {
             for (int j = 0; j < MA2; ++j) {
                 const int64_t n = m0 + rq + 16 * j;
                 const bool nv = n < M;
-                ra[2 * j] = (nv && v0) ? dy0[n * OHW] : 0.f;
-                ra[2 * j + 1] = (nv && v1) ? dy1[n * OHW] : 0.f;
+                if (!FK) {  // mode 2: FK = false selects dy = BN backward of (g, y), computed here
+                    const float4 kc = a.bn_cf[nv ? n : 0];
+                    const int64_t o0 = p2.b * a.cout * OHW + pofs0 + n * OHW, o1 = q1.b * a.cout * OHW + pofs1 + n * OHW;
+                    ra[2 * j] = (nv && v0) ? kc.x * (a.bn_g[o0] - kc.y - (a.bn_y[o0] - kc.w) * kc.z) : 0.f;
+                    ra[2 * j + 1] = (nv && v1) ? kc.x * (a.bn_g[o1] - kc.y - (a.bn_y[o1] - kc.w) * kc.z) : 0.f;
+                } else {
+                    ra[2 * j] = (nv && v0) ? dy0[n * OHW] : 0.f;
+                    ra[2 * j + 1] = (nv && v1) ? dy1[n * OHW] : 0.f;
+                }
             }
             const float* x0 = a.x + p2.b * a.cin * IHW + (int64_t)p2.oh * s * a.IW + p2.ow * s;
             const float* x1 = a.x + q1.b * a.cin * IHW + (int64_t)q1.oh * s * a.IW + q1.ow * s;
@@ -420,7 +427,8 @@ int launch_convg_bf16(ConvGArgs a, hipStream_t s) {
     const int64_t nblocks = mt * nt * (a.mode == 2 ? a.nslice : 1);
     PCX_CHECK_ARG(nblocks < ((int64_t)1 << 31), "convg_bf16: grid too large");
     if (a.mode == 2) PCX_CHECK_ARG(a.kslice % KB == 0 && a.nslice >= 1, "convg_bf16: bad weight-gradient split");
-    const bool fk = a.mode == 2 || (a.mode == 0 ? a.cin : a.cout) % KB == 0;
+    // (mode 2 reuses the flag: false = dy computed as the BN backward of (bn_g, bn_y) while staging)
+    const bool fk = a.mode == 2 ? a.bn_g == nullptr : (a.mode == 0 ? a.cin : a.cout) % KB == 0;
     if (a.mode != 2 && a.wpack) {
         const int64_t KK = (int64_t)a.KH * a.KW;
         int64_t K = a.mode == 0 ? a.cin * KK : a.cout * KK;

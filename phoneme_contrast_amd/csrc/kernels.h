@@ -235,6 +235,11 @@ struct ConvGArgs {
     int nslice;
     int bf16;             // operands rounded to bf16, float32 accumulation (convg_bf16.hip)
     void* wpack;          // bf16, modes 0/1/3: scratch for the weights packed as [M][K rounded to 32]
+    // mode 2 only: dy computed while staging as BN backward of (bn_g, bn_y) with per-channel
+    // {a, mb, mgi, mean} (dy = a (g - mb - (y - mean) mgi)); `dy` is then unused
+    const float* bn_g;
+    const float* bn_y;
+    const float4* bn_cf;
 };
 size_t convg_bf16_wpack_bytes(int mode, int cin, int cout, int k);
 int launch_convg(ConvGArgs a, hipStream_t s);
