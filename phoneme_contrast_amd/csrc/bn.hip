@@ -21,9 +21,11 @@ __device__ __forceinline__ double block_sum_d(double v, double* red) {
     return r;
 }
 
-// one block per channel
-__global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(BnFwdArgs a) {
-    __shared__ double red[256];
+// one block per channel, 1024 threads, 4 independent loads in flight per thread: the partial
+// counts reach 64000 per channel (cnn_small L1/L2), and a 256-thread loop with one outstanding load
+// per iteration was memory-latency bound (0.1-0.3 ms per launch)
+__global__ __launch_bounds__(1024) void bn_fwd_finalize_kernel(BnFwdArgs a) {
+    __shared__ double red[1024];
     const int c = blockIdx.x;
     const float g = a.gamma ? a.gamma[c] : 1.f;
     const float be = a.beta ? a.beta[c] : 0.f;
@@ -40,21 +42,46 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(BnFwdArgs a) {
     const float* s0 = a.part0 + (int64_t)c * a.nblk;
     const float* s1 = a.part1 + (int64_t)c * a.nblk;
     double sum = 0.0, n = 0.0;
-    for (int i = threadIdx.x; i < a.nblk; i += blockDim.x) {
-        sum += (double)s0[i];
-        n += (double)a.partn[i];
+    {
+        const int st = blockDim.x;
+        int i = threadIdx.x;
+        for (; i + 3 * st < a.nblk; i += 4 * st) {
+            const float x0 = s0[i], x1 = s0[i + st], x2 = s0[i + 2 * st], x3 = s0[i + 3 * st];
+            const float n0 = a.partn[i], n1 = a.partn[i + st], n2 = a.partn[i + 2 * st], n3 = a.partn[i + 3 * st];
+            sum += (double)x0 + (double)x1 + (double)x2 + (double)x3;
+            n += (double)n0 + (double)n1 + (double)n2 + (double)n3;
+        }
+        for (; i < a.nblk; i += st) {
+            sum += (double)s0[i];
+            n += (double)a.partn[i];
+        }
     }
     sum = block_sum_d(sum, red);
     n = block_sum_d(n, red);
     const double mean = sum / n;
     // M2 = sum_b [M2_b + n_b (mean_b - mean)^2]
     double m2 = 0.0;
-    for (int i = threadIdx.x; i < a.nblk; i += blockDim.x) {
-        double nb = (double)a.partn[i];
-        if (nb > 0) {
-            double d = (double)s0[i] / nb - mean;
-            m2 += (double)s1[i] + nb * d * d;
+    {
+        const int st = blockDim.x;
+        int i = threadIdx.x;
+        auto term = [&](float sv, float mv, float nv) {
+            const double nb = (double)nv;
+            if (nb <= 0) return 0.0;
+            const double d = (double)sv / nb - mean;
+            return (double)mv + nb * d * d;
+        };
+        for (; i + 3 * st < a.nblk; i += 4 * st) {
+            float sv[4], mv[4], nv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                sv[u] = s0[i + u * st];
+                mv[u] = s1[i + u * st];
+                nv[u] = a.partn[i + u * st];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) m2 += term(sv[u], mv[u], nv[u]);
         }
+        for (; i < a.nblk; i += st) m2 += term(s0[i], s1[i], a.partn[i]);
     }
     m2 = block_sum_d(m2, red);
     if (threadIdx.x == 0) {
@@ -71,8 +98,8 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(BnFwdArgs a) {
     }
 }
 
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(BnBwdArgs a) {
-    __shared__ double red[256];
+__global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(BnBwdArgs a) {
+    __shared__ double red[1024];
     const int c = blockIdx.x;
     const float* s0 = a.part0 + (int64_t)c * a.nblk;
     const float* s1 = a.part1 + (int64_t)c * a.nblk;
@@ -97,13 +124,13 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(BnBwdArgs a) {
 }  // namespace
 
 int launch_bn_fwd_finalize(BnFwdArgs a, hipStream_t s) {
-    bn_fwd_finalize_kernel<<<a.C, 256, 0, s>>>(a);
+    bn_fwd_finalize_kernel<<<a.C, a.train ? 1024 : 64, 0, s>>>(a);
     PCX_LAUNCH_CHECK("bn_fwd_finalize_kernel");
     return PCX_OK;
 }
 
 int launch_bn_bwd_finalize(BnBwdArgs a, hipStream_t s) {
-    bn_bwd_finalize_kernel<<<a.C, 256, 0, s>>>(a);
+    bn_bwd_finalize_kernel<<<a.C, 1024, 0, s>>>(a);
     PCX_LAUNCH_CHECK("bn_bwd_finalize_kernel");
     return PCX_OK;
 }

@@ -383,13 +383,36 @@ __global__ __launch_bounds__(256) void wgrad1_kernel(Wgrad1Args a) {
     }
 }
 
-__global__ void sum_slices_kernel(const float* __restrict__ part, int nslice, int64_t n,
-                                  float* __restrict__ out) {
-    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= n) return;
+// out[e] = sum_k part[k][e]: a block owns 32 consecutive outputs; its 8 thread groups sum slices
+// g, g + 8, ... (coalesced 128-byte rows), then the 8 group sums are added in a fixed order
+// (deterministic; the previous one-thread-per-output form left most of the chip idle for the
+// small weight tensors: 36 blocks for a 32 x 32 x 9 gradient)
+__global__ __launch_bounds__(256) void sum_slices_kernel(const float* __restrict__ part, int nslice, int64_t n,
+                                                         float* __restrict__ out) {
+    __shared__ float red[8][33];
+    const int o = threadIdx.x & 31, g = threadIdx.x >> 5;
+    const int64_t e = (int64_t)blockIdx.x * 32 + o;
     float s = 0.f;
-    for (int k = 0; k < nslice; ++k) s += part[(int64_t)k * n + e];
-    out[e] = s;
+    if (e < n) {
+        int k = g;
+        for (; k + 24 < nslice; k += 32) {
+            const float a0 = part[(int64_t)k * n + e], a1 = part[(int64_t)(k + 8) * n + e];
+            const float a2 = part[(int64_t)(k + 16) * n + e], a3 = part[(int64_t)(k + 24) * n + e];
+            s += a0;
+            s += a1;
+            s += a2;
+            s += a3;
+        }
+        for (; k < nslice; k += 8) s += part[(int64_t)k * n + e];
+    }
+    red[g][o] = s;
+    __syncthreads();
+    if (g == 0 && e < n) {
+        float t = red[0][o];
+#pragma unroll
+        for (int q = 1; q < 8; ++q) t += red[q][o];
+        out[e] = t;
+    }
 }
 
 __global__ void pack_fwd_kernel(const float* __restrict__ w, float* __restrict__ wp, int cout, int cin) {
@@ -460,7 +483,7 @@ int launch_wgrad1(Wgrad1Args a, hipStream_t s) {
 }
 
 int launch_sum_slices(const float* part, int nslice, int64_t n, float* out, hipStream_t s) {
-    sum_slices_kernel<<<ceil_div(n, 256), 256, 0, s>>>(part, nslice, n, out);
+    sum_slices_kernel<<<ceil_div(n, 32), 256, 0, s>>>(part, nslice, n, out);
     PCX_LAUNCH_CHECK("sum_slices_kernel");
     return PCX_OK;
 }
