@@ -135,6 +135,15 @@ __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
             const int64_t k = kbase + kq;
             const int tap = (int)(k / CK), ch = (int)(k - (int64_t)tap * CK);
             const bool kv = k < K;
+            if (a.wpack) {  // packed [M][K16] rows: 16 lanes read 64 contiguous bytes
+                const float* wp = static_cast<const float*>(a.wpack) + k;
+                const int64_t Kp = (K + KC - 1) / KC * KC;
+#pragma unroll
+                for (int j = 0; j < NA; ++j) {
+                    const int64_t m = m0 + colq + 16 * j;
+                    ra[j] = m < M ? wp[m * Kp] : 0.f;
+                }
+            } else
 #pragma unroll
             for (int j = 0; j < NA; ++j) {
                 const int64_t m = m0 + colq + 16 * j;
@@ -721,6 +730,40 @@ int convg_nslice(const ConvGArgs& a, int64_t* kslice) {
     return (int)((K + ks - 1) / ks);
 }
 
+namespace {
+// fp32 A operand of modes 0 / 1 / 3 packed once per launch as [M][K rounded to 16] (tap-major k)
+__global__ __launch_bounds__(256) void pack_wf32_kernel(const float* __restrict__ w, float* __restrict__ wp, int mode,
+                                                        int cin, int cout, int KH, int KW, int par, int pad, int64_t M,
+                                                        int64_t Kp, int64_t K) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= M * Kp) return;
+    const int64_t m = i / Kp, k = i - m * Kp;
+    float v = 0.f;
+    if (k < K) {
+        const int KK = KH * KW;
+        if (mode == 0) {
+            const int tap = (int)(k / cin), c = (int)(k - (int64_t)tap * cin);
+            v = w[(m * cin + c) * KK + tap];
+        } else if (mode == 1) {
+            const int tap = (int)(k / cout), n = (int)(k - (int64_t)tap * cout);
+            v = w[((int64_t)n * cin + m) * KK + tap];
+        } else {
+            const int ph = par >> 1, pw = par & 1;
+            const int kh0 = (ph + pad) & 1, kw0 = (pw + pad) & 1, ntw = (KW - kw0 + 1) / 2;
+            const int tp = (int)(k / cout), n = (int)(k - (int64_t)tp * cout);
+            v = w[(((int64_t)n * cin + m) * KH + kh0 + 2 * (tp / ntw)) * KW + kw0 + 2 * (tp % ntw)];
+        }
+    }
+    wp[i] = v;
+}
+}  // namespace
+
+size_t convg_wpack_bytes(int mode, int cin, int cout, int k) {
+    if (mode == 2) return 0;
+    const int64_t M = mode == 0 ? cout : cin, K = (int64_t)(mode == 0 ? cin : cout) * k * k;
+    return (size_t)M * ((K + KC - 1) / KC * KC) * 4;
+}
+
 int launch_convg(ConvGArgs a, hipStream_t s) {
     PCX_CHECK_ARG(a.stride == 1 || a.stride == 2, "convg: stride %d unsupported", a.stride);
     PCX_CHECK_ARG(a.B > 0 && a.cin > 0 && a.cout > 0, "convg: empty tensor");
@@ -752,6 +795,20 @@ int launch_convg(ConvGArgs a, hipStream_t s) {
     // tap-uniform K chunks: the K channel count (cin forward, cout data gradient) a multiple of 16
     // (mode 2 reuses the flag: false = dy computed as the BN backward of (bn_g, bn_y) while staging)
     const bool fk = a.mode == 2 ? a.bn_g == nullptr : (a.mode == 0 ? a.cin : a.cout) % KC == 0;
+    if (a.mode != 2 && a.wpack) {
+        const int64_t KK = (int64_t)a.KH * a.KW;
+        int64_t K = a.mode == 0 ? a.cin * KK : a.cout * KK;
+        if (a.mode == 3) {
+            const int kh0 = ((a.par >> 1) + a.pad) & 1, kw0 = ((a.par & 1) + a.pad) & 1;
+            K = (int64_t)a.cout * ((a.KH - kh0 + 1) / 2) * ((a.KW - kw0 + 1) / 2);
+        }
+        const int64_t Kp = (K + KC - 1) / KC * KC;
+        if (M * Kp > 0)
+            pack_wf32_kernel<<<(unsigned)ceil_div(M * Kp, 256), 256, 0, s>>>(a.w, static_cast<float*>(a.wpack), a.mode,
+                                                                              a.cin, a.cout, a.KH, a.KW, a.par, a.pad,
+                                                                              M, Kp, K);
+        PCX_LAUNCH_CHECK("pack_wf32_kernel");
+    }
 #define PCX_CG(MODE_, KH_, WM_)                                                                      \
     if (a.mode == MODE_ && a.KH == KH_ && wm == WM_) {                                               \
         if (fk) convg_kernel<MODE_, KH_, KH_, WM_, 2, true><<<grid, 256, 0, s>>>(a);                 \

@@ -478,7 +478,9 @@ size_t convg_bf16_wpack_bytes(int mode, int cin, int cout, int k) {
 // the kernel-level parity tests of both precisions and by micro-benchmarks.
 extern "C" size_t pcx_conv2d_workspace_bytes(int mode, int precision, int B, int cin, int cout, int OH, int OW,
                                              int k) {
-    if (mode != 2) return precision ? (pcx::convg_bf16_wpack_bytes(mode, cin, cout, k) + 255) / 256 * 256 : 0;
+    if (mode != 2)
+        return ((precision ? pcx::convg_bf16_wpack_bytes(mode, cin, cout, k) : pcx::convg_wpack_bytes(mode, cin, cout, k)) +
+                255) / 256 * 256;
     pcx::ConvGArgs a{};
     a.B = B; a.cin = cin; a.cout = cout; a.OH = OH; a.OW = OW; a.KH = a.KW = k;
     int64_t ks;
@@ -509,7 +511,7 @@ extern "C" int pcx_conv2d(int mode, int precision, int B, int cin, int cout, int
     PCX_CHECK_ARG(need == 0 || (ws && ws_bytes >= need), "pcx_conv2d: needs %zu workspace bytes, got %zu", need,
                   ws_bytes);
     if (mode != 2) {
-        a.wpack = precision ? ws : nullptr;
+        a.wpack = ws;
         return launch_convg(a, stream);
     }
     a.nslice = convg_nslice(a, &a.kslice);

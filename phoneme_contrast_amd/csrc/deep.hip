@@ -36,7 +36,7 @@ struct DeepPlan {
     int H0, W0, H1, W1;
     size_t y0, a0, cf0, cfb0, dz0, mparg;
     size_t wpk, identw;           // packed 3x3 weights of a routed conv; identity BN coefficients
-    size_t wpk16;                 // bf16: packed GEMM weights of the current conv (convg_bf16.hip)
+    size_t wpk16;                 // packed GEMM weights of the current general-engine conv
     int cmax;
     DeepBlock blk[4];
     size_t g, dyA, dyB, dd, hdz;   // backward scratch
@@ -151,17 +151,20 @@ int build_deep(Plan& p) {
     d.identw = p.carve("identw", (size_t)cmax * 16);
     d.cmax = cmax;
     d.wpk = p.carve("wpack", std::max<size_t>(wpk, 1) * 4);
-    if (d.bf16) {
-        size_t w16 = convg_bf16_wpack_bytes(0, 1, C0, 7);
+    {  // packed GEMM weights of the general engine (fp32 or bf16 rows)
+        auto need = [&](int mode, int ci, int co, int kk) {
+            return d.bf16 ? convg_bf16_wpack_bytes(mode, ci, co, kk) : convg_wpack_bytes(mode, ci, co, kk);
+        };
+        size_t w16 = need(0, 1, C0, 7);
         for (int i = 0; i < 4; ++i) {
             const DeepBlock& k = d.blk[i];
             for (int mode = 0; mode < 2; ++mode) {
-                w16 = std::max(w16, convg_bf16_wpack_bytes(mode, k.cin, k.cout, 3));
-                w16 = std::max(w16, convg_bf16_wpack_bytes(mode, k.cout, k.cout, 3));
-                if (k.sc) w16 = std::max(w16, convg_bf16_wpack_bytes(mode, k.cin, k.cout, 1));
+                w16 = std::max(w16, need(mode, k.cin, k.cout, 3));
+                w16 = std::max(w16, need(mode, k.cout, k.cout, 3));
+                if (k.sc) w16 = std::max(w16, need(mode, k.cin, k.cout, 1));
             }
         }
-        d.wpk16 = p.carve("wpack16", w16);
+        d.wpk16 = p.carve("wpack_g", w16);
     }
     d.ia = pidx;
     d.ip = pidx + (p.cfg.use_attention ? 2 : 0);
@@ -233,7 +236,7 @@ int conv_bn_fwd(const Ctx& c, const char* label, int layer, const float* x, int 
         a.KH = a.KW = k; a.stride = stride; a.pad = pad;
         a.x = x; a.w = wgt; a.out = y;
         a.bf16 = c.d.bf16;
-        a.wpack = c.d.bf16 ? c.w<void>(c.d.wpk16) : nullptr;
+        a.wpack = c.w<void>(c.d.wpk16);
         Scope sc(&c.p.prof, c.s, label, layer);
         RC(launch_convg(a, c.s));
     }
@@ -329,7 +332,7 @@ int conv_dgrad(const Ctx& c, int layer, const float* dy, int cout, int OH, int O
     a.KH = a.KW = k; a.stride = stride; a.pad = pad;
     a.w = wgt; a.dy = dy; a.out = dx; a.accumulate = accumulate;
     a.bf16 = c.d.bf16;
-    a.wpack = c.d.bf16 ? c.w<void>(c.d.wpk16) : nullptr;
+    a.wpack = c.w<void>(c.d.wpk16);
     Scope sc(&c.p.prof, c.s, "conv_dgrad", layer);
     return launch_convg(a, c.s);
 }

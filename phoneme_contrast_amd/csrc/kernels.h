@@ -234,7 +234,8 @@ struct ConvGArgs {
     int64_t kslice;       // mode 2: pixels per slice (multiple of 32)
     int nslice;
     int bf16;             // operands rounded to bf16, float32 accumulation (convg_bf16.hip)
-    void* wpack;          // bf16, modes 0/1/3: scratch for the weights packed as [M][K rounded to 32]
+    void* wpack;          // modes 0/1/3 (optional): scratch for the weights packed as GEMM rows
+                          // (fp32 [M][K rounded to 16]; bf16 [M][K rounded to 32])
     // mode 2 only: dy computed while staging as BN backward of (bn_g, bn_y) with per-channel
     // {a, mb, mgi, mean} (dy = a (g - mb - (y - mean) mgi)); `dy` is then unused
     const float* bn_g;
@@ -242,6 +243,7 @@ struct ConvGArgs {
     const float4* bn_cf;
 };
 size_t convg_bf16_wpack_bytes(int mode, int cin, int cout, int k);
+size_t convg_wpack_bytes(int mode, int cin, int cout, int k);  // fp32 packed weights (wpack)
 int launch_convg(ConvGArgs a, hipStream_t s);
 int launch_convg_bf16(ConvGArgs a, hipStream_t s);
 int convg_nslice(const ConvGArgs& a, int64_t* kslice);

@@ -1,5 +1,5 @@
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_deep_gpu.py tests/test_deep_bf16_gpu.py -x -q --timeout 200 --timeout-method thread > gpurun_out/t.log 2>&1; tail -2 gpurun_out/t.log
+timeout -k 10 300 python -u -m pytest tests/test_conv2d_gpu.py tests/test_deep_gpu.py tests/test_deep_bf16_gpu.py -x -q --timeout 200 --timeout-method thread > gpurun_out/t.log 2>&1; tail -2 gpurun_out/t.log
 for pr in fp32 bf16; do
 timeout -k 10 300 python bench.py --model cnn_deep --precision $pr --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/bench_deep_$pr.json 2> gpurun_out/bench_deep_$pr.err
 python3 -c "
