@@ -786,7 +786,9 @@ int launch_convg(ConvGArgs a, hipStream_t s) {
         M = a.cin;
         N = a.B * (int64_t)((a.IH - (a.par >> 1) + 1) / 2) * ((a.IW - (a.par & 1) + 1) / 2);
     } else { M = a.cout; N = (int64_t)a.cin * a.KH * a.KW; }
-    const int wm = M >= 128 ? 2 : 1, wn = 2;
+    // narrow weight-gradient GEMMs (stem 7x7 of one channel: N = 49; 1x1 shortcuts of <= 64
+    // channels) take 64-column tiles: a 128-column tile would multiply mostly padding
+    const int wm = M >= 128 ? 2 : 1, wn = (a.mode == 2 && N <= 64 && (a.KH == 7 || a.KH == 1)) ? 1 : 2;
     const int64_t mt = ceil_div(M, 64 * wm), nt = ceil_div(N, 64 * wn);
     const int64_t nblocks = mt * nt * (a.mode == 2 ? a.nslice : 1);
     PCX_CHECK_ARG(nblocks < ((int64_t)1 << 31), "convg: grid too large");
@@ -808,6 +810,17 @@ int launch_convg(ConvGArgs a, hipStream_t s) {
                                                                               a.cin, a.cout, a.KH, a.KW, a.par, a.pad,
                                                                               M, Kp, K);
         PCX_LAUNCH_CHECK("pack_wf32_kernel");
+    }
+    if (wn == 1) {
+#define PCX_CG1(KH_, WM_)                                                                            \
+        if (a.KH == KH_ && wm == WM_) {                                                              \
+            if (fk) convg_kernel<2, KH_, KH_, WM_, 1, true><<<grid, 256, 0, s>>>(a);                 \
+            else convg_kernel<2, KH_, KH_, WM_, 1, false><<<grid, 256, 0, s>>>(a);                   \
+            PCX_LAUNCH_CHECK("convg_kernel");                                                        \
+            return PCX_OK;                                                                           \
+        }
+        PCX_CG1(1, 1) PCX_CG1(1, 2) PCX_CG1(7, 1) PCX_CG1(7, 2)
+#undef PCX_CG1
     }
 #define PCX_CG(MODE_, KH_, WM_)                                                                      \
     if (a.mode == MODE_ && a.KH == KH_ && wm == WM_) {                                               \
