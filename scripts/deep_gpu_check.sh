@@ -1,3 +1,4 @@
+# GPU-box check: deep parity tests (fp32 + bf16 + conv2d engine) and one cnn_deep bench per precision
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_conv2d_gpu.py tests/test_deep_gpu.py tests/test_deep_bf16_gpu.py -x -q --timeout 200 --timeout-method thread > gpurun_out/t.log 2>&1; tail -2 gpurun_out/t.log
 for pr in fp32 bf16; do

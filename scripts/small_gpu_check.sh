@@ -1,3 +1,4 @@
+# GPU-box check: the full -m gpu suite and one default cnn_small bench line with per-kernel times
 mkdir -p gpurun_out
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/t.log 2>&1; tail -2 gpurun_out/t.log
 timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench.json 2> gpurun_out/bench.err
