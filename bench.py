@@ -151,6 +151,36 @@ def cpu_baseline(budget_s=12.0, B=64, T=200):
                       f"float32 torch-CPU restatement oracle/torch_port.py, {threads} threads"}
 
 
+def measure_peaks(dev):
+    """Achievable peaks on this box (report against vendor and measured): HBM by a
+    2 GiB device-to-device copy, fp32 matrix rate by an 8192^3 torch.mm (rocBLAS / hipBLASLt
+    fp32 GEMM on the MFMA).  Timed with HIP events after a warm-up; ~1 s in total."""
+    n = 1 << 29  # floats: 2 GiB per buffer
+    a = torch.empty(n, device=dev)
+    b = torch.empty(n, device=dev)
+    b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(5):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    hbm = 5 * 2 * 4 * n / (e0.elapsed_time(e1) / 1000.0) / 1e9
+    del a, b
+    m = 8192
+    x = torch.randn(m, m, device=dev)
+    y = torch.randn(m, m, device=dev)
+    torch.mm(x, y)
+    e0.record()
+    for _ in range(5):
+        torch.mm(x, y)
+    e1.record()
+    torch.cuda.synchronize()
+    gemm = 5 * 2 * m ** 3 / (e0.elapsed_time(e1) / 1000.0) / 1e12
+    return {"hbm_copy_GBps": round(hbm, 1), "fp32_gemm_TFLOPs": round(gemm, 1),
+            "note": "measured on this GPU: 2 GiB D2D copy (read + write bytes); torch.mm fp32 8192^3"}
+
+
 def load_pmc(label):
     """HBM bytes per launch of `label` from a committed rocprofv3 --pmc summary, or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -176,6 +206,7 @@ def main():
                     help="cnn_deep conv operand precision (bf16: float32 accumulation, float32 elsewhere)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--no-peaks", action="store_true", help="skip the measured-peak probes")
     args = ap.parse_args()
 
     from phoneme_contrast_amd import distributed as ddp
@@ -286,6 +317,18 @@ def main():
                  "mfma_fraction": round(sf / (el / args.steps) / (peak * 1e12), 4),
                  "hbm_fraction": round(sb / (el / args.steps) / (HBM_PEAK_GBS * 1e9), 4)}
 
+    peaks = None
+    if rank == 0 and not args.no_peaks:
+        try:
+            peaks = measure_peaks(dev)
+            if roof is not None:
+                meas = peaks["fp32_gemm_TFLOPs"] if roof["bound"] == "mfma" and not bf16 else (
+                    peaks["hbm_copy_GBps"] if roof["bound"] == "hbm" else None)
+                if meas:
+                    roof["frac_of_measured_peak"] = round(roof["achieved"] / meas, 4)
+        except Exception as exc:  # pragma: no cover - reported, never fatal
+            peaks = {"error": repr(exc)}
+
     cpu = None
     if world == 1 and not args.no_cpu_baseline and not deep:
         try:
@@ -313,6 +356,7 @@ def main():
         "roofline": roof,
         "step_roofline": step_roof,
         "cpu_baseline": cpu,
+        "measured_peaks": peaks,
         "kernels": kernels,
         "final_loss": round(final_loss, 5),
     }
