@@ -193,7 +193,7 @@ __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
             };
             if (FK) {
                 const int tap = (int)(kbase / CK), c0 = (int)(kbase - (int64_t)tap * CK);
-                int oh, ow;
+                int oh = 0, ow = 0;
                 const bool ok = bvalid && src(tap, oh, ow);
                 const float* p = a.dy + xbase + (int64_t)(c0 + brow) * OHW + (int64_t)oh * a.OW + ow;
 #pragma unroll
@@ -205,7 +205,7 @@ __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
                     float v = 0.f;
                     if (bvalid && kb < K) {
                         const int tap = (int)(kb / CK), nn = (int)(kb - (int64_t)tap * CK);
-                        int oh, ow;
+                        int oh = 0, ow = 0;
                         if (src(tap, oh, ow)) v = a.dy[xbase + ((int64_t)nn * a.OH + oh) * a.OW + ow];
                     }
                     rb[i] = v;

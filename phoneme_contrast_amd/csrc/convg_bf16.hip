@@ -20,7 +20,7 @@ constexpr int RS = 40;  // LDS row stride in bf16 (32 k + 8 pad = 80 B)
 
 struct Pix {  // (sample, row, column) of an output pixel index, advanced without division
     int64_t b;
-    int oh, ow;
+    int oh = 0, ow = 0;
 };
 
 __device__ __forceinline__ void pix_step(Pix& p, int n, int OH, int OW) {
@@ -225,7 +225,7 @@ __global__ __launch_bounds__(256) void convg_bf16_kernel(ConvGArgs a) {
                     src = a.x + xbase + (int64_t)c0 * IHW + (int64_t)ih * a.IW + iw;
                     cst = IHW;
                 } else {
-                    int oh, ow;
+                    int oh = 0, ow = 0;
                     if (MODE == 3) {
                         oh = (ih0 - (kh0 + 2 * (tap / ntw))) >> 1;
                         ow = (iw0 - (kw0 + 2 * (tap % ntw))) >> 1;
@@ -259,7 +259,7 @@ __global__ __launch_bounds__(256) void convg_bf16_kernel(ConvGArgs a) {
                             if (ih >= 0 && ih < a.IH && iw >= 0 && iw < a.IW)
                                 v = a.x[xbase + (int64_t)ch * IHW + (int64_t)ih * a.IW + iw];
                         } else {
-                            int oh, ow;
+                            int oh = 0, ow = 0;
                             bool ok;
                             if (MODE == 3) {
                                 oh = (ih0 - (kh0 + 2 * (tap / ntw))) >> 1;
