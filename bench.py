@@ -99,12 +99,21 @@ def deep_kernel_costs(B, F, T):
     return out
 
 
-def deep_step_cost(B, F, T, D=128):
-    flops, act = 0, 4 * 2 * B * F * T
+def deep_step_cost(B, F, T, D=128, e=4):
+    """SURVEY 8(d)'s cnn_deep model: input read twice, every conv output written / read / re-read /
+    gradient written / read (5 passes), the same for the init max-pool output and every block
+    output; + 40 B per parameter and 12 B*D for SupCon (122.37 GB / step at B = 4096, T = 200)."""
+    flops, act = 0, e * 2 * B * F * T
     for fl, wl, dl, ci, co, k, s, IH, IW, OH, OW in deep_convs(F, T):
         macs = B * OH * OW * co * ci * k * k
         flops += 2 * macs * (3 if dl else 2)
-        act += 4 * 5 * B * co * OH * OW
+        act += e * 5 * B * co * OH * OW
+    H, W = (F - 1) // 2 + 1, (T - 1) // 2 + 1
+    act += e * 5 * B * DEEP_DIMS[0] * H * W  # init max-pool output
+    for i, co in enumerate(DEEP_DIMS):
+        s = 1 if i == 0 else 2
+        H, W = (H - 1) // s + 1, (W - 1) // s + 1
+        act += e * 5 * B * co * H * W        # block output
     flops += 4 * B * B * D + 3 * 2 * B * DEEP_DIMS[-1] * D
     return flops, act + 40 * 4968833 + 12 * B * D
 
@@ -123,13 +132,22 @@ def step_cost(B, F, T, D=128):
 
 
 # ----------------------------------------------------------------------------- CPU baseline
-def cpu_baseline(budget_s=12.0, B=64, T=200):
-    """float32 torch-CPU port of the reference train step (the reference cannot travel to the
-    GPU box), threads = cores - 2 as the reference's device helper sets (device.py:58-61)."""
+def cpu_model_name():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _cpu_leg(B, T, threads, min_s, min_steps, max_steps=200):
+    """One timed leg of the float32 torch-CPU port of the reference train step: 1 warm-up step,
+    then steps until min_s seconds and min_steps steps have passed."""
     from oracle import torch_port as tp
     from phoneme_contrast_amd.models import PhonemeNet
-    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 2)
-    threads = max(1, min(share, os.cpu_count() or share) - 2)
     torch.set_num_threads(threads)
     torch.manual_seed(42)
     sd = {k: v.clone() for k, v in PhonemeNet({"embedding_dim": 128, "dropout_rate": 0.1}).state_dict().items()}
@@ -144,11 +162,30 @@ def cpu_baseline(budget_s=12.0, B=64, T=200):
         tr.step(x, labels, masks)
         n += 1
         el = time.perf_counter() - t0
-        if (el > budget_s and n >= 2) or n >= 200:
+        if (el >= min_s and n >= min_steps) or n >= max_steps:
             break
-    return {"value": round(B * n / el, 2), "unit": "samples/s", "cores": threads, "kind": "port",
-            "sample": f"cnn_small train step (fwd+SupCon+bwd+Adam) B={B} T={T}, {n} steps in {el:.1f}s, "
-                      f"float32 torch-CPU restatement oracle/torch_port.py, {threads} threads"}
+    return {"B": B, "threads": threads, "steps": n, "seconds": round(el, 2), "samples_per_s": round(B * n / el, 2)}
+
+
+def cpu_baseline(full=False, T=200):
+    """The reference step on the host cores (the reference itself cannot travel to the GPU box):
+    the float32 torch-CPU restatement (oracle/torch_port.py, pinned to the reference's fixtures),
+    at the reference's real train batch B = 24 (6 classes x 2 clips x 2 views) with cores - 2
+    threads (src/utils/device.py:58-61) and with all cores; `full` adds the BASELINE's B = 4096
+    (1 warm-up + 2 timed steps per thread count: several minutes)."""
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 2)
+    allc = max(1, min(share, os.cpu_count() or share))
+    rule = max(1, allc - 2)
+    legs = [_cpu_leg(24, T, rule, 6.0, 3), _cpu_leg(24, T, allc, 6.0, 3)]
+    if full:
+        legs += [_cpu_leg(4096, T, rule, 0.0, 2, 2), _cpu_leg(4096, T, allc, 0.0, 2, 2)]
+    main = legs[0]
+    return {"value": main["samples_per_s"], "unit": "samples/s", "cores": main["threads"], "kind": "port",
+            "cpu_model": cpu_model_name(), "host_threads_available": allc,
+            "sample": f"cnn_small train step (fwd+SupCon+bwd+Adam) at the reference's real batch B=24, T={T}, "
+                      f"{main['steps']} steps in {main['seconds']}s on cores-2 = {main['threads']} threads "
+                      "(reference rule, src/utils/device.py:58-61); float32 torch-CPU restatement "
+                      "oracle/torch_port.py", "legs": legs}
 
 
 def measure_peaks(dev):
@@ -181,13 +218,14 @@ def measure_peaks(dev):
             "note": "measured on this GPU: 2 GiB D2D copy (read + write bytes); torch.mm fp32 8192^3"}
 
 
-def load_pmc(label):
-    """HBM bytes per launch of `label` from a committed rocprofv3 --pmc summary, or None."""
+def load_pmc(model, precision, label):
+    """HBM bytes per launch of `label` in the (model, precision) workload from the committed
+    rocprofv3 --pmc summary (profiles/pmc_traffic.json, keyed "<model>/<precision>"), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get(label, {}).get("hbm_bytes_per_launch")
+        return d.get(f"{model}/{precision}", {}).get(label, {}).get("hbm_bytes_per_launch")
     except Exception:
         return None
 
@@ -205,6 +243,9 @@ def main():
     ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
                     help="cnn_deep conv operand precision (bf16: float32 accumulation, float32 elsewhere)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-full", action="store_true", help="also time the CPU baseline at B=4096 (minutes)")
+    ap.add_argument("--bucket-mb", type=float, default=None,
+                    help="N > 1: gradient all-reduce bucket size (default 0.5 MB cnn_small, 4 MB cnn_deep)")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-peaks", action="store_true", help="skip the measured-peak probes")
     args = ap.parse_args()
@@ -235,6 +276,10 @@ def main():
     model = model.to(dev).train()
     ddp.broadcast_module(model)
     opt = FusedAdam(model.parameters(), lr=3e-4, weight_decay=1e-4)
+    bucketer = None
+    if world > 1:  # buckets all-reduced on a side stream behind the native backward
+        mb = args.bucket_mb if args.bucket_mb is not None else (4.0 if deep else 0.5)
+        bucketer = ddp.GradBucketer(model, bucket_bytes=int(mb * (1 << 20)))
     loss_fn = SupervisedContrastiveLoss(temperature=0.15)
     g = torch.Generator().manual_seed(1234 + rank)
     x = torch.randn(B, 1, F, T, generator=g).to(dev)
@@ -246,9 +291,7 @@ def main():
         opt.zero_grad(set_to_none=True)
         loss.backward()
         if world > 1:
-            flat = opt.flat_grad_views()
-            ddp.allreduce_flat(flat[0])
-            opt.step(flat_grads=flat, grad_scale=1.0 / world)
+            opt.step(flat_grads=bucketer.finish(), grad_scale=1.0 / world)
         else:
             opt.step()
         return loss
@@ -308,7 +351,7 @@ def main():
             ach = by / avg_s / 1e9
             roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4)}
-        roof["traffic"] = load_pmc(dom)
+        roof["traffic"] = load_pmc(args.model, args.precision if deep else "fp32", dom)
         roof["algorithmic_flops_per_launch"] = fl
         roof["algorithmic_bytes_per_launch"] = by
         roof["avg_launch_ms"] = round(avg_s * 1000.0, 4)
@@ -332,7 +375,7 @@ def main():
     cpu = None
     if world == 1 and not args.no_cpu_baseline and not deep:
         try:
-            cpu = cpu_baseline()
+            cpu = cpu_baseline(full=args.cpu_full)
         except Exception as exc:  # pragma: no cover - reported, never fatal for the GPU number
             cpu = {"error": repr(exc)}
 
@@ -352,7 +395,9 @@ def main():
         "config": {"workload": f"{args.model} contrastive train step: fwd + SupCon(T=0.15) + bwd + "
                                "grad all-reduce + Adam(lr 3e-4, wd 1e-4)",
                    "per_gpu_batch": B, "global_batch": B * world, "n_mfcc": F, "T": T,
-                   "embedding_dim": D, "parallelism": f"dp{world}"},
+                   "embedding_dim": D, "parallelism": f"dp{world}",
+                   "allreduce": None if world == 1 else f"{len(bucketer.buckets(next(iter(model._plans.values()))))} "
+                                                        "RCCL buckets behind the backward"},
         "roofline": roof,
         "step_roofline": step_roof,
         "cpu_baseline": cpu,

@@ -124,6 +124,20 @@ int pcx_net_profile(void* plan, int enable);
 int pcx_net_profile_read(void* plan, char* labels, size_t labels_len, float* total_ms,
                          int* counts, int max_entries);
 
+/* Gradient buckets for a data-parallel all-reduce that overlaps the backward (DDP).
+ * pcx_net_grad_buckets(plan, n, first_param) splits the parameter list into n buckets: bucket k
+ * holds parameters [first_param[k], first_param[k-1]) (first_param[-1] = nparams; the list must
+ * be strictly decreasing, first_param[n-1] = 0: bucket 0 holds the LAST parameters, whose
+ * gradients the backward finishes first).  During every later pcx_net_backward the plan records
+ * an event on its stream as soon as all gradients of a bucket are written.  pcx_net_bucket_wait
+ * makes `stream` wait for bucket k's event of the most recent backward (the caller then enqueues
+ * that bucket's collective on `stream`).  pcx_net_grad_stages lists the parameter indices at which
+ * the backward completes a stage (descending; a good bucket boundary), returns their count.
+ * n = 0 removes the buckets. */
+int pcx_net_grad_buckets(void* plan, int n, const int* first_param);
+int pcx_net_bucket_wait(void* plan, int k, hipStream_t stream);
+int pcx_net_grad_stages(const void* plan, int* first_param, int max_entries);
+
 /* Dropout2d keep-scale masks: out[i] = (u_i >= p) ? 1/(1-p) : 0 with u_i a counter-based
  * uniform draw from (seed, offset + i).  Not bit-compatible with torch's CPU generator. */
 int pcx_dropout_masks(float* out, int64_t n, float p, uint64_t seed, uint64_t offset,

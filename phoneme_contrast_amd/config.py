@@ -9,7 +9,8 @@ this image, so `compose()` implements the subset the reference's configs use:
   * command-line overrides `key.path=value`, `group=option`, `+new.key=value`, `~key`;
   * `${a.b}` interpolation and `${hydra:runtime.output_dir}` (outputs/<date>/<time>);
   * an attribute-access config object with `.get`, `dict(...)`, `to_container()`, `to_yaml()`.
-When hydra *is* importable, scripts/train.py uses it instead.
+When hydra *is* importable, scripts/train.py composes with @hydra.main instead and wraps the
+resolved container with `wrap()`.
 """
 import copy
 import datetime
@@ -41,6 +42,11 @@ def _wrap(x):
     if isinstance(x, list):
         return [_wrap(v) for v in x]
     return x
+
+
+def wrap(d):
+    """Attribute-access config from a plain (resolved) container, e.g. OmegaConf.to_container."""
+    return _wrap(d)
 
 
 def to_container(cfg):

@@ -1,264 +1,16 @@
-// Convolution kernels of the phoneme CNN on CDNA4 (gfx950), fp32 throughout.
+// Direct (non-GEMM) kernels of the cnn_small trunk on CDNA4 (gfx950), fp32 throughout.
 //
-//  * conv3x3_kernel  — 3x3 / stride 1 / pad 1 conv as an implicit GEMM on v_mfma_f32_32x32x2_f32
-//                      (exact f32).  One kernel body serves the forward conv (reference
-//                      src/models/phoneme_cnn.py:39,47,50,58,61) and its data gradient (the same conv
-//                      on dy with flipped, transposed weights).  The BN/ReLU/MaxPool/Dropout2d that
-//                      sit between two convs (phoneme_cnn.py:37-43, 48-54, 59-64) are applied while
-//                      the input tile is staged into LDS (prologue); BN statistics, or the backward
-//                      of ReLU/MaxPool/Dropout plus the BN-backward sums, are fused into the
-//                      epilogue.  No activation tensor is materialised between a conv and its BN.
-//  * conv1_fwd_kernel — the Cin = 1 first conv (phoneme_cnn.py:36): direct, HBM-write-bound.
-//  * wgrad1_kernel — first-layer weight gradient (the 3x3 weight gradients live in wgrad.hip).
+//  * conv1_fwd_kernel — the Cin = 1 first conv (reference src/models/phoneme_cnn.py:36): direct,
+//                       HBM-write-bound, with the BN statistics of its output in the epilogue.
+//  * wgrad1_kernel    — its weight gradient (the 3x3 implicit-GEMM convs live in conv_dma.hip,
+//                       their weight gradients in wgrad_win.hip / wgrad_w32.hip).
+//  * sum_slices / pack kernels — deterministic slice reduction and GEMM weight layouts.
 //
-// Tensor layout is the reference's planar NCHW.  MFMA orientation: A = weights (M = output
-// channels), B = input pixels (N = 32 consecutive flattened pixels per lane group), so each
-// accumulator register holds one channel for 32 consecutive pixels and the output stores are
-// 128-byte coalesced rows of a channel plane.
+// Tensor layout is the reference's planar NCHW.
 #include "conv_epilogue.h"
 
 namespace pcx {
 namespace {
-
-constexpr int PADL = 4;  // left pad of an LDS row: data column 0 sits 16-byte aligned
-constexpr int CK = 8;    // input channels staged per K-chunk
-
-__device__ __forceinline__ int fdiv(int n, int d, float inv) {  // n / d for 0 <= n < 2^22
-    int q = (int)((float)n * inv);
-    int r = n - q * d;
-    if (r < 0) --q;
-    else if (r >= d) ++q;
-    return q;
-}
-
-__device__ __forceinline__ int xcd_remap(int orig, int nb) {
-    // blocks b and b+8 share an XCD (observed round-robin dispatch): give each XCD a contiguous
-    // range of tiles so neighbouring tiles (which share halo rows) hit the same L2.  Bijective.
-    int q = nb >> 3, r = nb & 7, x = orig & 7;
-    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (orig >> 3);
-}
-
-// ------------------------------------------------------------------ prologue (staging)
-template <int PRO>
-__device__ __forceinline__ float pro_elem(const ConvArgs& a, int c, int b, int hh, int w) {
-    if (PRO == PRO_RAW) {
-        return a.src[(((int64_t)b * a.cin + c) * a.H + hh) * a.W + w];
-    } else if (PRO == PRO_BNRELU) {
-        float4 cf = a.cf_in[c];
-        float v = a.src[(((int64_t)b * a.cin + c) * a.H + hh) * a.W + w];
-        return fmaxf(fmaf(v, cf.x, cf.y), 0.f);
-    } else if (PRO == PRO_BNRELU_POOL) {
-        float4 cf = a.cf_in[c];
-        const float* p = a.src + (((int64_t)b * a.cin + c) * a.srcH + 2 * hh) * a.srcW + 2 * w;
-        float m = fmaxf(fmaxf(fmaf(p[0], cf.x, cf.y), fmaf(p[1], cf.x, cf.y)),
-                        fmaxf(fmaf(p[a.srcW], cf.x, cf.y), fmaf(p[a.srcW + 1], cf.x, cf.y)));
-        m = fmaxf(m, 0.f);
-        return a.drop_in ? m * a.drop_in[(int64_t)b * a.cin + c] : m;
-    } else {  // PRO_BNBWD
-        float4 cf = a.cf_in[c];
-        int64_t o = (((int64_t)b * a.cin + c) * a.H + hh) * a.W + w;
-        return cf.x * (a.src[o] - cf.y - (a.src2[o] - cf.w) * cf.z);
-    }
-}
-
-template <int PRO>
-__device__ __forceinline__ float4 pro_quad(const ConvArgs& a, int c, int b, int hh, int w) {
-    // four consecutive conv-input columns w..w+3 (w % 4 == 0) of channel c, row hh of sample b
-    const bool full = (w + 3 < a.W) && ((a.W & 3) == 0) &&
-                      (PRO != PRO_BNRELU_POOL || (a.srcW & 3) == 0);
-    if (full) {
-        if (PRO == PRO_RAW || PRO == PRO_BNRELU) {
-            float4 v = ld4(a.src + (((int64_t)b * a.cin + c) * a.H + hh) * a.W + w);
-            if (PRO == PRO_BNRELU) {
-                float4 cf = a.cf_in[c];
-                v.x = fmaxf(fmaf(v.x, cf.x, cf.y), 0.f);
-                v.y = fmaxf(fmaf(v.y, cf.x, cf.y), 0.f);
-                v.z = fmaxf(fmaf(v.z, cf.x, cf.y), 0.f);
-                v.w = fmaxf(fmaf(v.w, cf.x, cf.y), 0.f);
-            }
-            return v;
-        } else if (PRO == PRO_BNRELU_POOL) {
-            float4 cf = a.cf_in[c];
-            const float* p = a.src + (((int64_t)b * a.cin + c) * a.srcH + 2 * hh) * a.srcW + 2 * w;
-            float4 t0 = ld4(p), t1 = ld4(p + 4), u0 = ld4(p + a.srcW), u1 = ld4(p + a.srcW + 4);
-            auto bn = [&](float v) { return fmaf(v, cf.x, cf.y); };
-            float4 r;
-            r.x = fmaxf(fmaxf(fmaxf(bn(t0.x), bn(t0.y)), fmaxf(bn(u0.x), bn(u0.y))), 0.f);
-            r.y = fmaxf(fmaxf(fmaxf(bn(t0.z), bn(t0.w)), fmaxf(bn(u0.z), bn(u0.w))), 0.f);
-            r.z = fmaxf(fmaxf(fmaxf(bn(t1.x), bn(t1.y)), fmaxf(bn(u1.x), bn(u1.y))), 0.f);
-            r.w = fmaxf(fmaxf(fmaxf(bn(t1.z), bn(t1.w)), fmaxf(bn(u1.z), bn(u1.w))), 0.f);
-            if (a.drop_in) {
-                float d = a.drop_in[(int64_t)b * a.cin + c];
-                r.x *= d; r.y *= d; r.z *= d; r.w *= d;
-            }
-            return r;
-        } else {
-            float4 cf = a.cf_in[c];
-            int64_t o = (((int64_t)b * a.cin + c) * a.H + hh) * a.W + w;
-            float4 dz = ld4(a.src + o), y = ld4(a.src2 + o);
-            float4 r;
-            r.x = cf.x * (dz.x - cf.y - (y.x - cf.w) * cf.z);
-            r.y = cf.x * (dz.y - cf.y - (y.y - cf.w) * cf.z);
-            r.z = cf.x * (dz.z - cf.y - (y.z - cf.w) * cf.z);
-            r.w = cf.x * (dz.w - cf.y - (y.w - cf.w) * cf.z);
-            return r;
-        }
-    }
-    float4 r;
-    r.x = (w + 0 < a.W) ? pro_elem<PRO>(a, c, b, hh, w + 0) : 0.f;
-    r.y = (w + 1 < a.W) ? pro_elem<PRO>(a, c, b, hh, w + 1) : 0.f;
-    r.z = (w + 2 < a.W) ? pro_elem<PRO>(a, c, b, hh, w + 2) : 0.f;
-    r.w = (w + 3 < a.W) ? pro_elem<PRO>(a, c, b, hh, w + 3) : 0.f;
-    return r;
-}
-
-// ------------------------------------------------------------------ 3x3 implicit GEMM
-template <int WM, int WN, int PRO, int EPI>
-__global__ __launch_bounds__(256) void conv3x3_kernel(ConvArgs a) {
-    constexpr int SU = (PRO == PRO_BNRELU_POOL || PRO == PRO_BNBWD) ? 2 : 4;  // staging unroll
-    constexpr int COUT_T = 32 * WM;
-    constexpr int BP = 4 * WN * 32;  // pixels per block
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int PLANE = a.NR * a.RS;
-    float* xs = smem;
-    float* wsm = smem + CK * PLANE;
-
-    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int ny = a.cout / COUT_T;
-    const int nb = gridDim.x;
-    const int flat = xcd_remap(blockIdx.x, nb);
-    const int tile = flat / ny;
-    const int n0 = (flat - tile * ny) * COUT_T;
-    const int64_t HW = (int64_t)a.H * a.W;
-    const int64_t Mtot = (int64_t)a.B * HW;
-    const int64_t m0 = (int64_t)tile * BP;
-    const int64_t row0 = m0 / a.W - 1;  // global row (b*H + h) of staged row 0
-    const int64_t nrows = (int64_t)a.B * a.H;
-
-    int pixoff[WN];
-    bool vup[WN], vdn[WN], valid[WN];
-    int pb[WN], pp[WN];
-#pragma unroll
-    for (int ni = 0; ni < WN; ++ni) {
-        int64_t m = m0 + (wave * WN + ni) * 32 + l32;
-        valid[ni] = m < Mtot;
-        int64_t mm = valid[ni] ? m : Mtot - 1;
-        int64_t gr = mm / a.W;
-        int w = (int)(mm - gr * a.W);
-        int b = (int)(gr / a.H);
-        int hr = (int)(gr - (int64_t)b * a.H);
-        pixoff[ni] = (int)(gr - row0) * a.RS + PADL + w;
-        vup[ni] = hr > 0;
-        vdn[ni] = hr < a.H - 1;
-        pb[ni] = b;
-        pp[ni] = hr * a.W + w;
-    }
-
-    f32x16 acc[WM][WN];
-#pragma unroll
-    for (int mi = 0; mi < WM; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < WN; ++ni) acc[mi][ni] = f32x16{0.f};
-
-    // staged-row table: sample and row of every LDS row (b = -1 outside the batch)
-    __shared__ int2 rinfo[160];
-    for (int lr = tid; lr < a.NR; lr += 256) {
-        int64_t gr = row0 + lr;
-        bool ok = gr >= 0 && gr < nrows;
-        int b = ok ? (int)(gr / a.H) : -1;
-        rinfo[lr] = make_int2(b, ok ? (int)(gr - (int64_t)b * a.H) : 0);
-    }
-    const int Q = a.RS >> 2;
-    const int QT = CK * a.NR * Q;
-    const float invQ = 1.f / Q, invNR = 1.f / a.NR;
-    const int wlast = ((a.W - 1) >> 2) << 2;  // start of the last data quad
-    for (int c0 = 0; c0 < a.cin; c0 += CK) {
-        __syncthreads();
-        // ---- stage CK input channels x NR rows (prologue applied); U quads in flight per thread
-        for (int e0 = tid; e0 < QT; e0 += 256 * SU) {
-            float4 v[SU];
-            int dst[SU];
-#pragma unroll
-            for (int u = 0; u < SU; ++u) {
-                const int e = e0 + u * 256;
-                const bool in = e < QT;
-                const int ee = in ? e : 0;
-                const int row = fdiv(ee, Q, invQ);
-                const int q = ee - row * Q;
-                const int cl = fdiv(row, a.NR, invNR);
-                const int lr = row - cl * a.NR;
-                const int2 ri = rinfo[lr];
-                const int w = (q - 1) * 4;
-                const bool ok = in && ri.x >= 0 && q >= 1 && w < a.W;
-                float4 t = pro_quad<PRO>(a, c0 + cl, max(ri.x, 0), ri.y, min(max(w, 0), wlast));
-                v[u] = ok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
-                dst[u] = in ? cl * PLANE + lr * a.RS + 4 * q : -1;
-            }
-#pragma unroll
-            for (int u = 0; u < SU; ++u)
-                if (dst[u] >= 0) st4(xs + dst[u], v[u]);
-        }
-        // ---- stage the weight chunk [9][CK][COUT_T]
-        constexpr int QW = COUT_T / 4;
-#pragma unroll 4
-        for (int slot = tid; slot < 9 * CK * QW; slot += 256) {
-            int row = slot / QW, q = slot - row * QW;
-            int tap = row / CK, cc = row - tap * CK;
-            st4(wsm + row * COUT_T + 4 * q,
-                ld4(a.wpack + ((int64_t)(tap * a.cin + c0 + cc)) * a.cout + n0 + 4 * q));
-        }
-        __syncthreads();
-        // ---- 9 taps x CK/2 MFMA k-steps
-#pragma unroll
-        for (int tap = 0; tap < 9; ++tap) {
-            const int dh = tap / 3 - 1, dw = tap % 3 - 1;
-            const int toff = dh * a.RS + dw;
-#pragma unroll
-            for (int s = 0; s < CK / 2; ++s) {
-                float av[WM], bv[WN];
-#pragma unroll
-                for (int mi = 0; mi < WM; ++mi)
-                    av[mi] = wsm[(tap * CK + 2 * s + h) * COUT_T + mi * 32 + l32];
-#pragma unroll
-                for (int ni = 0; ni < WN; ++ni) {
-                    float v = xs[(2 * s + h) * PLANE + pixoff[ni] + toff];
-                    if (dh < 0 && !vup[ni]) v = 0.f;
-                    if (dh > 0 && !vdn[ni]) v = 0.f;
-                    bv[ni] = v;
-                }
-#pragma unroll
-                for (int mi = 0; mi < WM; ++mi)
-#pragma unroll
-                    for (int ni = 0; ni < WN; ++ni) acc[mi][ni] = mfma32(av[mi], bv[ni], acc[mi][ni]);
-            }
-        }
-    }
-
-    // ------------------------------------------------------------------ epilogues
-    __syncthreads();  // LDS is reused for the cross-wave statistics below
-    conv_epilogue<WM, WN, EPI>(a, acc, smem, tile, n0, m0, Mtot, HW, wave, tid, valid, pb, pp);
-}
-
-template <int WM, int WN>
-int launch_tiles(int pro, int epi, const ConvArgs& a, dim3 grid, size_t smem, hipStream_t s) {
-#define PCX_CONV_CASE(P, E)                                                                      \
-    if (pro == P && epi == E) {                                                                 \
-        (void)hipFuncSetAttribute((const void*)conv3x3_kernel<WM, WN, P, E>,                          \
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);            \
-        conv3x3_kernel<WM, WN, P, E><<<grid, 256, smem, s>>>(a);                                \
-        PCX_LAUNCH_CHECK("conv3x3_kernel");                                                     \
-        return PCX_OK;                                                                          \
-    }
-    PCX_CONV_CASE(PRO_RAW, EPI_FWD)
-    PCX_CONV_CASE(PRO_BNRELU, EPI_FWD)
-    PCX_CONV_CASE(PRO_BNRELU_POOL, EPI_FWD)
-    PCX_CONV_CASE(PRO_BNBWD, EPI_BWD_RELU)
-    PCX_CONV_CASE(PRO_BNBWD, EPI_BWD_POOL)
-#undef PCX_CONV_CASE
-    set_error("conv3x3: unsupported prologue/epilogue pair (%d, %d)", pro, epi);
-    return PCX_EINVAL;
-}
 
 void tile_shape(int cout, int* wm, int* wn) {
     if (cout == 32) { *wm = 1; *wn = 4; }
@@ -440,26 +192,6 @@ size_t conv3x3_nblk(int B, int H, int W, int cout) {
     return (size_t)ceil_div(M, 4 * wn * 32);
 }
 
-int launch_conv3x3(int pro, int epi, ConvArgs a, hipStream_t s) {
-    PCX_CHECK_ARG(a.cin % CK == 0, "conv3x3: cin %d must be a multiple of %d", a.cin, CK);
-    PCX_CHECK_ARG(a.cout == 32 || a.cout % 64 == 0, "conv3x3: cout %d unsupported", a.cout);
-    PCX_CHECK_ARG(a.B > 0 && a.H > 0 && a.W > 0, "conv3x3: empty tensor");
-    int wm, wn;
-    tile_shape(a.cout, &wm, &wn);
-    const int bp = 4 * wn * 32, cout_t = 32 * wm;
-    const int64_t M = (int64_t)a.B * a.H * a.W;
-    const int ntile = ceil_div(M, bp);
-    PCX_CHECK_ARG(a.nblk == ntile, "conv3x3: partial buffer sized for %d tiles, need %d", a.nblk, ntile);
-    a.NR = (bp - 1 + a.W - 1) / a.W + 1 + 2;
-    a.RS = PADL + ((a.W + 1 + 3) / 4) * 4;
-    size_t smem = ((size_t)CK * a.NR * a.RS + 9 * CK * cout_t) * sizeof(float);
-    size_t red = ((size_t)4 * cout_t * 3 + 4 * (size_t)cout_t) * sizeof(float);  // epilogue partials + cf table
-    if (smem < red) smem = red;
-    PCX_CHECK_ARG(smem <= 150 * 1024 && a.NR <= 160, "conv3x3: W=%d needs %zu B of LDS", a.W, smem);
-    dim3 grid((unsigned)(ntile * (a.cout / cout_t)));
-    if (wm == 1 && wn == 4) return launch_tiles<1, 4>(pro, epi, a, grid, smem, s);
-    return launch_tiles<2, 2>(pro, epi, a, grid, smem, s);
-}
 
 int conv1_nblk(int B, int H, int* rows_per_blk) {
     int64_t nrows = (int64_t)B * H;

@@ -5,9 +5,9 @@
 //    the weight chunk are copied HBM/L2 -> LDS by global_load_lds (dwordx4 when rows are 16-byte
 //    aligned, dword otherwise) into one of two buffers; chunk k+1 is in flight while the MFMAs of
 //    chunk k run, so staging latency is hidden and costs no VGPRs;
-//  * the prologue (BN+ReLU of the producer, or the BN backward (dz, y) -> dy for the data
-//    gradient) is applied when a B operand is read from LDS, together with the zero-padding /
-//    sample-boundary mask of its tap (3-5 VALU per operand, under the 64-cycle MFMA shadow);
+//  * the prologue (BN+ReLU of the producer; the data gradient reads the dy its weight gradient
+//    materialised, raw) is applied when a B operand is read from LDS, together with the
+//    zero-padding / sample-boundary mask of its tap;
 //  * one barrier per chunk; all per-chunk tables live in the single dynamic LDS array (no second
 //    __shared__ object, so hipcc does not drain the DMA queue before LDS reads).
 #include "conv_epilogue.h"
@@ -79,24 +79,21 @@ __host__ __device__ constexpr int dma_table_floats(int cin, int NR) {
     return 4 * cin + ((2 * NR + 3) & ~3) + ((NR + 3) & ~3) + 4 * NR;
 }
 
-// raw image of one K-chunk: NSRC tensors x CK channels x NR staged rows x W columns (dense)
-template <int VEC, int NSRC>
+// raw image of one K-chunk: CK channels x NR staged rows x W columns (dense)
+template <int VEC>
 __device__ __forceinline__ void issue_raw(const ConvArgs& a, const int2* rinfo, unsigned raw, int c0,
                                           int wave, int lane, int total, int CK, float invPL,
                                           float invW) {
     const int PL = a.NR * a.W;  // floats per channel plane of the image
     for (int base = wave * 64 * VEC; base < total; base += 4 * 64 * VEC) {
         const int f = min(base + lane * VEC, total - VEC);
-        const int src = (NSRC == 2) ? (f >= CK * PL ? 1 : 0) : 0;
-        const int ff = f - src * CK * PL;
-        const int cl = fdiv(ff, PL, invPL);
-        const int rem = ff - cl * PL;
+        const int cl = fdiv(f, PL, invPL);
+        const int rem = f - cl * PL;
         const int lr = fdiv(rem, a.W, invW);
         const int w = rem - lr * a.W;
         const int2 ri = rinfo[lr];
         const int b = ri.x < 0 ? 0 : ri.x;
-        const float* t = (src == 0) ? a.src : a.src2;
-        const float* g = t + ((((int64_t)b * a.cin + c0 + cl) * a.H + ri.y) * a.W + w);
+        const float* g = a.src + ((((int64_t)b * a.cin + c0 + cl) * a.H + ri.y) * a.W + w);
         dma<VEC>(g, raw + 4u * base);
     }
 }
@@ -122,15 +119,13 @@ constexpr int dma_occ(int wm) { return wm == 2 ? 4 : 3; }
 
 template <int WM, int WN, int VEC, int PRO, int EPI, int CK, bool PRE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_occ(WM)))) void conv3x3_dma_kernel(ConvArgs a) {
-    static_assert(!PRE || PRO != PRO_BNBWD, "precomputed copies stage one source");
     constexpr int COUT_T = 32 * WM;
     constexpr int BP = 4 * WN * 32;
-    constexpr int NSRC = (PRO == PRO_BNBWD) ? 2 : 1;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     // channel-plane stride of the staged image: dense rows (NR * W), or with PRE the row segments
     // of each sample placed at the 16-byte phase of their global address (host-computed bound)
     const int PL = PRE ? a.RS : a.NR * a.W;
-    const int rawf = ((NSRC * CK * PL + 64 * VEC - 1) / (64 * VEC)) * (64 * VEC);
+    const int rawf = ((CK * PL + 64 * VEC - 1) / (64 * VEC)) * (64 * VEC);
     const int wtsf = ((9 * CK * COUT_T + 255) / 256) * 256;
     float4* cft = reinterpret_cast<float4*>(smem);                        // [cin]
     int2* rinfo = reinterpret_cast<int2*>(smem + 4 * a.cin);              // [NR] (padded to 4)
@@ -222,7 +217,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_occ(WM)
 #pragma unroll
         for (int ni = 0; ni < WN; ++ni) acc[mi][ni] = f32x16{0.f};
 
-    const int rawtotal = NSRC * CK * PL;
+    const int rawtotal = CK * PL;
     const float invPL = 1.f / PL, invW = 1.f / a.W;
     const int nchunk = a.cin / CK;
     constexpr int WTOT = 9 * CK * COUT_T;
@@ -270,7 +265,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_occ(WM)
                 if (base < WTOT) dma_s<4>(sw, woff[j], wts_lds + nb * 4u * wtsf + 4u * base);
             }
         } else {
-            issue_raw<VEC, NSRC>(a, rinfo, raw_lds + nb * 4u * rawf, c0, wave, lane, rawtotal, CK, invPL, invW);
+            issue_raw<VEC>(a, rinfo, raw_lds + nb * 4u * rawf, c0, wave, lane, rawtotal, CK, invPL, invW);
             issue_wts<WM>(a, wts_lds + nb * 4u * wtsf, c0, n0, wave, lane, CK);
         }
     };
@@ -293,8 +288,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_occ(WM)
         // before the MFMAs of step i (sched_barrier keeps the scheduler from sinking the reads
         // next to their use, which exposes the LDS latency in front of the MFMAs)
         constexpr int NST = 9 * (CK / 2);
-        float av[2][WM], rv[2][WN], rv2[2][WN];
-        auto load = [&](int st, float (&a_)[WM], float (&r_)[WN], float (&r2_)[WN]) {
+        float av[2][WM], rv[2][WN];
+        auto load = [&](int st, float (&a_)[WM], float (&r_)[WN]) {
             const int tap = st / (CK / 2), s = st % (CK / 2);
             const int toff = (tap / 3 - 1) * a.W + (tap % 3 - 1);
 #pragma unroll
@@ -303,14 +298,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_occ(WM)
             for (int ni = 0; ni < WN; ++ni) {
                 const int o = (2 * s + h) * PL + pixoff[ni] + toff;
                 r_[ni] = (PCX_CONV_EXPT & 32) ? (float)(o & 7) : raw[o];
-                if (PRO == PRO_BNBWD) r2_[ni] = raw[o + CK * PL];
             }
         };
-        load(0, av[0], rv[0], rv2[0]);
+        load(0, av[0], rv[0]);
 #pragma unroll
         for (int st = 0; st < NST; ++st) {
             const int cur = st & 1;
-            if (st + 1 < NST) load(st + 1, av[cur ^ 1], rv[cur ^ 1], rv2[cur ^ 1]);
+            if (st + 1 < NST) load(st + 1, av[cur ^ 1], rv[cur ^ 1]);
             __builtin_amdgcn_sched_barrier(0);
             const int tap = st / (CK / 2), s = st % (CK / 2);
             const int dh = tap / 3 - 1, dw = tap % 3 - 1;
@@ -320,10 +314,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_occ(WM)
                 float v;
                 if (PRO == PRO_RAW || (PCX_CONV_EXPT & 16)) {
                     v = rv[cur][ni];
-                } else if (PRO == PRO_BNRELU) {
+                } else {  // PRO_BNRELU
                     v = fmaxf(fmaf(rv[cur][ni], cf[s].x, cf[s].y), 0.f);
-                } else {  // PRO_BNBWD: dy = a * (dz - mb - (y - mean) * mgi)
-                    v = cf[s].x * (rv[cur][ni] - cf[s].y - (rv2[cur][ni] - cf[s].w) * cf[s].z);
                 }
                 bool ok = true;
                 if (PCX_CONV_EXPT & 16) {
@@ -410,13 +402,12 @@ __global__ __launch_bounds__(256) void bn_relu_pool_kernel(const float* __restri
 
 }  // namespace
 
-int conv3x3_dma_ck(int pro, int cout, int PL, int NR, int cin) {
+int conv3x3_dma_ck(int cout, int PL, int NR, int cin) {
     // largest K-chunk whose double-buffered raw image + weights let dma_occ blocks share a CU
-    const int nsrc = pro == PRO_BNBWD ? 2 : 1;
     const int cout_t = cout == 32 ? 32 : 64;
     for (int ck = 8; ck >= 2; ck >>= 1) {
         if (cin % ck) continue;
-        size_t raw = (size_t)nsrc * ck * PL + 256;
+        size_t raw = (size_t)ck * PL + 256;
         size_t wts = (size_t)9 * ck * cout_t + 256;
         size_t bytes = (2 * raw + 2 * wts + (size_t)dma_table_floats(cin, NR)) * 4;
         if (bytes <= (size_t)160 * 1024 / dma_occ(cout == 32 ? 1 : 2)) return ck;
@@ -426,21 +417,20 @@ int conv3x3_dma_ck(int pro, int cout, int PL, int NR, int cin) {
 
 int launch_conv3x3_dma(int pro, int epi, ConvArgs a, hipStream_t s) {
     PCX_CHECK_ARG(a.cout == 32 || a.cout % 64 == 0, "conv3x3: cout %d unsupported", a.cout);
-    PCX_CHECK_ARG(pro == PRO_RAW || pro == PRO_BNRELU || pro == PRO_BNBWD, "conv3x3_dma: prologue %d", pro);
+    PCX_CHECK_ARG(pro == PRO_RAW || pro == PRO_BNRELU, "conv3x3_dma: prologue %d", pro);
     const int wm = a.cout == 32 ? 1 : 2, wn = a.cout == 32 ? 4 : 2;
     const int bp = 4 * wn * 32, cout_t = 32 * wm;
     const int64_t M = (int64_t)a.B * a.H * a.W;
     const int ntile = ceil_div(M, bp);
     PCX_CHECK_ARG(a.nblk == ntile, "conv3x3: partial buffer sized for %d tiles, need %d", a.nblk, ntile);
     a.NR = (bp - 1 + a.W - 1) / a.W + 1 + 2;
-    const int nsrc = pro == PRO_BNBWD ? 2 : 1;
     // Preferred: segment layout (16-byte copies at any W, offsets precomputed per tile).  A tile's
     // rows span at most NR / H + 2 samples plus an invalid run at either end; each segment costs
     // at most 7 floats of alignment gap.
     const int64_t HW = (int64_t)a.H * a.W;
     const int PLseg = ((a.NR * a.W + 8 * (a.NR / a.H + 4)) + 3) & ~3;
-    int ck = conv3x3_dma_ck(pro, a.cout, PLseg, a.NR, a.cin);
-    bool pre = nsrc == 1 && HW % 4 == 0 && a.cin % ck == 0 && ceil_div(ck * PLseg, 1024) <= DMA_MAXR &&
+    int ck = conv3x3_dma_ck(a.cout, PLseg, a.NR, a.cin);
+    bool pre = HW % 4 == 0 && a.cin % ck == 0 && ceil_div(ck * PLseg, 1024) <= DMA_MAXR &&
                ceil_div(9 * ck * cout_t, 1024) <= DMA_MAXW &&
                (int64_t)((a.NR / a.H + 3) * a.cin) * HW * 4 < ((int64_t)1 << 31);
     int vec = 4, PL = PLseg;
@@ -449,10 +439,10 @@ int launch_conv3x3_dma(int pro, int epi, ConvArgs a, hipStream_t s) {
     } else {
         vec = (a.W % 4 == 0) ? 4 : 1;
         PL = a.NR * a.W;
-        ck = conv3x3_dma_ck(pro, a.cout, PL, a.NR, a.cin);
+        ck = conv3x3_dma_ck(a.cout, PL, a.NR, a.cin);
     }
     PCX_CHECK_ARG(a.cin % ck == 0, "conv3x3: cin %d not a multiple of %d", a.cin, ck);
-    const int rawf = ((nsrc * ck * PL + 64 * vec - 1) / (64 * vec)) * (64 * vec);
+    const int rawf = ((ck * PL + 64 * vec - 1) / (64 * vec)) * (64 * vec);
     const int wtsf = ((9 * ck * cout_t + 255) / 256) * 256;
     size_t smem = ((size_t)dma_table_floats(a.cin, a.NR) + 2 * (size_t)rawf + 2 * (size_t)wtsf) * 4;
     size_t red = ((size_t)4 * cout_t * 3 + 4 * (size_t)cout_t) * 4;  // epilogue partials + cf table

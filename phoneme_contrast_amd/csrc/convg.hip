@@ -767,7 +767,7 @@ size_t convg_wpack_bytes(int mode, int cin, int cout, int k) {
 int launch_convg(ConvGArgs a, hipStream_t s) {
     PCX_CHECK_ARG(a.stride == 1 || a.stride == 2, "convg: stride %d unsupported", a.stride);
     PCX_CHECK_ARG(a.B > 0 && a.cin > 0 && a.cout > 0, "convg: empty tensor");
-    if (a.mode == 1 && a.stride == 2 && !getenv("PCX_CONVG_NOPARITY")) {
+    if (a.mode == 1 && a.stride == 2) {
         for (int par = 0; par < 4; ++par) {  // each parity class of dx written exactly once
             ConvGArgs c = a;
             c.mode = 3;
@@ -890,7 +890,7 @@ int launch_maxpool3_fwd(const float* y, const float4* cf, float* out, uint8_t* a
                   H, W);
     const int64_t rows = (int64_t)B * C;
     const size_t lds = (size_t)H * W * 4;
-    if (lds <= 64 * 1024 && !getenv("PCX_MAXPOOL_OLD")) {
+    if (lds <= 64 * 1024) {  // plane fits: LDS-staged form
         if ((H * W) % 4 == 0) maxpool3_fwd_lds_kernel<4><<<(unsigned)rows, 256, lds, s>>>(y, cf, out, arg, C, H, W, OH, OW);
         else maxpool3_fwd_lds_kernel<1><<<(unsigned)rows, 256, lds, s>>>(y, cf, out, arg, C, H, W, OH, OW);
         PCX_LAUNCH_CHECK("maxpool3_fwd_lds_kernel");
@@ -904,7 +904,7 @@ int launch_maxpool3_fwd(const float* y, const float4* cf, float* out, uint8_t* a
 bool maxpool3_bwd_prep_fits(int H, int W, int OH, int OW) {
     (void)H;
     (void)W;
-    return (size_t)OH * OW * 5 <= 64 * 1024 && !getenv("PCX_MAXPOOL_OLD");
+    return (size_t)OH * OW * 5 <= 64 * 1024;
 }
 
 int launch_maxpool3_bwd_prep(const uint8_t* arg, const float* dout, const float* y, const float4* cf, float* g,

@@ -90,8 +90,7 @@ int build_deep(Plan& p) {
     size_t wpk = 0;
     int cmax = 0;
     for (int i = 0; i < 4; ++i) cmax = std::max(cmax, d.h[i]);
-    const char* dmaenv = getenv("PCX_DEEP_DMA");  // "0": every conv on the general engine (A/B)
-    const bool route = !d.bf16 && !(dmaenv && dmaenv[0] == '0');
+    const bool route = !d.bf16;  // fp32: stride-1 3x3 convs on the LDS-DMA / 32x32 engines
     // a stride-1 3x3 conv cin -> cout at HxW on the DMA conv (fwd, dgrad) and the 32x32 wgrad
     auto plan_routed = [&](int ci, int co, int h, int w, bool* fwd, bool* w32, WgradArgs* wga, int* nblk) {
         *fwd = route && (co == 32 || co % 64 == 0) && (ci == 32 || ci % 64 == 0) && ci % 2 == 0;
@@ -184,6 +183,11 @@ int build_deep(Plan& p) {
     p.hp_dwa = p.carve("hp_dwa", (size_t)K * B * 4);
     p.hp_dba = p.carve("hp_dba", (size_t)B * 4);
     p.nparams = d.ip + 4;
+    // backward completion points: projection, attention, blocks 3..0, stem
+    p.stages = {d.ip};
+    if (p.cfg.use_attention) p.stages.push_back(d.ia);
+    for (int i = 3; i >= 0; --i) p.stages.push_back(d.blk[i].pidx);
+    p.stages.push_back(0);
     p.nbn = bnidx + 1;
     p.ndrop = 4;
     for (int i = 0; i < 4; ++i) p.drop_ch[i] = d.h[i];
@@ -458,6 +462,7 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
     const int ip = d.ip, ia = d.ia;
     // dy is handed to the routed weight gradients ready-made: identity BN-backward coefficients
     RC(launch_fill_cf(c.w<float4>(d.identw), d.cmax, make_float4(1.f, 0.f, 0.f, 1.f), s));
+    p.buckets.begin();
     {
         ProjArgs j{};
         j.B = B; j.K = p.C6; j.D = p.D;
@@ -481,6 +486,7 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
         Scope sc(&p.prof, s, "proj_bwd");
         RC(launch_proj_bwd(j, s));
     }
+    p.buckets.mark(ip, s);
     {
         HeadPoolArgs h{};
         h.B = B; h.C = p.C6; h.P = p.P6;
@@ -500,6 +506,7 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
         if (p.cfg.use_attention) {
             RC(launch_row_sum(h.p_dwa, p.C6, B, G[ia], s));
             RC(launch_row_sum(h.p_dba, 1, B, G[ia + 1], s));
+            p.buckets.mark(ia, s);
         }
     }
     // upstream gradient of the current block's output (already ReLU-masked for the last block)
@@ -599,6 +606,7 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
         }
         dout = da;
         masked = false;
+        p.buckets.mark(k.pidx, s);
     }
     // ---- stem: MaxPool(3,2,1) + ReLU backward, BN0 backward, 7x7 weight gradient
     const int C0 = d.h[0];
@@ -638,14 +646,18 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
     // the stem's dy feeds only its weight gradient: the fp32 engine applies the BN backward while
     // staging (one pass over y0 / g instead of three); the bf16 engine's pixel-pair staging is
     // faster on a materialised dy (measured: 3.3 ms + apply vs 11 ms fused)
-    if (!d.bf16)
-        return conv_wgrad(c, 0, x, 1, d.H0, d.W0, 7, 1, 3, nullptr, C0, d.H0, d.W0, G[0], G[1], nullptr, dz0,
-                          c.w<float>(d.y0), c.w<float4>(d.cfb0));
-    {
-        Scope sc(&p.prof, s, "bn_bwd_apply");
-        RC(launch_bn_bwd_apply(dz0, c.w<float>(d.y0), c.w<float4>(d.cfb0), dz0, B, C0, P0, s));
+    if (!d.bf16) {
+        RC(conv_wgrad(c, 0, x, 1, d.H0, d.W0, 7, 1, 3, nullptr, C0, d.H0, d.W0, G[0], G[1], nullptr, dz0,
+                      c.w<float>(d.y0), c.w<float4>(d.cfb0)));
+    } else {
+        {
+            Scope sc(&p.prof, s, "bn_bwd_apply");
+            RC(launch_bn_bwd_apply(dz0, c.w<float>(d.y0), c.w<float4>(d.cfb0), dz0, B, C0, P0, s));
+        }
+        RC(conv_wgrad(c, 0, x, 1, d.H0, d.W0, 7, 1, 3, dz0, C0, d.H0, d.W0, G[0], G[1]));
     }
-    return conv_wgrad(c, 0, x, 1, d.H0, d.W0, 7, 1, 3, dz0, C0, d.H0, d.W0, G[0], G[1]);
+    p.buckets.mark(0, s);
+    return PCX_OK;
 }
 
 }  // namespace pcx

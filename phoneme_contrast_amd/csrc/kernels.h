@@ -10,8 +10,6 @@ namespace pcx {
 enum Prologue {
     PRO_RAW = 0,        // x = src
     PRO_BNRELU = 1,     // x = max(0, src*s[c] + t[c])                        (cf = {s,t,.,.})
-    PRO_BNRELU_POOL = 2,// x = drop[b,c] * max_2x2 max(0, src*s + t), src at 2x resolution
-    PRO_BNBWD = 3,      // x = a*(dz - mb - (y - mean)*mgi)   src=dz, src2=y   (cf = {a,mb,mgi,mean})
 };
 // What a conv kernel does with its accumulator tile:
 enum Epilogue {
@@ -48,10 +46,9 @@ struct ConvArgs {
     int accumulate;       // EPI_BWD_STORE: add into out instead of overwriting
 };
 
-int launch_conv3x3(int pro, int epi, ConvArgs a, hipStream_t s);
 size_t conv3x3_nblk(int B, int H, int W, int cout);
-// Same GEMM with raw rows DMA'd (global_load_lds, double-buffered) and the prologue applied at
-// operand-read time (conv_dma.hip).  Prologues PRO_RAW, PRO_BNRELU, PRO_BNBWD.
+// Raw rows DMA'd into LDS (global_load_lds, double-buffered), the prologue applied at operand-read
+// time (conv_dma.hip).  Prologues PRO_RAW, PRO_BNRELU.
 int launch_conv3x3_dma(int pro, int epi, ConvArgs a, hipStream_t s);
 // materialised block tail x = drop * maxpool2(relu(y*s + t)) (feeds PRO_RAW convs)
 int launch_bn_relu_pool(const float* y, const float4* cf, const float* drop, float* x, int B, int C,
@@ -88,14 +85,8 @@ struct WgradArgs {
     int MT, NPM, NPC;     // MFMA tile (16 or 32), tiles per block along cout / cin
     int VX;               // wgrad_win: vector width of the x staging
     int KW, ntslice;      // wgrad_w32: waves splitting K on one tile, task slices (nslice = ntslice * KW)
-    int expt;             // timing experiments only (PCX_WGRAD_EXPT): 1 no staging, 2 no MFMA, 4 no barrier
 };
-int launch_wgrad3x3(int pro, WgradArgs a, hipStream_t s);
-void wgrad3x3_geometry(int B, int H, int W, int cin, int cout, WgradArgs* a);
-// software-pipelined variant (wgrad_pipe.hip, the default): prologues PRO_RAW / PRO_BNRELU
-int launch_wgrad_pipe(int pro, WgradArgs a, hipStream_t s);
-void wgrad_pipe_geometry(int B, int H, int W, int cin, int cout, WgradArgs* a);
-// sliding-row-window variant (wgrad_win.hip, the default): prologues PRO_RAW / PRO_BNRELU
+// sliding-row-window weight gradient on 16 x 16 tiles (wgrad_win.hip): prologues PRO_RAW / PRO_BNRELU
 int launch_wgrad_win(int pro, WgradArgs a, hipStream_t s);
 // same row window on 32 x 32 tiles (wgrad_w32.hip; channels multiples of 32): false if it does not apply
 bool wgrad_w32_geometry(int B, int H, int W, int cin, int cout, WgradArgs* a);

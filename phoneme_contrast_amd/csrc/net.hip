@@ -61,12 +61,8 @@ int build_small(Plan& p) {
             L.wp = p.carve("wp", (size_t)9 * L.cin * L.cout * 4);
             L.wpd = p.carve("wpd", (size_t)9 * L.cin * L.cout * 4);
             L.nblk = (int)conv3x3_nblk(B, L.H, L.W, L.cout);
-            if (p.wgrad_impl == 0) {
-                if (!wgrad_w32_geometry(B, L.H, L.W, L.cin, L.cout, &L.wg))
-                    wgrad_win_geometry(B, L.H, L.W, L.cin, L.cout, &L.wg);
-            } else if (p.wgrad_impl == 3) wgrad_win_geometry(B, L.H, L.W, L.cin, L.cout, &L.wg);
-            else if (p.wgrad_impl == 1) wgrad_pipe_geometry(B, L.H, L.W, L.cin, L.cout, &L.wg);
-            else wgrad3x3_geometry(B, L.H, L.W, L.cin, L.cout, &L.wg);
+            if (!wgrad_w32_geometry(B, L.H, L.W, L.cin, L.cout, &L.wg))
+                wgrad_win_geometry(B, L.H, L.W, L.cin, L.cout, &L.wg);
             wg = std::max(wg, (size_t)L.wg.nslice * L.cout * L.cin * 9);
         } else {
             L.nblk = conv1_nblk(B, L.H, &p.conv1_rows);
@@ -108,6 +104,10 @@ int build_small(Plan& p) {
     p.hp_dwa = p.carve("hp_dwa", (size_t)K * B * 4);
     p.hp_dba = p.carve("hp_dba", (size_t)B * 4);
     p.nparams = p.cfg.use_attention ? 30 : 28;
+    // backward completion points: projection, attention, then conv layers 6..1
+    p.stages = {p.cfg.use_attention ? 26 : 24};
+    if (p.cfg.use_attention) p.stages.push_back(24);
+    for (int l = 6; l >= 1; --l) p.stages.push_back(p_conv_w(l));
     p.nbn = 7;
     p.ndrop = 3;
     p.drop_ch[0] = 32; p.drop_ch[1] = 64; p.drop_ch[2] = 128;
@@ -179,21 +179,18 @@ int small_forward(const Plan& p, const float* const* P, float* const* bnstat, in
         c.part1 = part + (size_t)L.cout * L.nblk;
         c.partn = part + (size_t)2 * L.cout * L.nblk;
         c.nblk = L.nblk;
-        if (p.dma) {
-            int pro = PRO_BNRELU;
-            if (L.pooled_in) {  // block tail materialised once; the conv and its wgrad read it raw
-                Scope sc(&p.prof, s, "bn_relu_pool", l);
-                RC(launch_bn_relu_pool(c.src, c.cf_in, c.drop_in, at<float>(ws, L.xp), B, L.cin, L.srcH,
-                                       L.srcW, s));
-                c.src = at<float>(ws, L.xp);
-                c.srcH = L.H; c.srcW = L.W;
-                pro = PRO_RAW;
-            }
+        int pro = PRO_BNRELU;
+        if (L.pooled_in) {  // block tail materialised once; the conv and its wgrad read it raw
+            Scope sc(&p.prof, s, "bn_relu_pool", l);
+            RC(launch_bn_relu_pool(c.src, c.cf_in, c.drop_in, at<float>(ws, L.xp), B, L.cin, L.srcH,
+                                   L.srcW, s));
+            c.src = at<float>(ws, L.xp);
+            c.srcH = L.H; c.srcW = L.W;
+            pro = PRO_RAW;
+        }
+        {
             Scope sc(&p.prof, s, "conv_fwd", l);
             RC(launch_conv3x3_dma(pro, EPI_FWD, c, s));
-        } else {
-            Scope sc(&p.prof, s, "conv_fwd", l);
-            RC(launch_conv3x3(L.pooled_in ? PRO_BNRELU_POOL : PRO_BNRELU, EPI_FWD, c, s));
         }
         RC(finalize(l));
     }
@@ -245,6 +242,7 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
     float* part = at<float>(ws, p.stat_part);
     float* wgp = at<float>(ws, p.wg_part);
     const int ia = 24, ip = p.cfg.use_attention ? 26 : 24;
+    p.buckets.begin();
 
     // projection / BN1d / normalize backward
     {
@@ -269,6 +267,7 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
         j.part = at<float>(ws, p.proj_part);
         { Scope sc(&p.prof, s, "proj_bwd"); RC(launch_proj_bwd(j, s)); }
     }
+    p.buckets.mark(ip, s);
     // attention + pool + Dropout2d + ReLU backward -> dz6 and BN6 partials
     {
         HeadPoolArgs h{};
@@ -289,6 +288,7 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
         if (p.cfg.use_attention) {
             RC(launch_row_sum(h.p_dwa, p.C6, B, G[ia], s));
             RC(launch_row_sum(h.p_dba, 1, B, G[ia + 1], s));
+            p.buckets.mark(ia, s);
         }
     }
     auto bwd_finalize = [&](int l, int nblk, double count) {
@@ -326,21 +326,19 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
             w.drop = L.pooled_in ? dmask[L.drop_idx] : nullptr;
             w.srcH = L.srcH; w.srcW = L.srcW;
             w.part = wgp;
-            int pro = L.pooled_in ? PRO_BNRELU_POOL : PRO_BNRELU;
-            if (p.dma && L.pooled_in) {  // pooled input materialised by the forward
+            int pro = PRO_BNRELU;
+            if (L.pooled_in) {  // pooled input materialised by the forward
                 w.src = at<float>(ws, L.xp);
                 w.srcH = L.H; w.srcW = L.W;
                 pro = PRO_RAW;
             }
-            if (p.dma) w.dy_out = at<float>(ws, p.dyb);
-            if (const char* e = getenv("PCX_WGRAD_EXPT")) w.expt = atoi(e);
+            w.dy_out = at<float>(ws, p.dyb);
             {
                 Scope sc(&p.prof, s, "wgrad", l);
-                RC(p.wgrad_impl == 0 || p.wgrad_impl == 3
-                       ? (w.MT == 32 ? launch_wgrad_w32(pro, w, s) : launch_wgrad_win(pro, w, s))
-                   : p.wgrad_impl == 1 ? launch_wgrad_pipe(pro, w, s) : launch_wgrad3x3(pro, w, s));
+                RC(w.MT == 32 ? launch_wgrad_w32(pro, w, s) : launch_wgrad_win(pro, w, s));
             }
             { Scope sc(&p.prof, s, "wgrad_reduce", l); RC(launch_sum_slices(wgp, w.nslice, (int64_t)L.cout * L.cin * 9, G[p_conv_w(l)], s)); }
+            p.buckets.mark(p_conv_w(l), s);  // BN l's dgamma / dbeta came with layer l+1's data gradient
         }
         // ---- data gradient -> dz of the previous BN (through ReLU / MaxPool / Dropout2d)
         {
@@ -354,7 +352,7 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
             c.src = at<float>(ws, L.dz);
             c.src2 = at<float>(ws, L.y);
             c.cf_in = at<float4>(ws, L.cfb);
-            if (p.dma) c.src = at<float>(ws, p.dyb);  // dy materialised by the weight gradient
+            c.src = at<float>(ws, p.dyb);  // dy = BN backward of (dz, y), materialised by the weight gradient
             c.srcH = L.H; c.srcW = L.W;
             c.wpack = at<float>(ws, L.wpd);
             c.out = dzp;
@@ -369,7 +367,7 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
             {
                 Scope sc(&p.prof, s, "conv_dgrad", l);
                 const int epi = L.pooled_in ? EPI_BWD_POOL : EPI_BWD_RELU;
-                RC(p.dma ? launch_conv3x3_dma(PRO_RAW, epi, c, s) : launch_conv3x3(PRO_BNBWD, epi, c, s));
+                RC(launch_conv3x3_dma(PRO_RAW, epi, c, s));
             }
             RC(bwd_finalize(l - 1, nblk, (double)B * Lp.H * Lp.W));
         }
@@ -390,6 +388,7 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
         { Scope sc(&p.prof, s, "wgrad", 1); RC(launch_wgrad1(w, s)); }
         RC(launch_sum_slices(wgp, w.nslice, (int64_t)L.cout * 9, G[p_conv_w(1)], s));
     }
+    p.buckets.mark(0, s);
     return PCX_OK;
 }
 
@@ -414,14 +413,6 @@ extern "C" void* pcx_net_create(const pcx_net_config* cfg, int64_t B, int64_t F,
     p->cfg = *cfg;
     p->B = (int)B; p->F = (int)F; p->T = (int)T; p->D = cfg->embedding_dim;
     p->total = 0;
-    {
-        const char* impl = getenv("PCX_CONV");  // A/B switch for measurements: "legacy" = conv.hip
-        p->dma = !(impl && strcmp(impl, "legacy") == 0);
-        const char* wg = getenv("PCX_WGRAD");  // "dma" / "legacy" for A/B measurements
-        p->wgrad_impl = (!p->dma || (wg && strcmp(wg, "legacy") == 0)) ? 2
-                        : (wg && strcmp(wg, "pipe") == 0) ? 1
-                        : (wg && strcmp(wg, "win16") == 0) ? 3 : 0;
-    }
     int rc = PCX_EINVAL;
     if (cfg->kind == PCX_NET_CNN_SMALL && cfg->conv_bf16)
         set_error("pcx_net_create: conv_bf16 is a PhonemeNetDeep option (cnn_small is float32)");
@@ -488,6 +479,51 @@ extern "C" int pcx_net_backward(const void* plan, const float* const* params, co
     if (ws_bytes < p->total) { set_error("pcx_net_backward: workspace too small"); return PCX_EWORKSPACE; }
     if (p->deep) return deep_backward(*p, params, x, dropout, emb, d_emb, grads, ws, stream);
     return small_backward(*p, params, x, dropout, emb, d_emb, grads, ws, stream);
+}
+
+extern "C" int pcx_net_grad_buckets(void* plan, int n, const int* first_param) {
+    using namespace pcx;
+    PCX_CHECK_ARG(plan && n >= 0 && (n == 0 || first_param), "pcx_net_grad_buckets: bad argument");
+    Plan* p = static_cast<Plan*>(plan);
+    for (int k = 0; k < n; ++k) {
+        const int hi = k ? first_param[k - 1] : p->nparams;
+        PCX_CHECK_ARG(first_param[k] >= 0 && first_param[k] < hi, "pcx_net_grad_buckets: first_param[%d] = %d not in [0, %d)",
+                      k, first_param[k], hi);
+    }
+    PCX_CHECK_ARG(n == 0 || first_param[n - 1] == 0, "pcx_net_grad_buckets: the last bucket must start at parameter 0");
+    p->buckets.clear();
+    for (int k = 0; k < n; ++k) {
+        hipEvent_t e;
+        hipError_t err = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+        if (err != hipSuccess) {
+            p->buckets.clear();
+            return hip_status(err, "pcx_net_grad_buckets");
+        }
+        p->buckets.ev.push_back(e);
+        p->buckets.first.push_back(first_param[k]);
+    }
+    p->buckets.fired.assign(n, 0);
+    return PCX_OK;
+}
+
+extern "C" int pcx_net_bucket_wait(void* plan, int k, hipStream_t stream) {
+    using namespace pcx;
+    PCX_CHECK_ARG(plan, "pcx_net_bucket_wait: NULL plan");
+    Plan* p = static_cast<Plan*>(plan);
+    PCX_CHECK_ARG(k >= 0 && k < (int)p->buckets.ev.size(), "pcx_net_bucket_wait: bucket %d of %d", k,
+                  (int)p->buckets.ev.size());
+    PCX_CHECK_ARG(p->buckets.fired[k], "pcx_net_bucket_wait: bucket %d was not recorded by a backward", k);
+    return hip_status_ok(hipStreamWaitEvent(stream, p->buckets.ev[k], 0), "pcx_net_bucket_wait");
+}
+
+extern "C" int pcx_net_grad_stages(const void* plan, int* first_param, int max_entries) {
+    using namespace pcx;
+    PCX_CHECK_ARG(plan, "pcx_net_grad_stages: NULL plan");
+    const Plan* p = static_cast<const Plan*>(plan);
+    const int n = (int)p->stages.size();
+    for (int i = 0; i < n && i < max_entries; ++i)
+        if (first_param) first_param[i] = p->stages[i];
+    return n;
 }
 
 extern "C" int pcx_net_profile(void* plan, int enable) {

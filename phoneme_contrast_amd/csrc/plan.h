@@ -63,6 +63,30 @@ struct Scope {
     }
 };
 
+// Gradient buckets (pcx_net_grad_buckets): events recorded during the backward once every
+// gradient of a bucket is written, so a DDP all-reduce can start behind the remaining layers.
+struct GradBuckets {
+    std::vector<int> first;          // descending parameter indices: bucket k = [first[k], first[k-1])
+    std::vector<hipEvent_t> ev;
+    std::vector<char> fired;
+    void clear() {
+        for (auto e : ev) (void)hipEventDestroy(e);
+        ev.clear();
+        first.clear();
+        fired.clear();
+    }
+    void begin() { fired.assign(first.size(), 0); }
+    // every parameter with index >= low has its final gradient on stream s
+    void mark(int low, hipStream_t s) {
+        for (size_t k = 0; k < first.size(); ++k)
+            if (!fired[k] && first[k] >= low) {
+                (void)hipEventRecord(ev[k], s);
+                fired[k] = 1;
+            }
+    }
+    ~GradBuckets() { clear(); }
+};
+
 struct Layer {  // one 3x3 conv of the trunk (L = 1..6)
     int cin, cout, H, W;   // conv resolution
     int srcH, srcW;        // resolution of the tensor its prologue reads
@@ -91,10 +115,9 @@ struct Plan {
     size_t total;
     std::vector<Region> regions;
     int nparams, nbn, ndrop, drop_ch[4];
-    bool dma;                       // LDS-DMA conv path (default); PCX_CONV=legacy selects conv.hip
-    int wgrad_impl;                 // 0 row window, 32x32 tiles where they apply (default), 1 pipelined
-                                    // chunks, 2 wgrad.hip, 3 row window on 16x16 tiles (PCX_WGRAD)
     mutable Profiler prof;
+    mutable GradBuckets buckets;
+    std::vector<int> stages;        // parameter indices at which the backward completes a stage
 
     size_t carve(const char* name, size_t bytes) {
         size_t off = total;

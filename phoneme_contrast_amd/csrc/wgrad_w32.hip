@@ -213,21 +213,6 @@ bool wgrad_w32_geometry(int B, int H, int W, int cin, int cout, WgradArgs* a) {
                 if (cost < bcost) { bcost = cost; best = {TM, TN, cw, vx}; }
             }
     }
-    // tuning override "cin,cout,TM,TN,CW,VX[;...]" per layer shape; TM = 0 selects the 16x16 kernel
-    if (const char* e = getenv("PCX_WG32")) {
-        for (const char* q = e; q && *q; q = strchr(q, ';') ? strchr(q, ';') + 1 : nullptr) {
-            int ci, co;
-            W32Cfg o{};
-            if (sscanf(q, "%d,%d,%d,%d,%d,%d", &ci, &co, &o.TM, &o.TN, &o.CW, &o.VX) != 6 || ci != cin || co != cout)
-                continue;
-            if (o.TM == 0) return false;
-            if (o.TM * o.TN >= 1 && 4 % (o.TM * o.TN) == 0 && cout % (32 * o.TM) == 0 && cin % (32 * o.TN) == 0 &&
-                w32_fits(o.TM, o.TN, o.CW, o.VX, W))
-                best = o;
-        }
-    }
-    if (getenv("PCX_WG32_LOG"))
-        fprintf(stderr, "wgrad_w32 %dx%d W=%d: tiles %dx%d CW %d VX %d\n", cin, cout, W, best.TM, best.TN, best.CW, best.VX);
     if (!best.TM) return false;
     a->MT = 32;
     a->NPM = best.TM;

@@ -166,21 +166,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
         for (int r = 0; r < a.H; ++r) {
             const bool pre = r + 1 < a.H;
             const bool prex = r + 2 < a.H;  // row H is never read (bottom-row taps are skipped)
-            if (pre && !(a.expt & 1)) st.load_dy(a, g, wk, dzb, yb, w0, r + 1, NB);
-            if (prex && !(a.expt & 1)) st.load_x(a, g, wk, xb, w0, r + 2, CB);
+            if (pre) st.load_dy(a, g, wk, dzb, yb, w0, r + 1, NB);
+            if (prex) st.load_x(a, g, wk, xb, w0, r + 2, CB);
             const float* dyt = lds + (r & 1) * g.dyslot;
             const float* xr0 = lds + g.xbase + (r & 3) * g.xslot;
             const float* xr1 = lds + g.xbase + ((r + 1) & 3) * g.xslot;
             const float* xr2 = lds + g.xbase + ((r + 2) & 3) * g.xslot;
             const bool top = r == 0, bot = r + 1 == a.H;
-            if (a.expt & 2) {}
-            else if (!top && !bot) row_mfma<PW, 7>(acc, dyt, xr0, xr1, xr2, ao, xo, kend);
+            if (!top && !bot) row_mfma<PW, 7>(acc, dyt, xr0, xr1, xr2, ao, xo, kend);
             else if (top && !bot) row_mfma<PW, 6>(acc, dyt, xr0, xr1, xr2, ao, xo, kend);
             else if (!top && bot) row_mfma<PW, 3>(acc, dyt, xr0, xr1, xr2, ao, xo, kend);
             else row_mfma<PW, 2>(acc, dyt, xr0, xr1, xr2, ao, xo, kend);
-            if (pre && !(a.expt & 1)) st.store_dy(a, g, wk, tid, lds, cfd, dyo, w0, r + 1, (r + 1) & 1, NB);
-            if (prex && !(a.expt & 1)) st.store_x(a, g, wk, tid, lds, cfx, w0, (r + 3) & 3, CB);
-            if (!(a.expt & 4)) __syncthreads();
+            if (pre) st.store_dy(a, g, wk, tid, lds, cfd, dyo, w0, r + 1, (r + 1) & 1, NB);
+            if (prex) st.store_x(a, g, wk, tid, lds, cfx, w0, (r + 3) & 3, CB);
+            __syncthreads();
         }
     }
     float* out = a.part + (int64_t)slice * a.cout * a.cin * 9;

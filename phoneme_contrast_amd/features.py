@@ -105,6 +105,8 @@ class _MelBase(FeatureExtractor):
     def _prep(self, waveform, gain):
         wave = _as_batch(waveform)
         _lib.require_gpu(wave, gain, what=type(self).__name__)
+        if self.fb_padded.device != wave.device:  # the filterbank / DCT buffers follow the input
+            self.to(wave.device)
         wave = wave.contiguous().float()
         if gain is not None:
             gain = gain.reshape(-1).contiguous().float()

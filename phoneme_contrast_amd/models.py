@@ -126,6 +126,7 @@ class _NativeNet(BaseModel):
         self._plans = {}
         self._next_masks = None
         self.last_dropout_masks = None
+        self._grad_bucketer = None
 
     # --- configuration handed to the native plan
     def _net_config(self) -> "_lib.NetConfig":
@@ -246,11 +247,16 @@ class _NativeNet(BaseModel):
             off += n
         da = _ptr_array(masks) if masks is not None else None
         g_emb = demb.contiguous().float()  # held until the launch is enqueued
+        bucketer = getattr(self, "_grad_bucketer", None)
+        if bucketer is not None:
+            bucketer.prepare(plan)
         _lib.check(lib.pcx_net_backward(plan.handle, _ptr_array([p.detach() for p in params]),
                                         _lib.ptr(x), da, _lib.ptr(emb),
                                         _lib.ptr(g_emb), _ptr_array(grads),
                                         _lib.ptr(ws), plan.ws_bytes, _lib.stream_of(x)),
                    "pcx_net_backward")
+        if bucketer is not None:  # DDP: bucket all-reduces start behind the layers still running
+            bucketer.launch(plan, flat)
         return grads
 
     # initialisation shared by both nets (reference phoneme_cnn.py:79-96, :259-272)

@@ -40,11 +40,19 @@ class FusedAdam(torch.optim.Optimizer):
         v = torch.zeros(n, device=dev, dtype=torch.float32)
         step = 0
         off = 0
+        # parameters re-bound behind the optimizer's back (model.to(), load_state_dict(assign=True)):
+        # the moments and step count of the previous flat buffers carry over; state loaded through
+        # load_state_dict (which drops the flat buffers) comes from self.state
+        prev = st if st is not None and st["n"] == n else None
         for p in ps:
             k = p.numel()
             flat[off:off + k].copy_(p.detach().reshape(-1))
             s = self.state.get(p)
-            if s and "exp_avg" in s:  # carry over state loaded through load_state_dict
+            if prev is not None:
+                m[off:off + k].copy_(prev["m"][off:off + k])
+                v[off:off + k].copy_(prev["v"][off:off + k])
+                step = prev["step"]
+            elif s and "exp_avg" in s:
                 m[off:off + k].copy_(s["exp_avg"].reshape(-1))
                 v[off:off + k].copy_(s["exp_avg_sq"].reshape(-1))
                 step = int(s["step"])
@@ -69,7 +77,9 @@ class FusedAdam(torch.optim.Optimizer):
         """The group's gradients as one flat tensor: a zero-copy view when the backward produced
         them contiguously in parameter order (libpcx does), else one gather copy."""
         g0 = ps[0].grad
-        if g0 is not None and g0.is_contiguous():
+        # zero-copy only when the view starts 16-byte aligned (pcx_adam_step's vector loads): a
+        # second parameter group's gradients can sit at any offset of the backward's flat buffer
+        if g0 is not None and g0.is_contiguous() and g0.data_ptr() % 16 == 0:
             base, sto = g0.data_ptr(), g0.untyped_storage().data_ptr()
             off, ok = 0, True
             for p in ps:

@@ -8,8 +8,9 @@ defaults apply (SURVEY finding 4).  Kept on purpose so results match the referen
 
 MI355X additions (all optional, no behaviour change for a single process):
   * data parallel: with torch.distributed initialised and world_size > 1 the flat gradient is
-    all-reduced once per step (RCCL) and averaged inside the fused Adam (phoneme_contrast_amd.
-    distributed); the DataLoader is expected to hand each rank its own shard.
+    all-reduced (RCCL; bucketed behind the backward with distributed.GradBucketer) and averaged
+    inside the fused Adam (phoneme_contrast_amd.distributed); the DataLoader is expected to hand
+    each rank its own shard (scripts/train.py: ShardedBatchSampler).
   * FusedAdam fast path: when the optimizer is a FusedAdam the all-reduced flat buffer is passed
     straight to its single-kernel step.
 """
@@ -109,15 +110,32 @@ class ContrastiveTrainer:
         return {"loss": total_loss / max(num_batches, 1), "lr": self.optimizer.param_groups[0]["lr"]}
 
     def _reduce_clip_step(self):
-        """(all-reduce) -> (clip) -> optimizer step, in the reference's order (trainer.py:143-152)."""
+        """(all-reduce) -> (clip) -> optimizer step, in the reference's order (trainer.py:143-152).
+
+        FusedAdam over every model parameter: the gradients stay in the backward's flat buffer
+        (zero-copy views); with world_size > 1 it is summed by RCCL (in buckets behind the
+        backward when a GradBucketer is attached) and the 1/world average is folded into the
+        Adam kernel; clipping scales the summed buffer by min(1, clip / (||avg|| + 1e-6)) on the
+        device (torch.nn.utils.clip_grad_norm_'s rule, no host sync).  Any other optimizer: the
+        averaged gradient is written back into p.grad and torch's own clip / step run."""
         from .optim import FusedAdam
         clip = self.config.get("gradient_clip_val")
-        fused = isinstance(self.optimizer, FusedAdam)
-        if self.world_size > 1 and fused and not clip:
-            flats = self.optimizer.flat_grad_views()  # zero-copy views of p.grad when contiguous
-            for f in flats:
-                ddp.allreduce_flat(f)
-            self.optimizer.step(flat_grads=flats, grad_scale=1.0 / self.world_size)
+        opt = self.optimizer
+        if isinstance(opt, FusedAdam) and ddp.covers(opt, self.model):
+            flats, scale = None, 1.0
+            if self.world_size > 1:
+                bucketer = getattr(self.model, "_grad_bucketer", None)
+                flats = bucketer.finish() if bucketer is not None and bucketer.pending() else None
+                if flats is None:
+                    flats = opt.flat_grad_views()
+                    for f in flats:
+                        ddp.allreduce_flat(f)
+                scale = 1.0 / self.world_size
+            if clip:
+                if flats is None:
+                    flats = opt.flat_grad_views()
+                ddp.clip_flat_(flats, float(clip), scale)
+            opt.step(flat_grads=flats, grad_scale=scale)
             return
         if self.world_size > 1:  # generic path: leave the AVERAGED gradient in p.grad
             grads = [p.grad for p in self.model.parameters() if p.grad is not None]
@@ -130,7 +148,7 @@ class ContrastiveTrainer:
                 off += g.numel()
         if clip:
             torch.nn.utils.clip_grad_norm_(self.model.parameters(), clip)
-        self.optimizer.step()
+        opt.step()
 
     def _validate(self) -> Dict[str, float]:
         self.model.eval()

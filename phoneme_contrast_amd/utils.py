@@ -20,7 +20,9 @@ def get_best_device(device_str: str = "auto", logger: Optional[logging.Logger] =
     if torch.cuda.is_available():
         n = torch.cuda.device_count()
         log(f"Found {n} ROCm GPU device(s)")
-        local = int(os.environ.get("LOCAL_RANK", "0"))
+        # N ranks rehearsed on fewer GPUs (PCX_DIST_BACKEND=gloo) share them round-robin
+        from .distributed import local_device_index
+        local = local_device_index(int(os.environ.get("LOCAL_RANK", "0")), n)
         props = torch.cuda.get_device_properties(local)
         log(f"Selected GPU {local}: {props.name}")
         return torch.device(f"cuda:{local}")

@@ -18,10 +18,8 @@ DGRAD = [f"conv_dgrad_L{l}" for l in range(6, 1, -1)]
 # kernel family (name up to '<' / '(') -> layer labels in per-step dispatch order
 ORDER = {
     "conv3x3_dma_kernel": FWD + DGRAD,
-    "wgrad_pipe_kernel": [f"wgrad_L{l}" for l in range(6, 1, -1)],
     "wgrad_win_kernel": [f"wgrad_L{l}" for l in range(6, 1, -1)],
     "wgrad_w32_kernel": [f"wgrad_L{l}" for l in range(6, 3, -1)],
-    "wgrad3x3_kernel": [f"wgrad_L{l}" for l in range(6, 1, -1)],
     "bn_relu_pool_kernel": ["bn_relu_pool_L3", "bn_relu_pool_L5"],
     "conv1_fwd_kernel": ["conv1_fwd_L1"],
     "wgrad1_kernel": ["wgrad_L1"],
@@ -87,7 +85,9 @@ def durations(path):
     return {k: {"avg_ms": round(sum(v) / len(v), 4), "launches": len(v)} for k, v in out.items()}
 
 
-def main(prof_dir, out_json, out_dur=None):
+def main(prof_dir, out_json, out_dur=None, key="cnn_small/fp32"):
+    """Writes {key: {label: traffic}} into out_json (merged with the other workloads already
+    there: bench.py looks traffic up by (model, precision, label))."""
     fetch = counters(f"{prof_dir}/pmc_fetch/run_counter_collection.csv", "FETCH_SIZE")
     write = counters(f"{prof_dir}/pmc_write/run_counter_collection.csv", "WRITE_SIZE")
     res = {}
@@ -97,8 +97,14 @@ def main(prof_dir, out_json, out_dur=None):
         res[lab] = {"fetch_size_kb": f, "write_size_kb": w,
                     "hbm_bytes_per_launch": int(2 * f * 1024 + w * 1024),
                     "note": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE half-count correction)"}
+    try:
+        with open(out_json) as fi:
+            allres = json.load(fi)
+    except (OSError, ValueError):
+        allres = {}
+    allres[key] = res
     with open(out_json, "w") as fo:
-        json.dump(res, fo, indent=1)
+        json.dump(allres, fo, indent=1)
     print(json.dumps(res, indent=1))
     if out_dur:
         d = durations(f"{prof_dir}/trace/run_kernel_trace.csv")
@@ -131,4 +137,4 @@ if __name__ == "__main__":
     if sys.argv[1] == "--stalls":
         stalls(sys.argv[2], sys.argv[3])
     else:
-        main(*sys.argv[1:4])
+        main(*sys.argv[1:5])

@@ -7,9 +7,15 @@
 Same flow as the reference (scripts/train.py:24-200): compose the config, logger, seeds, device,
 system adjustment, data, model from the registry, Adam (+ cosine schedule), loss from the loss
 registry, ContrastiveTrainer.train.  Differences: the model / loss / optimizer step run in the
-MI355X kernels (phoneme_contrast_amd), torchrun launches data-parallel training (one process
-per GPU, gradients all-reduced over RCCL), and `accel.synthetic_data=true` trains on synthetic
-MFCC views when the WAV dataset (and its torchaudio MFCC pipeline) is not available.
+MI355X kernels (phoneme_contrast_amd); the data path keeps the clips in HBM and builds the
+MFCC / SpecAugment views on the GPU (phoneme_contrast_amd.data) with the reference's sampler;
+torchrun launches data-parallel training (one process per GPU, gradients all-reduced over RCCL
+in buckets behind the backward); `accel.synthetic_data=true` trains on synthetic clips when the
+WAV dataset is not available.  The per-rank batch is classes_per_batch x samples_per_class x
+views_per_sample embeddings, e.g. the BASELINE's 4096 per GPU:
+
+    python scripts/train.py accel.synthetic_data=true accel.synthetic.num_classes=20000 \
+        data.contrastive.classes_per_batch=1024
 """
 import os
 import sys
@@ -19,96 +25,75 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 
 import torch  # noqa: E402
-from torch.utils.data import DataLoader, Dataset, Sampler  # noqa: E402
-
 from phoneme_contrast_amd import config as cfglib  # noqa: E402
 from phoneme_contrast_amd import distributed as ddp  # noqa: E402
+from phoneme_contrast_amd.data import (GpuContrastiveBatches, GpuEvalBatches, ShardedBatchSampler,  # noqa: E402
+                                       WaveformStore, parse_dataset)
+from phoneme_contrast_amd.features import GpuViewBuilder, build_feature_extractor  # noqa: E402
 from phoneme_contrast_amd.losses import get_loss_fn  # noqa: E402
 from phoneme_contrast_amd.models import model_registry  # noqa: E402
 from phoneme_contrast_amd.optim import FusedAdam  # noqa: E402
+from phoneme_contrast_amd.samplers import ContrastiveBatchSampler  # noqa: E402
 from phoneme_contrast_amd.trainer import ContrastiveTrainer  # noqa: E402
+from phoneme_contrast_amd.transforms import build_augmentation_pipeline  # noqa: E402
 from phoneme_contrast_amd.utils import adjust_params_for_system, create_logger, get_best_device  # noqa: E402
 
 
-class SyntheticMFCCDataset(Dataset):
-    """Random MFCC 'clips' with the reference dataset's item format: {'views': [V,1,40,T] (train) or
-    [1,40,T] (val), 'label': int, 'index': int} (reference src/datasets/dataset.py:65-111)."""
-
-    def __init__(self, n_items, n_classes, n_mfcc, n_frames, views, mode, seed):
-        self.labels = [i % n_classes for i in range(n_items)]
-        self.n_mfcc, self.n_frames, self.views, self.mode, self.seed = n_mfcc, n_frames, views, mode, seed
-
-    def __len__(self):
-        return len(self.labels)
-
-    def __getitem__(self, idx):
-        g = torch.Generator().manual_seed(self.seed * 100003 + idx)
-        base = torch.randn(1, self.n_mfcc, self.n_frames, generator=g)
-        if self.mode == "train":
-            views = torch.stack([base + 0.1 * torch.randn(base.shape, generator=g) for _ in range(self.views)])
-        else:
-            views = base
-        return {"views": views, "label": self.labels[idx], "index": idx}
-
-
-class ClassBalancedBatchSampler(Sampler):
-    """K classes x M samples per batch (views are added by the dataset), shuffled per epoch, each
-    rank drawing its own batches (reference src/datasets/samplers.py:84-118 layout)."""
-
-    def __init__(self, labels, classes_per_batch, samples_per_class, seed, rank=0, world=1):
-        self.by_class = {}
-        for i, l in enumerate(labels):
-            self.by_class.setdefault(l, []).append(i)
-        self.K, self.M, self.seed, self.rank, self.world = classes_per_batch, samples_per_class, seed, rank, world
-        self.epoch = 0
-
-    def __len__(self):
-        return len(self.by_class) // self.K // self.world
-
-    def __iter__(self):
-        g = torch.Generator().manual_seed(self.seed + self.epoch)
-        self.epoch += 1
-        classes = list(self.by_class)
-        order = torch.randperm(len(classes), generator=g).tolist()
-        batches = []
-        for s in range(0, len(order) - self.K + 1, self.K):
-            idx = []
-            for ci in order[s:s + self.K]:
-                pool = self.by_class[classes[ci]]
-                pick = torch.randint(0, len(pool), (self.M,), generator=g).tolist()
-                idx += [pool[p] for p in pick]
-            batches.append(idx)
-        for b in batches[self.rank::self.world][:len(self)]:
-            yield b
-
-
-def setup_data(cfg, logger, rank, world):
-    if not cfg.accel.get("synthetic_data", False):
-        raise NotImplementedError(
-            "WAV -> MFCC -> SpecAugment data path (reference src/datasets) is not part of this "
-            "build yet (it needs torchaudio on the host; the on-GPU MFCC kernels are the next row "
-            "of the plan).  Run with accel.synthetic_data=true.")
-    s = cfg.accel.synthetic
-    n_items = s.num_classes * s.samples_per_class
-    n_mfcc = cfg.data.feature_extractor.mfcc_params.n_mfcc
+def setup_data(cfg, logger, rank, world, device):
+    """Reference scripts/train.py:24-117 on the GPU data path (phoneme_contrast_amd.data):
+    parse the WAV tree (or build synthetic clips: accel.synthetic_data=true), the same seeded
+    85/15 randperm split, waveforms resident in HBM, the reference's ContrastiveBatchSampler
+    (sharded over ranks), views built on the GPU by GpuViewBuilder."""
+    fx = build_feature_extractor(dict(cfg.data.feature_extractor))
+    aug = build_augmentation_pipeline(dict(cfg.data.augmentation))
+    target_sr = cfg.data.get("target_sr", 16000)
+    max_samples = int(cfg.data.get("max_length_ms", 2000) * target_sr / 1000)
+    if cfg.accel.get("synthetic_data", False):
+        s = cfg.accel.synthetic
+        store = WaveformStore.synthetic(s.num_classes, s.samples_per_class, s.get("clip_samples", max_samples),
+                                        cfg.experiment.seed, device, target_sr)
+        labels, n_classes = store.labels, s.num_classes
+        logger.info(f"Synthetic data: {len(store)} clips of {store.waves.shape[1]} samples, {n_classes} classes")
+    else:
+        file_paths, labels, label_map, metadata = parse_dataset(Path(cfg.data.data_path), logger)
+        store, n_classes = None, len(label_map)
+    n_files = len(labels)
+    n_train = int(n_files * cfg.data.train_split)
+    indices = torch.randperm(n_files).tolist()  # the reference's split (seeded by experiment.seed)
+    train_idx, val_idx = indices[:n_train], indices[n_train:]
+    if store is not None:
+        train_store, val_store = store.subset(train_idx), store.subset(val_idx)
+        del store
+    else:
+        train_store = WaveformStore.from_files([file_paths[i] for i in train_idx], [labels[i] for i in train_idx],
+                                               [metadata[i] for i in train_idx], target_sr, max_samples, "train",
+                                               device)
+        val_store = WaveformStore.from_files([file_paths[i] for i in val_idx], [labels[i] for i in val_idx],
+                                             [metadata[i] for i in val_idx], target_sr, max_samples, "val", device)
     c = cfg.data.contrastive
-    n_train = int(n_items * cfg.data.train_split)
-    train = SyntheticMFCCDataset(n_train, s.num_classes, n_mfcc, s.n_frames, c.views_per_sample, "train",
-                                 cfg.experiment.seed)
-    val = SyntheticMFCCDataset(n_items - n_train, s.num_classes, n_mfcc, s.n_frames, 1, "val",
-                               cfg.experiment.seed + 1)
-    sampler = ClassBalancedBatchSampler(train.labels, c.classes_per_batch, c.samples_per_class,
-                                        cfg.experiment.seed, rank, world)
-    train_loader = DataLoader(train, batch_sampler=sampler, num_workers=0)
-    val_loader = DataLoader(val, batch_size=cfg.training.batch_size, shuffle=False, num_workers=0)
-    logger.info(f"Synthetic data: {len(train)} train / {len(val)} val clips, {s.num_classes} classes, "
-                f"{len(sampler)} batches per epoch per rank")
-    return train_loader, val_loader, s.num_classes
+    sampler = ContrastiveBatchSampler(labels=train_store.labels, classes_per_batch=c.classes_per_batch,
+                                      samples_per_class=c.samples_per_class, views_per_sample=c.views_per_sample,
+                                      shuffle=True, seed=cfg.experiment.seed, min_samples_to_exclude=0)
+    logger.info(f"Total unique classes in training: {len(set(train_store.labels))}")
+    logger.info(f"Classes in sampler: {len(sampler.valid_classes)}")
+    logger.info(f"Classes per batch: {c.classes_per_batch}")
+    logger.info(f"Samples per class: {c.samples_per_class}")
+    logger.info(f"Total batches per epoch: {len(sampler)}")
+    sharded = ShardedBatchSampler(sampler, rank, world)
+    train_loader = GpuContrastiveBatches(train_store, sharded,
+                                         GpuViewBuilder(fx, aug, c.views_per_sample, mode="train"))
+    val_loader = GpuEvalBatches(val_store, cfg.training.batch_size, GpuViewBuilder(fx, None, 1, mode="val"))
+    logger.info(f"Rank {rank}/{world}: {len(sharded)} batches per epoch of {c.classes_per_batch} classes x "
+                f"{c.samples_per_class} samples x {c.views_per_sample} views = "
+                f"{c.classes_per_batch * c.samples_per_class * c.views_per_sample} embeddings")
+    return train_loader, val_loader, n_classes
 
 
-def setup_model(cfg, device):
+def setup_model(cfg, device, world=1):
     model = model_registry.create(cfg.model.type, dict(cfg.model)).to(device)
     ddp.broadcast_module(model)
+    if world > 1:  # gradient all-reduce in buckets behind the native backward
+        ddp.GradBucketer(model, bucket_bytes=int(cfg.accel.get("bucket_mb", 4) * (1 << 20)))
     wd = cfg.training.get("weight_decay", 0)
     if cfg.accel.get("fused_adam", True):
         optimizer = FusedAdam(model.parameters(), lr=cfg.training.learning_rate, weight_decay=wd)
@@ -133,18 +118,39 @@ def main(cfg):
     torch.cuda.manual_seed_all(cfg.experiment.seed)
     device = get_best_device(cfg.get("device", "auto"), logger)
     cfg = adjust_params_for_system(cfg, device, logger)
-    train_loader, val_loader, num_classes = setup_data(cfg, logger, rank, world)
-    model, optimizer, scheduler, loss_fn = setup_model(cfg, device)
+    logger.info("Setting up data...")
+    train_loader, val_loader, num_classes = setup_data(cfg, logger, rank, world, device)
+    logger.info(f"Train batches: {len(train_loader)}, Val batches: {len(val_loader)}")
+    logger.info(f"Number of phoneme classes: {num_classes}")
+    logger.info("Setting up model...")
+    model, optimizer, scheduler, loss_fn = setup_model(cfg, device, world)
     trainer = ContrastiveTrainer(model=model, train_loader=train_loader, val_loader=val_loader,
                                  loss_fn=loss_fn, optimizer=optimizer, scheduler=scheduler,
                                  device=device, config=cfglib.to_container(cfg),
                                  output_dir=output_dir, logger=logger)
+    logger.info("Starting training...")
     trainer.train(num_epochs=cfg.training.epochs)
     logger.info("Training complete!")
     if world > 1:
         torch.distributed.destroy_process_group()
+    return trainer
+
+
+def cli():
+    """Hydra when it is installed (the reference's @hydra.main), else the compose shim."""
+    try:
+        import hydra
+        from omegaconf import OmegaConf
+    except ImportError:
+        overrides = [a for a in sys.argv[1:] if "=" in a]
+        return main(cfglib.compose(str(ROOT / "configs"), "config", overrides))
+
+    @hydra.main(version_base=None, config_path="../configs", config_name="config")
+    def _main(cfg):
+        return main(cfglib.wrap(OmegaConf.to_container(cfg, resolve=True)))
+
+    return _main()
 
 
 if __name__ == "__main__":
-    overrides = [a for a in sys.argv[1:] if "=" in a]
-    main(cfglib.compose(str(ROOT / "configs"), "config", overrides))
+    cli()

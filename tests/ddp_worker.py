@@ -1,0 +1,100 @@
+"""One rank of the data-parallel product path, run as a child process by tests/test_ddp_gpu.py.
+
+Each scenario: the HIP model (libpcx) forward + SupCon + backward on this rank's shard of a golden
+case, then ContrastiveTrainer._reduce_clip_step -- the trainer's own all-reduce (one flat
+collective, or GradBucketer buckets launched behind the native backward) + optional device-side
+clip + FusedAdam.step(flat_grads, grad_scale = 1/world) -- exactly the step order of the
+reference's _train_epoch (src/training/trainer.py:143-152).  Writes parameters, Adam moments and
+the loss of every scenario to <out_dir>/rank<r>.npz.
+
+    RANK=r WORLD_SIZE=2 MASTER_ADDR=127.0.0.1 MASTER_PORT=p PCX_DIST_BACKEND=gloo \
+        python tests/ddp_worker.py OUT_DIR
+"""
+import logging
+import os
+import sys
+import tempfile
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
+
+# (name, golden case, model config, bucketed, gradient_clip_val)
+SCENARIOS = [
+    ("small_flat", "cnn_small_T201", {"embedding_dim": 128, "use_attention": True, "dropout_rate": 0.1}, False, None),
+    ("small_bucket_clip", "cnn_small_T201", {"embedding_dim": 128, "use_attention": True, "dropout_rate": 0.1},
+     True, 0.05),
+    ("deep_flat", "cnn_deep_T200", {"embedding_dim": 128, "use_attention": True, "dropout_rate": 0.2,
+                                    "hidden_dims": [8, 16, 32, 64]}, False, None),
+    ("deep_bucket", "cnn_deep_T200", {"embedding_dim": 128, "use_attention": True, "dropout_rate": 0.2,
+                                      "hidden_dims": [8, 16, 32, 64]}, True, None),
+]
+
+
+def run(name, case, cfg, bucketed, clip, rank, world, out):
+    from golden_util import model_case
+    from phoneme_contrast_amd import distributed as ddp
+    from phoneme_contrast_amd.losses import SupervisedContrastiveLoss
+    from phoneme_contrast_amd.models import model_registry
+    from phoneme_contrast_amd.optim import FusedAdam
+    from phoneme_contrast_amd.trainer import ContrastiveTrainer
+
+    c = model_case(case)
+    kind = "phoneme_cnn_deep" if "deep" in case else "phoneme_cnn"
+    m = model_registry.create(kind, cfg)
+    state = {k: torch.tensor(v) for k, v in c["state0"].items()}
+    if rank == 1:  # the broadcast must overwrite a diverged replica
+        state = {k: v + 1.0 if v.is_floating_point() else v for k, v in state.items()}
+    m.load_state_dict(state)
+    m = m.cuda().train()
+    ddp.broadcast_module(m)
+    opt = FusedAdam(m.parameters(), lr=c["lr"], weight_decay=c["weight_decay"])
+    loss_fn = SupervisedContrastiveLoss(temperature=c["temperature"])
+    tmp = tempfile.mkdtemp(prefix=f"ddp_{name}_{rank}_")
+    trainer = ContrastiveTrainer(model=m, train_loader=[], val_loader=None, loss_fn=loss_fn, optimizer=opt,
+                                 scheduler=None, device=torch.device("cuda"),
+                                 config={"gradient_clip_val": clip} if clip else {}, output_dir=tmp,
+                                 logger=logging.getLogger("ddp_worker"))
+    assert trainer.world_size == world
+    bucketer = ddp.GradBucketer(m, bucket_bytes=1024) if bucketed else None
+    B = c["x"].shape[0]
+    lo, hi = ddp.shard(B, rank, world)
+    m.set_dropout_masks([torch.tensor(k[lo:hi]) for k in c["steps"][0]["masks"]])
+    x = torch.tensor(c["x"][lo:hi]).cuda()
+    labels = torch.tensor(c["labels"][lo:hi]).cuda()
+    loss = loss_fn(m(x), labels)
+    opt.zero_grad()
+    loss.backward()
+    nb = len(bucketer.buckets(next(iter(m._plans.values())))) if bucketer else 1
+    if not bucketer:  # this rank's own gradient, before the all-reduce
+        out[f"{name}/local"] = opt.flat_grad_views()[0].cpu().numpy().copy()
+    trainer._reduce_clip_step()
+    torch.cuda.synchronize()
+    st = opt._flat[0]
+    out[f"{name}/loss"] = np.array([loss.item()])
+    out[f"{name}/flat"] = st["flat"].cpu().numpy()
+    out[f"{name}/m"] = st["m"].cpu().numpy()
+    out[f"{name}/v"] = st["v"].cpu().numpy()
+    out[f"{name}/nbuckets"] = np.array([nb])
+    if bucketer:
+        bucketer.detach()
+
+
+def main():
+    out_dir = sys.argv[1]
+    from phoneme_contrast_amd import distributed as ddp
+    rank, world, local = ddp.init_from_env(backend="gloo")
+    torch.cuda.set_device(ddp.local_device_index(local, torch.cuda.device_count()))
+    out = {}
+    for sc in SCENARIOS:
+        run(*sc, rank, world, out)
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **out)
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+    print(f"rank {rank}: ok", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,181 @@
+"""The data-parallel product path on the GPU: world size 2 (gloo over the one GPU of the box),
+each rank a fresh child process running the HIP backward on its shard, the trainer's
+all-reduce (flat, or GradBucketer buckets overlapping the native backward) + clip + FusedAdam
+with grad_scale = 1/2 (tests/ddp_worker.py).
+
+Oracle (DDP-equivalent semantics): the float64 restatement run separately on each
+shard (its own BatchNorm statistics and SupCon negatives) and the per-shard gradients averaged.
+Checked: both ranks end bit-identical; the first Adam moment is exactly (1 - b1)((g0 + g1)/2 +
+wd p) of the two ranks' own gradients (the all-reduce and the 1/world scale); each rank's gradient
+matches its shard's float64 oracle, and the recovered average the oracle average, within 5e-3 *
+max|g| per tensor (BN-fed biases 1e-4 abs) -- looser than the 2e-3 of the 8-sample model tests
+because a 4-sample shard makes a ReLU / max-pool kink that flips at float32 resolution weigh
+more: measured 2.6e-3 on cnn_small_T201 shard 0, and the float32 torch port of the reference
+shows the same 1.4e-3 flips on shard 1 -- the second moment and the update are consistent with
+the first moment; with gradient_clip_val the clipped average (torch's clip_grad_norm_ rule);
+bucketed and flat all-reduce give bit-identical updates (cnn_deep, reduced widths)."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from golden_util import bn_fed_bias, model_case
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+B1, B2, EPS = 0.9, 0.999, 1e-8
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.fixture(scope="module")
+def ranks(tmp_path_factory):
+    out = tmp_path_factory.mktemp("ddp")
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), PCX_DIST_BACKEND="gloo")
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "ddp_worker.py"), str(out)],
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    logs = []
+    for p in procs:
+        try:
+            logs.append(p.communicate(timeout=240)[0])
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    for p, log in zip(procs, logs):
+        assert p.returncode == 0, log[-4000:]
+    return [dict(np.load(out / f"rank{r}.npz")) for r in range(2)]
+
+
+def _names_offsets(case, cfg):
+    from phoneme_contrast_amd.models import model_registry
+    m = model_registry.create("phoneme_cnn_deep" if "deep" in case else "phoneme_cnn", cfg)
+    out, off = {}, 0
+    for k, p in m.named_parameters():
+        out[k] = (off, p.numel(), tuple(p.shape))
+        off += p.numel()
+    return out
+
+
+def _oracle_avg_grads(case):
+    from oracle import np_models as nm
+    c = model_case(case)
+    B = c["x"].shape[0]
+    acc = None
+    for r in range(2):
+        lo, hi = r * B // 2, (r + 1) * B // 2
+        _, _, g, _, _ = nm.train_step(c["state0"], c["x"][lo:hi], c["labels"][lo:hi],
+                                      [k[lo:hi] for k in c["steps"][0]["masks"]], c["temperature"], 0.07,
+                                      c["lr"], c["weight_decay"])
+        acc = {k: v.copy() for k, v in g.items()} if acc is None else {k: acc[k] + g[k] for k in acc}
+    return {k: v / 2 for k, v in acc.items()}, c
+
+
+def _check(ranks, name, case, cfg, clip=None):
+    r0, r1 = ranks
+    for key in ("flat", "m", "v"):  # (the losses are per shard)
+        assert np.array_equal(r0[f"{name}/{key}"], r1[f"{name}/{key}"]), (name, key)
+    g_avg, c = _oracle_avg_grads(case)
+    if f"{name}/local" in r0:  # the reduce itself, exactly: m = (1-b1) * (0.5 * (g0 + g1) + wd p0)
+        p0_all = np.concatenate([c["state0"][k].reshape(-1) for k in _names_offsets(case, cfg)]).astype(np.float32)
+        gsum = (r0[f"{name}/local"] + r1[f"{name}/local"]).astype(np.float32)
+        m_ref = np.float32(1 - B1) * (np.float32(0.5) * gsum + np.float32(c["weight_decay"]) * p0_all)
+        assert np.allclose(r0[f"{name}/m"], m_ref, rtol=1e-5, atol=1e-12), name
+        assert not np.array_equal(r0[f"{name}/local"], r1[f"{name}/local"])  # the shards really differ
+    if clip:  # torch.nn.utils.clip_grad_norm_ on the averaged gradient, before the optimizer step
+        total = np.sqrt(sum((v.astype(np.float64) ** 2).sum() for v in g_avg.values()))
+        coef = min(1.0, clip / (total + 1e-6))
+        assert coef < 0.5, "clip must be active in this scenario"
+        g_avg = {k: v * coef for k, v in g_avg.items()}
+    lr, wd = c["lr"], c["weight_decay"]
+    m1, v1, p1 = (r0[f"{name}/{k}"].astype(np.float64) for k in ("m", "v", "flat"))
+    bad = {}
+    for k, (off, n, shape) in _names_offsets(case, cfg).items():
+        p0 = c["state0"][k].reshape(-1).astype(np.float64)
+        g_hat = m1[off:off + n] / (1 - B1) - wd * p0
+        ref = g_avg[k].reshape(-1)
+        if bn_fed_bias(k, None):
+            err, tol = np.abs(g_hat - ref).max(), 1e-4
+        else:
+            err, tol = np.abs(g_hat - ref).max() / max(np.abs(ref).max(), 1e-30), 5e-3
+        if err > tol:
+            bad[k] = err
+        # second moment and the update are consistent with the first (one Adam step, step = 1)
+        gw = g_hat + wd * p0
+        assert np.allclose(v1[off:off + n], (1 - B2) * gw * gw, rtol=1e-4, atol=1e-12), k
+        upd = p0 - lr * (m1[off:off + n] / (1 - B1)) / (np.sqrt(v1[off:off + n] / (1 - B2)) + EPS)
+        assert np.abs(p1[off:off + n] - upd).max() <= 1e-6 + 1e-6 * np.abs(p0).max(), k
+    assert not bad, bad
+
+
+def test_ddp_small_flat_allreduce_matches_per_shard_oracle(ranks):
+    _check(ranks, "small_flat", "cnn_small_T201", {"embedding_dim": 128, "use_attention": True, "dropout_rate": 0.1})
+
+
+def test_ddp_small_bucketed_with_clip_matches_oracle(ranks):
+    assert ranks[0]["small_bucket_clip/nbuckets"][0] > 1
+    _check(ranks, "small_bucket_clip", "cnn_small_T201",
+           {"embedding_dim": 128, "use_attention": True, "dropout_rate": 0.1}, clip=0.05)
+
+
+def test_ddp_deep_matches_oracle_and_bucketing_is_exact(ranks):
+    cfg = {"embedding_dim": 128, "use_attention": True, "dropout_rate": 0.2, "hidden_dims": [8, 16, 32, 64]}
+    _check(ranks, "deep_flat", "cnn_deep_T200", cfg)
+    assert ranks[0]["deep_bucket/nbuckets"][0] > 1
+    for key in ("flat", "m", "v"):
+        assert np.array_equal(ranks[0][f"deep_flat/{key}"], ranks[0][f"deep_bucket/{key}"]), key
+
+
+def test_adam_grad_scale_matches_torch():
+    """pcx_adam_step with grad_scale != 1 (the 1/world average) against torch.optim.Adam on the
+    pre-scaled gradient."""
+    from phoneme_contrast_amd.optim import FusedAdam
+    torch.manual_seed(0)
+    p0 = torch.randn(1000, device="cuda")
+    ps_f = [torch.nn.Parameter(p0[:600].clone()), torch.nn.Parameter(p0[600:].clone())]
+    ps_t = [torch.nn.Parameter(p0[:600].clone()), torch.nn.Parameter(p0[600:].clone())]
+    fa = FusedAdam(ps_f, lr=1e-2, weight_decay=1e-4)
+    ta = torch.optim.Adam(ps_t, lr=1e-2, weight_decay=1e-4)
+    for it in range(3):
+        g = torch.randn(1000, device="cuda")
+        flat = g.clone() * 4.0  # a 4-rank SUM
+        for p, q, sl in zip(ps_f, ps_t, (slice(0, 600), slice(600, 1000))):
+            p.grad = flat[sl].clone()
+            q.grad = g[sl].clone()
+        fa.step(flat_grads=[flat], grad_scale=0.25)
+        ta.step()
+        for p, q in zip(ps_f, ps_t):
+            assert torch.allclose(p, q, rtol=1e-6, atol=1e-7), it
+
+
+def test_fused_adam_second_group_unaligned_grads_match_torch():
+    """Two param groups whose gradients sit at an unaligned offset of one flat buffer:
+    the staged copy path, same result as torch.optim.Adam."""
+    from phoneme_contrast_amd.optim import FusedAdam
+    torch.manual_seed(1)
+    flat = torch.randn(1 + 777, device="cuda")
+    a_f, b_f = torch.nn.Parameter(torch.randn(1, device="cuda")), torch.nn.Parameter(torch.randn(777, device="cuda"))
+    a_t, b_t = torch.nn.Parameter(a_f.detach().clone()), torch.nn.Parameter(b_f.detach().clone())
+    fa = FusedAdam([{"params": [a_f]}, {"params": [b_f], "weight_decay": 1e-2}], lr=1e-3)
+    ta = torch.optim.Adam([{"params": [a_t]}, {"params": [b_t], "weight_decay": 1e-2}], lr=1e-3)
+    for _ in range(2):
+        a_f.grad, b_f.grad = flat[:1], flat[1:]  # b's gradient starts 4 bytes into the buffer
+        a_t.grad, b_t.grad = flat[:1].clone(), flat[1:].clone()
+        fa.step()
+        ta.step()
+    assert torch.allclose(b_f, b_t, rtol=1e-6, atol=1e-7) and torch.allclose(a_f, a_t, rtol=1e-6, atol=1e-7)
