@@ -3,7 +3,7 @@
 //  * conv1_fwd_kernel — the Cin = 1 first conv (reference src/models/phoneme_cnn.py:36): direct,
 //                       HBM-write-bound, with the BN statistics of its output in the epilogue.
 //  * wgrad1_kernel    — its weight gradient (the 3x3 implicit-GEMM convs live in conv_dma.hip,
-//                       their weight gradients in wgrad_win.hip / wgrad_w32.hip).
+//                       their weight gradients in wgrad_s.hip / wgrad_w32.hip).
 //  * sum_slices / pack kernels — deterministic slice reduction and GEMM weight layouts.
 //
 // Tensor layout is the reference's planar NCHW.

@@ -94,7 +94,9 @@ int build_deep(Plan& p) {
     // a stride-1 3x3 conv cin -> cout at HxW on the DMA conv (fwd, dgrad) and the 32x32 wgrad
     auto plan_routed = [&](int ci, int co, int h, int w, bool* fwd, bool* w32, WgradArgs* wga, int* nblk) {
         *fwd = route && (co == 32 || co % 64 == 0) && (ci == 32 || ci % 64 == 0) && ci % 2 == 0;
-        *w32 = route && wgrad_w32_geometry(B, h, w, ci, co, wga);
+        // the pixel-stream kernel from 50 columns up; narrower rows waste its 8-column stream granule,
+        // the 32x32 row-window kernel takes them
+        *w32 = route && (w >= 50 ? wgrad_s_geometry(B, h, w, ci, co, wga) : wgrad_w32_geometry(B, h, w, ci, co, wga));
         *nblk = 0;
         if (*fwd) {
             *nblk = (int)std::max(conv3x3_nblk(B, h, w, co), conv3x3_nblk(B, h, w, ci));
@@ -267,7 +269,7 @@ int conv_bn_fwd(const Ctx& c, const char* label, int layer, const float* x, int 
 int conv_wgrad(const Ctx& c, int layer, const float* x, int cin, int IH, int IW, int k, int stride, int pad,
                const float* dy, int cout, int OH, int OW, float* gw, float* gb, const WgradArgs* w32 = nullptr,
                const float* bn_g = nullptr, const float* bn_y = nullptr, const float4* bn_cf = nullptr) {
-    if (w32) {  // stride-1 3x3: the 32x32 row-window kernel
+    if (w32) {  // stride-1 3x3: pixel-stream (wgrad_s.hip, MT 16) or 32x32 row-window (wgrad_w32.hip) kernel
         WgradArgs w = *w32;
         w.B = c.p.B; w.H = OH; w.W = OW; w.cin = cin; w.cout = cout;
         if (bn_g) {  // BN backward in the staging: dy = f(g, y) computed per row and written to `dy`
@@ -287,7 +289,7 @@ int conv_wgrad(const Ctx& c, int layer, const float* x, int cin, int IH, int IW,
         w.srcH = IH; w.srcW = IW;
         float* wgp = c.w<float>(c.d.wgp);
         w.part = wgp;
-        { Scope sc(&c.p.prof, c.s, "wgrad", layer); RC(launch_wgrad_w32(PRO_RAW, w, c.s)); }
+        { Scope sc(&c.p.prof, c.s, "wgrad", layer); RC(w.MT == 16 ? launch_wgrad_s(PRO_RAW, w, c.s) : launch_wgrad_w32(PRO_RAW, w, c.s)); }
         RC(launch_sum_slices(wgp, w.nslice, (int64_t)cout * cin * 9, gw, c.s));
         return hip_status_ok(hipMemsetAsync(gb, 0, (size_t)cout * 4, c.s), "memset bias grad");
     }

@@ -83,15 +83,19 @@ struct WgradArgs {
     float* dy_out;        // optional: dy = BNBWD(dz, y) written here (consumed by the data grad)
     int R, CW, nseg, nrb, nchunks, per_slice, nslice;
     int MT, NPM, NPC;     // MFMA tile (16 or 32), tiles per block along cout / cin
-    int VX;               // wgrad_win: vector width of the x staging
+    int VX;               // vector width of the staged loads
     int KW, ntslice;      // wgrad_w32: waves splitting K on one tile, task slices (nslice = ntslice * KW)
+    int R0, DCS, XCS;     // wgrad_s: stream length, LDS channel strides of dy / x
+    int nvd, nvx;         // wgrad_s: staged vectors per dy / x channel row
 };
-// sliding-row-window weight gradient on 16 x 16 tiles (wgrad_win.hip): prologues PRO_RAW / PRO_BNRELU
-int launch_wgrad_win(int pro, WgradArgs a, hipStream_t s);
-// same row window on 32 x 32 tiles (wgrad_w32.hip; channels multiples of 32): false if it does not apply
+// sliding row window on 32 x 32 tiles (wgrad_w32.hip; channels multiples of 32; the narrow-row residual
+// convs): false if it does not apply
 bool wgrad_w32_geometry(int B, int H, int W, int cin, int cout, WgradArgs* a);
 int launch_wgrad_w32(int pro, WgradArgs a, hipStream_t s);
-void wgrad_win_geometry(int B, int H, int W, int cin, int cout, WgradArgs* a);
+// pixel-stream kernel (wgrad_s.hip, 16x16x4 tiles): channels multiples of 32, any W; force_cw > 0 pins the
+// strip width (timing tools)
+bool wgrad_s_geometry(int B, int H, int W, int cin, int cout, WgradArgs* a, int force_cw = 0);
+int launch_wgrad_s(int pro, WgradArgs a, hipStream_t s);
 
 // first-layer (Cin = 1) weight gradient
 struct Wgrad1Args {

@@ -61,8 +61,8 @@ int build_small(Plan& p) {
             L.wp = p.carve("wp", (size_t)9 * L.cin * L.cout * 4);
             L.wpd = p.carve("wpd", (size_t)9 * L.cin * L.cout * 4);
             L.nblk = (int)conv3x3_nblk(B, L.H, L.W, L.cout);
-            if (!wgrad_w32_geometry(B, L.H, L.W, L.cin, L.cout, &L.wg))
-                wgrad_win_geometry(B, L.H, L.W, L.cin, L.cout, &L.wg);
+            PCX_CHECK_ARG(wgrad_s_geometry(B, L.H, L.W, L.cin, L.cout, &L.wg),
+                          "PhonemeNet: no weight-gradient geometry for layer %d (%dx%d)", l, L.H, L.W);
             wg = std::max(wg, (size_t)L.wg.nslice * L.cout * L.cin * 9);
         } else {
             L.nblk = conv1_nblk(B, L.H, &p.conv1_rows);
@@ -335,7 +335,7 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
             w.dy_out = at<float>(ws, p.dyb);
             {
                 Scope sc(&p.prof, s, "wgrad", l);
-                RC(w.MT == 32 ? launch_wgrad_w32(pro, w, s) : launch_wgrad_win(pro, w, s));
+                RC(launch_wgrad_s(pro, w, s));
             }
             { Scope sc(&p.prof, s, "wgrad_reduce", l); RC(launch_sum_slices(wgp, w.nslice, (int64_t)L.cout * L.cin * 9, G[p_conv_w(l)], s)); }
             p.buckets.mark(p_conv_w(l), s);  // BN l's dgamma / dbeta came with layer l+1's data gradient

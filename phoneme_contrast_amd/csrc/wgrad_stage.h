@@ -1,5 +1,5 @@
-// Row staging shared by the sliding-row-window weight-gradient kernels (wgrad_win.hip: 16 x 16
-// tiles, wgrad_w32.hip: 32 x 32 tiles): per-thread register prefetch of the next dz / y / x rows,
+// Row staging of the sliding-row-window weight-gradient kernel (wgrad_w32.hip, 32 x 32 tiles):
+// per-thread register prefetch of the next dz / y / x rows,
 // BN backward / x prologue / zero padding, stores into the LDS row ring.
 #pragma once
 #include "kernels.h"

@@ -4,13 +4,13 @@
 //   conv layers of PhonemeNet, phoneme_cnn.py:35-65; dy = BN backward of (dz, y), x = the block
 //   input after BN + ReLU, or the materialised pooled input)
 //
-// Same walk and row staging as wgrad_win.hip (wgrad_stage.h: a block walks a column strip of one
-// sample top to bottom, x rows in a 4-slot LDS ring, dy rows in 2 slots, the next rows prefetched
-// into registers while the MFMAs of the current row run, one barrier per row).  The difference is
-// the tile: each wave owns a 32 (cout) x 32 (cin) tile for all 9 taps (144 accumulator VGPRs), so
-// one k-step (2 pixels) costs 1 A + 9 B LDS reads for 9 MFMAs of 64 cycles -- half the LDS
-// instructions per FLOP of the 16 x 16 x 4 form, and with the f32 MFMA sharing the vector issue
-// every instruction saved is time saved.  A block holds TM x TN tiles; when that is fewer than 4,
+// Used for the narrow rows (W < 50) of the residual network's stride-1 convs, where the 8-column
+// stream granule of wgrad_s.hip wastes more than it saves.  Row staging of wgrad_stage.h (a block
+// walks a column strip of one sample top to bottom, x rows in a 4-slot LDS ring, dy rows in 2
+// slots, the next rows prefetched into registers while the MFMAs of the current row run, one
+// barrier per row).  Each wave owns a 32 (cout) x 32 (cin) tile for all 9 taps (144 accumulator
+// VGPRs): one k-step (2 pixels) costs 1 A + 9 B LDS reads for 9 MFMAs of 64 cycles.  A block
+// holds TM x TN tiles; when that is fewer than 4,
 // KW = 4 / (TM TN) waves share a tile and split its k-steps (their partials are separate slices,
 // summed with the task slices by launch_sum_slices in a fixed order: deterministic).
 #include "wgrad_stage.h"
@@ -90,7 +90,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int ncb = a.cin / CB;
     const int ngroups = (a.cout / NB) * ncb;
-    // XCD-aware (slice, group) mapping as wgrad_win: the groups of one slice read the same rows
+    // XCD-aware (slice, group) mapping: the groups of one slice read the same rows
     const int f = blockIdx.x;
     const int kk = f >> 3;
     const int group = kk % ngroups;

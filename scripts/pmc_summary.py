@@ -18,8 +18,7 @@ DGRAD = [f"conv_dgrad_L{l}" for l in range(6, 1, -1)]
 # kernel family (name up to '<' / '(') -> layer labels in per-step dispatch order
 ORDER = {
     "conv3x3_dma_kernel": FWD + DGRAD,
-    "wgrad_win_kernel": [f"wgrad_L{l}" for l in range(6, 1, -1)],
-    "wgrad_w32_kernel": [f"wgrad_L{l}" for l in range(6, 3, -1)],
+    "wgrad_s_kernel": [f"wgrad_L{l}" for l in range(6, 1, -1)],
     "bn_relu_pool_kernel": ["bn_relu_pool_L3", "bn_relu_pool_L5"],
     "conv1_fwd_kernel": ["conv1_fwd_L1"],
     "wgrad1_kernel": ["wgrad_L1"],
@@ -30,12 +29,8 @@ ORDER = {
 
 
 def order_for(per):
-    """Layer labels per family; the 32x32 wgrad takes the cin >= 64 layers (L6..L4), the 16x16
-    one the rest (L3, L2) when both run."""
-    o = dict(ORDER)
-    if "wgrad_w32_kernel" in per:
-        o["wgrad_win_kernel"] = ["wgrad_L3", "wgrad_L2"]
-    return o
+    """Layer labels per family (one weight-gradient kernel, wgrad_s, serves L6..L2)."""
+    return dict(ORDER)
 
 
 def family(name):
