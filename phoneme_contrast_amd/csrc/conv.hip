@@ -20,13 +20,46 @@ void tile_shape(int cout, int* wm, int* wn) {
 // ------------------------------------------------------------------ Cin = 1 first conv
 constexpr int C1_CPW = 8;  // output channels per wave
 
+// 3 x 6 input window of a pixel quad (columns w0 - 1 .. w0 + 4, rows hh - 1 .. hh + 1), zero outside
+// the sample.  FULL: W % 4 == 0 (16-byte row quads; no partial quad)
+template <bool FULL>
+__device__ __forceinline__ void c1_window(const float* xb, int H, int W, int hh, int w0, float (&xr)[3][6]) {
+#pragma unroll
+    for (int dh = 0; dh < 3; ++dh) {
+        const int y = hh + dh - 1;
+        if (y < 0 || y >= H) {
+#pragma unroll
+            for (int e = 0; e < 6; ++e) xr[dh][e] = 0.f;
+            continue;
+        }
+        const float* row = xb + (int64_t)y * W;
+        if (FULL) {
+            const float4 v = ld4(row + w0);
+            xr[dh][1] = v.x; xr[dh][2] = v.y; xr[dh][3] = v.z; xr[dh][4] = v.w;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) xr[dh][1 + e] = w0 + e < W ? row[w0 + e] : 0.f;
+        }
+        xr[dh][0] = w0 > 0 ? row[w0 - 1] : 0.f;
+        xr[dh][5] = w0 + 4 < W ? row[w0 + 4] : 0.f;
+    }
+}
+
+// A block owns rows_per_blk consecutive (sample, row) image rows; wave w computes output channels
+// 8w .. 8w + 7 (+ 32k) for every pixel quad of those rows: lanes take consecutive quads (1 KB per
+// store instruction), the 3 x 6 input window comes from L1/L2 (the input is 1/32 of the output).
+// HBM-write-bound (the output is 32x the input).  BN partial statistics per (channel, block) as
+// {sum, M2 about the block's first output} (shifted one-pass form).
+template <bool FULL>
 __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Args a) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t HW = (int64_t)a.H * a.W;
-    const int64_t nrows = (int64_t)a.B * a.H;
-    const int64_t r0 = (int64_t)blockIdx.x * a.rows_per_blk;
-    const int64_t r1 = min(nrows, r0 + a.rows_per_blk);
+    const int HW = a.H * a.W;
+    const int nrows = a.B * a.H;
+    const int r0 = blockIdx.x * a.rows_per_blk;
+    const int r1 = min(nrows, r0 + a.rows_per_blk);
+    const int nq = (a.W + 3) >> 2;
+    const int ntask = (r1 - r0) * nq;
     for (int cg = wave * C1_CPW; cg < a.cout; cg += 4 * C1_CPW) {
         float wt[C1_CPW][9];
 #pragma unroll
@@ -36,43 +69,54 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Args a) {
         // shift for the one-pass variance: the output at the block's first pixel
         float K[C1_CPW];
         {
-            int b = (int)(r0 / a.H), hh = (int)(r0 - (int64_t)b * a.H);
-            float x9[9];
-#pragma unroll
-            for (int t = 0; t < 9; ++t) {
-                int y = hh + t / 3 - 1, x = t % 3 - 1;
-                x9[t] = (y >= 0 && y < a.H && x >= 0) ? a.x[(int64_t)b * HW + (int64_t)y * a.W + x] : 0.f;
-            }
+            const int b = r0 / a.H, hh = r0 - b * a.H;
+            float xr[3][6];
+            c1_window<false>(a.x + (int64_t)b * HW, a.H, a.W, hh, 0, xr);
 #pragma unroll
             for (int j = 0; j < C1_CPW; ++j) {
                 float v = 0.f;
 #pragma unroll
-                for (int t = 0; t < 9; ++t) v = fmaf(wt[j][t], x9[t], v);
+                for (int t = 0; t < 9; ++t) v = fmaf(wt[j][t], xr[t / 3][1 + t % 3 - 1], v);
                 K[j] = v;
             }
         }
         float s1[C1_CPW], s2[C1_CPW];
 #pragma unroll
         for (int j = 0; j < C1_CPW; ++j) s1[j] = s2[j] = 0.f;
-        for (int64_t gr = r0; gr < r1; ++gr) {
-            const int b = (int)(gr / a.H), hh = (int)(gr - (int64_t)b * a.H);
-            const float* xb = a.x + (int64_t)b * HW;
-            for (int w = lane; w < a.W; w += 64) {
-                float x9[9];
+        for (int t = lane; t < ntask; t += 64) {
+            const int rr = t / nq, q = t - rr * nq;
+            const int gr = r0 + rr, b = gr / a.H, hh = gr - b * a.H;
+            const int w0 = 4 * q;
+            float xr[3][6];
+            c1_window<FULL>(a.x + (int64_t)b * HW, a.H, a.W, hh, w0, xr);
+            float* ob = a.out + ((int64_t)b * a.cout + cg) * HW + (int64_t)hh * a.W + w0;
 #pragma unroll
-                for (int t = 0; t < 9; ++t) {
-                    int y = hh + t / 3 - 1, x = w + t % 3 - 1;
-                    x9[t] = (y >= 0 && y < a.H && x >= 0 && x < a.W) ? xb[(int64_t)y * a.W + x] : 0.f;
+            for (int j = 0; j < C1_CPW; ++j) {
+                float v[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float acc = 0.f;
+#pragma unroll
+                    for (int tp = 0; tp < 9; ++tp) acc = fmaf(wt[j][tp], xr[tp / 3][e + tp % 3], acc);
+                    v[e] = acc;
                 }
+                if (FULL) {
+                    st4(ob + (int64_t)j * HW, make_float4(v[0], v[1], v[2], v[3]));
 #pragma unroll
-                for (int j = 0; j < C1_CPW; ++j) {
-                    float v = 0.f;
+                    for (int e = 0; e < 4; ++e) {
+                        const float d = v[e] - K[j];
+                        s1[j] += d;
+                        s2[j] = fmaf(d, d, s2[j]);
+                    }
+                } else {
 #pragma unroll
-                    for (int t = 0; t < 9; ++t) v = fmaf(wt[j][t], x9[t], v);
-                    a.out[((int64_t)b * a.cout + cg + j) * HW + (int64_t)hh * a.W + w] = v;
-                    float d = v - K[j];
-                    s1[j] += d;
-                    s2[j] = fmaf(d, d, s2[j]);
+                    for (int e = 0; e < 4; ++e)
+                        if (w0 + e < a.W) {
+                            ob[(int64_t)j * HW + e] = v[e];
+                            const float d = v[e] - K[j];
+                            s1[j] += d;
+                            s2[j] = fmaf(d, d, s2[j]);
+                        }
                 }
             }
         }
@@ -90,38 +134,57 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Args a) {
 }
 
 // ------------------------------------------------------------------ weight gradient, Cin = 1
+// dW[n][tap] = sum dy[n] x(shifted), dy = BN backward of (dz, y).  Same quad walk as the forward:
+// wave w owns channels 8w .. 8w + 7 (+ 32k), lanes consecutive pixel quads (16-byte dz / y loads);
+// HBM-read-bound (dz and y are read once).  Partials per slice.
+template <bool FULL>
 __global__ __launch_bounds__(256) void wgrad1_kernel(Wgrad1Args a) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t HW = (int64_t)a.H * a.W;
-    const int64_t nrows = (int64_t)a.B * a.H;
-    const int64_t r0 = (int64_t)blockIdx.x * a.rows_per_slice;
-    const int64_t r1 = min(nrows, r0 + a.rows_per_slice);
+    const int HW = a.H * a.W;
+    const int nrows = a.B * a.H;
+    const int r0 = blockIdx.x * a.rows_per_slice;
+    const int r1 = min(nrows, r0 + a.rows_per_slice);
+    const int nq = (a.W + 3) >> 2;
+    const int ntask = (r1 - r0) * nq;
     for (int cg = wave * C1_CPW; cg < a.cout; cg += 4 * C1_CPW) {
         float acc[C1_CPW][9];
-        float4 cf[C1_CPW];
+        float A1[C1_CPW], A2[C1_CPW], A3[C1_CPW];
 #pragma unroll
         for (int j = 0; j < C1_CPW; ++j) {
-            cf[j] = a.cf_dy[cg + j];
+            const float4 k = a.cf_dy[cg + j];  // dy = a (dz - mb - (y - mean) mgi)
+            A1[j] = k.x;
+            A2[j] = -k.x * k.z;
+            A3[j] = k.x * (k.w * k.z - k.y);
 #pragma unroll
             for (int t = 0; t < 9; ++t) acc[j][t] = 0.f;
         }
-        for (int64_t gr = r0; gr < r1; ++gr) {
-            const int b = (int)(gr / a.H), hh = (int)(gr - (int64_t)b * a.H);
-            const float* xb = a.x + (int64_t)b * HW;
-            for (int w = lane; w < a.W; w += 64) {
-                float x9[9];
+        for (int t = lane; t < ntask; t += 64) {
+            const int rr = t / nq, q = t - rr * nq;
+            const int gr = r0 + rr, b = gr / a.H, hh = gr - b * a.H;
+            const int w0 = 4 * q;
+            float xr[3][6];
+            c1_window<FULL>(a.x + (int64_t)b * HW, a.H, a.W, hh, w0, xr);
+            const int64_t o = ((int64_t)b * a.cout + cg) * HW + (int64_t)hh * a.W + w0;
 #pragma unroll
-                for (int t = 0; t < 9; ++t) {
-                    int y = hh + t / 3 - 1, x = w + t % 3 - 1;
-                    x9[t] = (y >= 0 && y < a.H && x >= 0 && x < a.W) ? xb[(int64_t)y * a.W + x] : 0.f;
+            for (int j = 0; j < C1_CPW; ++j) {
+                float dz[4], yy[4];
+                if (FULL) {
+                    const float4 u = ld4(a.dz + o + (int64_t)j * HW), v = ld4(a.y + o + (int64_t)j * HW);
+                    dz[0] = u.x; dz[1] = u.y; dz[2] = u.z; dz[3] = u.w;
+                    yy[0] = v.x; yy[1] = v.y; yy[2] = v.z; yy[3] = v.w;
                 }
 #pragma unroll
-                for (int j = 0; j < C1_CPW; ++j) {
-                    int64_t o = ((int64_t)b * a.cout + cg + j) * HW + (int64_t)hh * a.W + w;
-                    float dy = cf[j].x * (a.dz[o] - cf[j].y - (a.y[o] - cf[j].w) * cf[j].z);
+                for (int e = 0; e < 4; ++e) {
+                    if (!FULL) {
+                        const bool ok = w0 + e < a.W;
+                        dz[e] = ok ? a.dz[o + (int64_t)j * HW + e] : 0.f;
+                        yy[e] = ok ? a.y[o + (int64_t)j * HW + e] : 0.f;
+                    }
+                    float dy = fmaf(A1[j], dz[e], fmaf(A2[j], yy[e], A3[j]));
+                    if (!FULL && w0 + e >= a.W) dy = 0.f;
 #pragma unroll
-                    for (int t = 0; t < 9; ++t) acc[j][t] = fmaf(dy, x9[t], acc[j][t]);
+                    for (int tp = 0; tp < 9; ++tp) acc[j][tp] = fmaf(dy, xr[tp / 3][e + tp % 3], acc[j][tp]);
                 }
             }
         }
@@ -202,14 +265,22 @@ int conv1_nblk(int B, int H, int* rows_per_blk) {
 
 int launch_conv1_fwd(Conv1Args a, hipStream_t s) {
     PCX_CHECK_ARG(a.cout % (4 * C1_CPW) == 0, "conv1: cout %d must be a multiple of 32", a.cout);
-    conv1_fwd_kernel<<<a.nblk, 256, 0, s>>>(a);
+    PCX_CHECK_ARG((int64_t)a.B * a.H < ((int64_t)1 << 31), "conv1: too many rows");
+    if (a.W % 4 == 0)
+        conv1_fwd_kernel<true><<<a.nblk, 256, 0, s>>>(a);
+    else
+        conv1_fwd_kernel<false><<<a.nblk, 256, 0, s>>>(a);
     PCX_LAUNCH_CHECK("conv1_fwd_kernel");
     return PCX_OK;
 }
 
 int launch_wgrad1(Wgrad1Args a, hipStream_t s) {
     PCX_CHECK_ARG(a.cout % (4 * C1_CPW) == 0, "wgrad1: cout must be a multiple of 32");
-    wgrad1_kernel<<<a.nslice, 256, 0, s>>>(a);
+    PCX_CHECK_ARG((int64_t)a.B * a.H < ((int64_t)1 << 31), "wgrad1: too many rows");
+    if (a.W % 4 == 0)
+        wgrad1_kernel<true><<<a.nslice, 256, 0, s>>>(a);
+    else
+        wgrad1_kernel<false><<<a.nslice, 256, 0, s>>>(a);
     PCX_LAUNCH_CHECK("wgrad1_kernel");
     return PCX_OK;
 }

@@ -355,10 +355,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_occ(WM)
 
 // ------------------------------------------------------------------ BN + ReLU + MaxPool2 + Dropout2d
 // x[b,c,h,w] = drop[b,c] * max_{2x2} relu(y*s + t)  (reference block tail phoneme_cnn.py:40-43)
-// One block per group of PPB channel planes; thread = 4 pooled outputs of one row.  32-bit index
-// math only (int64 division per element made this kernel ALU-bound), paired loads when the
-// source rows are 8-byte aligned (even width).
-template <bool PAIR>
+// One block per group of PPB channel planes; thread = 4 pooled outputs of one row (8 input columns
+// of two rows).  VEC4: source rows 16-byte aligned (Ws % 4 == 0) -> four 16-byte loads per thread;
+// otherwise paired / scalar loads.  32-bit index math only.
+template <int VEC>
 __global__ __launch_bounds__(256) void bn_relu_pool_kernel(const float* __restrict__ y, const float4* __restrict__ cf,
                                                            const float* __restrict__ drop, float* __restrict__ x,
                                                            int nplanes, int C, int Hs, int Ws, int Hp, int Wp, int ppb) {
@@ -371,25 +371,35 @@ __global__ __launch_bounds__(256) void bn_relu_pool_kernel(const float* __restri
         const int bc = pbase + pl;
         const float4 k = cf[bc % C];
         const float d = drop ? drop[bc] : 1.f;
-        const float* s0 = y + ((int64_t)bc * Hs + 2 * hp) * Ws;
+        const float* s0 = y + ((int64_t)bc * Hs + 2 * hp) * Ws + 8 * q;
         const float* s1 = s0 + Ws;
+        float u[8], v[8];
+        if (VEC == 4 && 8 * q + 8 <= Ws) {
+            const float4 a0 = ld4(s0), a1 = ld4(s0 + 4), b0 = ld4(s1), b1 = ld4(s1 + 4);
+            u[0] = a0.x; u[1] = a0.y; u[2] = a0.z; u[3] = a0.w; u[4] = a1.x; u[5] = a1.y; u[6] = a1.z; u[7] = a1.w;
+            v[0] = b0.x; v[1] = b0.y; v[2] = b0.z; v[3] = b0.w; v[4] = b1.x; v[5] = b1.y; v[6] = b1.z; v[7] = b1.w;
+        } else if (VEC >= 2) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const bool ok = 8 * q + 2 * j + 1 < Ws;
+                const float2 a0 = ok ? *reinterpret_cast<const float2*>(s0 + 2 * j) : make_float2(0.f, 0.f);
+                const float2 b0 = ok ? *reinterpret_cast<const float2*>(s1 + 2 * j) : make_float2(0.f, 0.f);
+                u[2 * j] = a0.x; u[2 * j + 1] = a0.y; v[2 * j] = b0.x; v[2 * j + 1] = b0.y;
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const bool ok = 8 * q + e < 2 * Wp;
+                u[e] = ok ? s0[e] : 0.f;
+                v[e] = ok ? s1[e] : 0.f;
+            }
+        }
         float out[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const int w = 4 * q + j;
-            if (w < Wp) {
-                float u0, u1, v0, v1;
-                if (PAIR) {
-                    const float2 u = *reinterpret_cast<const float2*>(s0 + 2 * w);
-                    const float2 v = *reinterpret_cast<const float2*>(s1 + 2 * w);
-                    u0 = u.x; u1 = u.y; v0 = v.x; v1 = v.y;
-                } else {
-                    u0 = s0[2 * w]; u1 = s0[2 * w + 1]; v0 = s1[2 * w]; v1 = s1[2 * w + 1];
-                }
-                float m = fmaxf(fmaxf(fmaf(u0, k.x, k.y), fmaf(u1, k.x, k.y)),
-                                fmaxf(fmaf(v0, k.x, k.y), fmaf(v1, k.x, k.y)));
-                out[j] = d * fmaxf(m, 0.f);
-            }
+            const float m = fmaxf(fmaxf(fmaf(u[2 * j], k.x, k.y), fmaf(u[2 * j + 1], k.x, k.y)),
+                                  fmaxf(fmaf(v[2 * j], k.x, k.y), fmaf(v[2 * j + 1], k.x, k.y)));
+            out[j] = d * fmaxf(m, 0.f);
         }
         float* dst = x + ((int64_t)bc * Hp + hp) * Wp + 4 * q;
         if ((Wp & 3) == 0) {
@@ -490,10 +500,12 @@ int launch_bn_relu_pool(const float* y, const float4* cf, const float* drop, flo
     const int nplanes = B * C, nqp = Hp * ((Wp + 3) / 4);
     const int ppb = std::max(1, 1024 / std::max(1, nqp));  // ~1024 quads per block
     const int blocks = ceil_div(nplanes, ppb);
-    if (Ws % 2 == 0)
-        bn_relu_pool_kernel<true><<<blocks, 256, 0, s>>>(y, cf, drop, x, nplanes, C, Hs, Ws, Hp, Wp, ppb);
+    if (Ws % 4 == 0)
+        bn_relu_pool_kernel<4><<<blocks, 256, 0, s>>>(y, cf, drop, x, nplanes, C, Hs, Ws, Hp, Wp, ppb);
+    else if (Ws % 2 == 0)
+        bn_relu_pool_kernel<2><<<blocks, 256, 0, s>>>(y, cf, drop, x, nplanes, C, Hs, Ws, Hp, Wp, ppb);
     else
-        bn_relu_pool_kernel<false><<<blocks, 256, 0, s>>>(y, cf, drop, x, nplanes, C, Hs, Ws, Hp, Wp, ppb);
+        bn_relu_pool_kernel<1><<<blocks, 256, 0, s>>>(y, cf, drop, x, nplanes, C, Hs, Ws, Hp, Wp, ppb);
     PCX_LAUNCH_CHECK("bn_relu_pool_kernel");
     return PCX_OK;
 }

@@ -113,6 +113,192 @@ __global__ __launch_bounds__(256) void head_pool_bwd_kernel(HeadPoolArgs a) {
     }
 }
 
+// Register-resident form for the PhonemeNet head (C = 128, P <= 512, P % 4 == 0; the cnn_small
+// trunk ends at 128 x 10 x 50): one block of 8 waves holds a whole sample in registers -- wave w
+// owns channels 16w .. 16w + 15, lane l the pixel quads 4l + 256k (k < 2) -- so y is read from HBM
+// once (16-byte loads) instead of once for the attention logits and again for the pool / dz; the
+// cross-channel logit sums and the attention map go through LDS.  Other shapes (the residual
+// network's 512 x 3 x 13) take the per-sample kernels above.
+constexpr int HR_C = 128, HR_CPW = 16, HR_KP = 2, HR_PMAX = 512;
+
+bool head_reg_fits(const HeadPoolArgs& a) { return a.C == HR_C && a.P % 4 == 0 && a.P <= HR_PMAX; }
+
+__global__ __launch_bounds__(512) void head_pool_fwd_reg_kernel(HeadPoolArgs a) {
+    __shared__ __attribute__((aligned(16))) float part[8][HR_PMAX];  // per-wave partial logits
+    __shared__ __attribute__((aligned(16))) float att[HR_PMAX];
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int c0 = wave * HR_CPW, P = a.P;
+    const float* yb = a.y + ((int64_t)b * HR_C + c0) * P;
+    float4 xv[HR_CPW][HR_KP];
+    float4 lg[HR_KP];
+#pragma unroll
+    for (int k = 0; k < HR_KP; ++k) lg[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int c = 0; c < HR_CPW; ++c) {
+        const float4 cf = a.cf[c0 + c];
+        const float d = a.drop ? a.drop[(int64_t)b * HR_C + c0 + c] : 1.f;
+        const float wa = a.wa ? a.wa[c0 + c] : 0.f;
+#pragma unroll
+        for (int k = 0; k < HR_KP; ++k) {
+            const int p = 4 * lane + 256 * k;
+            float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (p < P) {
+                const float4 y = ld4(yb + (int64_t)c * P + p);
+                x = make_float4(xval(y.x, cf, d), xval(y.y, cf, d), xval(y.z, cf, d), xval(y.w, cf, d));
+            }
+            xv[c][k] = x;
+            lg[k].x = fmaf(wa, x.x, lg[k].x);
+            lg[k].y = fmaf(wa, x.y, lg[k].y);
+            lg[k].z = fmaf(wa, x.z, lg[k].z);
+            lg[k].w = fmaf(wa, x.w, lg[k].w);
+        }
+    }
+    if (a.wa) {
+#pragma unroll
+        for (int k = 0; k < HR_KP; ++k) {
+            const int p = 4 * lane + 256 * k;
+            if (p < P) st4(&part[wave][p], lg[k]);
+        }
+        __syncthreads();
+        const float ba = a.ba[0];
+        for (int p = tid; p < P; p += 512) {
+            float l = ba;
+#pragma unroll
+            for (int w = 0; w < 8; ++w) l += part[w][p];
+            const float v = 1.f / (1.f + expf(-l));
+            att[p] = v;
+            a.att[(int64_t)b * P + p] = v;
+        }
+    } else {
+        for (int p = tid; p < P; p += 512) att[p] = 1.f;
+    }
+    __syncthreads();
+    const float invp = 1.f / (float)P;
+#pragma unroll
+    for (int c = 0; c < HR_CPW; ++c) {
+        float sum = 0.f;
+#pragma unroll
+        for (int k = 0; k < HR_KP; ++k) {
+            const int p = 4 * lane + 256 * k;
+            if (p < P) {
+                const float4 at = *reinterpret_cast<const float4*>(&att[p]);
+                sum = fmaf(xv[c][k].x, at.x, sum);
+                sum = fmaf(xv[c][k].y, at.y, sum);
+                sum = fmaf(xv[c][k].z, at.z, sum);
+                sum = fmaf(xv[c][k].w, at.w, sum);
+            }
+        }
+        sum = wave_sum(sum);
+        if (lane == 0) a.pooled[(int64_t)b * HR_C + c0 + c] = sum * invp;
+    }
+}
+
+__global__ __launch_bounds__(512) void head_pool_bwd_reg_kernel(HeadPoolArgs a) {
+    __shared__ __attribute__((aligned(16))) float part[8][HR_PMAX];
+    __shared__ __attribute__((aligned(16))) float att[HR_PMAX];
+    __shared__ __attribute__((aligned(16))) float dl[HR_PMAX];
+    __shared__ float red[8];
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int c0 = wave * HR_CPW, P = a.P;
+    const float invp = 1.f / (float)P;
+    const float* yb = a.y + ((int64_t)b * HR_C + c0) * P;
+    float4 yv[HR_CPW][HR_KP];
+#pragma unroll
+    for (int c = 0; c < HR_CPW; ++c)
+#pragma unroll
+        for (int k = 0; k < HR_KP; ++k) {
+            const int p = 4 * lane + 256 * k;
+            yv[c][k] = p < P ? ld4(yb + (int64_t)c * P + p) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    if (a.wa) {  // dl[p] = att (1 - att) sum_c dpooled[c] / P x[c][p]
+        float4 sp[HR_KP];
+#pragma unroll
+        for (int k = 0; k < HR_KP; ++k) sp[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int c = 0; c < HR_CPW; ++c) {
+            const float4 cf = a.cf[c0 + c];
+            const float d = a.drop ? a.drop[(int64_t)b * HR_C + c0 + c] : 1.f;
+            const float g = a.dpooled[(int64_t)b * HR_C + c0 + c] * invp;
+#pragma unroll
+            for (int k = 0; k < HR_KP; ++k) {
+                sp[k].x = fmaf(g, xval(yv[c][k].x, cf, d), sp[k].x);
+                sp[k].y = fmaf(g, xval(yv[c][k].y, cf, d), sp[k].y);
+                sp[k].z = fmaf(g, xval(yv[c][k].z, cf, d), sp[k].z);
+                sp[k].w = fmaf(g, xval(yv[c][k].w, cf, d), sp[k].w);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < HR_KP; ++k) {
+            const int p = 4 * lane + 256 * k;
+            if (p < P) st4(&part[wave][p], sp[k]);
+        }
+        __syncthreads();
+        float dls = 0.f;
+        for (int p = tid; p < P; p += 512) {
+            float sum = 0.f;
+#pragma unroll
+            for (int w = 0; w < 8; ++w) sum += part[w][p];
+            const float at = a.att[(int64_t)b * P + p];
+            const float d = sum * at * (1.f - at);
+            att[p] = at;
+            dl[p] = d;
+            dls += d;
+        }
+        dls = wave_sum(dls);
+        if (lane == 0) red[wave] = dls;
+        __syncthreads();
+        if (tid == 0) {
+            float t = 0.f;
+            for (int w = 0; w < 8; ++w) t += red[w];
+            a.p_dba[b] = t;
+        }
+    } else {
+        for (int p = tid; p < P; p += 512) {
+            att[p] = 1.f;
+            dl[p] = 0.f;
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int c = 0; c < HR_CPW; ++c) {
+        const float4 cf = a.cf[c0 + c];
+        const float dr = a.drop ? a.drop[(int64_t)b * HR_C + c0 + c] : 1.f;
+        const float g = a.dpooled[(int64_t)b * HR_C + c0 + c] * invp;
+        const float wac = a.wa ? a.wa[c0 + c] : 0.f;
+        float* dzc = a.dz + ((int64_t)b * HR_C + c0 + c) * P;
+        float sdz = 0.f, sdx = 0.f, sdw = 0.f;
+#pragma unroll
+        for (int k = 0; k < HR_KP; ++k) {
+            const int p = 4 * lane + 256 * k;
+            if (p < P) {
+                const float4 at = *reinterpret_cast<const float4*>(&att[p]);
+                const float4 dv = *reinterpret_cast<const float4*>(&dl[p]);
+                const float yy[4] = {yv[c][k].x, yv[c][k].y, yv[c][k].z, yv[c][k].w};
+                const float aa[4] = {at.x, at.y, at.z, at.w}, ll[4] = {dv.x, dv.y, dv.z, dv.w};
+                float dz[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float z = fmaf(yy[e], cf.x, cf.y);
+                    const float dx = fmaf(g, aa[e], ll[e] * wac);
+                    dz[e] = z > 0.f ? dx * dr : 0.f;
+                    sdz += dz[e];
+                    sdx = fmaf(dz[e], (yy[e] - cf.z) * cf.w, sdx);
+                    sdw = fmaf(ll[e], dr * fmaxf(z, 0.f), sdw);
+                }
+                st4(dzc + p, make_float4(dz[0], dz[1], dz[2], dz[3]));
+            }
+        }
+        sdz = wave_sum(sdz);
+        sdx = wave_sum(sdx);
+        sdw = wave_sum(sdw);
+        if (lane == 0) {
+            a.p_dz[(int64_t)(c0 + c) * a.B + b] = sdz;
+            a.p_dzx[(int64_t)(c0 + c) * a.B + b] = sdx;
+            if (a.wa) a.p_dwa[(int64_t)(c0 + c) * a.B + b] = sdw;
+        }
+    }
+}
+
 // --------------------------------------------------------------- projection
 constexpr int PR = 16;  // rows per block
 
@@ -357,6 +543,11 @@ size_t pool_smem(const HeadPoolArgs& a, bool bwd) {
 }  // namespace
 
 int launch_head_pool_fwd(HeadPoolArgs a, hipStream_t s) {
+    if (head_reg_fits(a)) {
+        head_pool_fwd_reg_kernel<<<a.B, 512, 0, s>>>(a);
+        PCX_LAUNCH_CHECK("head_pool_fwd_reg_kernel");
+        return PCX_OK;
+    }
     size_t sm = pool_smem(a, false);
     PCX_CHECK_ARG(sm <= 160 * 1024, "head: spatial size %d too large", a.P);
     (void)hipFuncSetAttribute((const void*)head_pool_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
@@ -366,6 +557,11 @@ int launch_head_pool_fwd(HeadPoolArgs a, hipStream_t s) {
 }
 
 int launch_head_pool_bwd(HeadPoolArgs a, hipStream_t s) {
+    if (head_reg_fits(a)) {
+        head_pool_bwd_reg_kernel<<<a.B, 512, 0, s>>>(a);
+        PCX_LAUNCH_CHECK("head_pool_bwd_reg_kernel");
+        return PCX_OK;
+    }
     size_t sm = pool_smem(a, true);
     PCX_CHECK_ARG(sm <= 160 * 1024, "head: spatial size %d too large", a.P);
     (void)hipFuncSetAttribute((const void*)head_pool_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
