@@ -184,3 +184,41 @@ def test_deep_eval_and_shapes():
         assert e.shape == (bs, 64)
         assert (e.double() - r).abs().max() < 1e-5
         assert torch.allclose(e.norm(dim=1), torch.ones(bs), atol=1e-6)
+
+
+def test_deep_fp32_full_size_properties():
+    """config 3 (cnn_deep fp32, B = 4096, T = 200, widths 64..512) at its full size, where the float64
+    oracle is out of reach: unit-norm finite embeddings, finite gradients, a bit-identical repeat (no
+    atomics on the path), and in eval mode (running BN statistics: samples independent) the first
+    8 embeddings of the 4096-batch equal those of an 8-sample batch -- a tiling / sample-boundary
+    check of every conv engine at the full shapes (the float64 parity itself is the small-batch
+    tests above)."""
+    from phoneme_contrast_amd.losses import SupervisedContrastiveLoss
+    from phoneme_contrast_amd.models import PhonemeNetDeep
+    torch.manual_seed(0)
+    m = PhonemeNetDeep({"embedding_dim": 128}).cuda().train()
+    B = 4096
+    x = torch.randn(B, 1, 40, 200, generator=torch.Generator().manual_seed(1)).cuda()
+    labels = (torch.arange(B) // 4).cuda()
+    masks = [(torch.rand(B, c) > 0.2).float() / 0.8 for c in m.hidden_dims]
+    fn = SupervisedContrastiveLoss(temperature=0.15)
+    outs = []
+    for _ in range(2):
+        m.zero_grad(set_to_none=True)
+        m.set_dropout_masks(masks)
+        e = m(x)
+        loss = fn(e, labels)
+        loss.backward()
+        outs.append((e.detach().clone(), loss.item(), [p.grad.clone() for p in m.parameters()]))
+    e, l, g = outs[0]
+    assert torch.allclose(e.norm(dim=1), torch.ones(B, device=e.device), atol=1e-5)
+    assert torch.isfinite(torch.tensor(l)) and all(torch.isfinite(t).all() for t in g)
+    assert any(t.abs().max() > 0 for t in g)
+    e2, l2, g2 = outs[1]
+    assert torch.equal(e, e2) and l == l2 and all(torch.equal(a, b) for a, b in zip(g, g2))
+    m.eval()
+    with torch.no_grad():
+        full = m(x)[:8]
+        part = m(x[:8].contiguous())
+    assert torch.isfinite(full).all()
+    assert (full - part).abs().max().item() < 1e-5

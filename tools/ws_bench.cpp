@@ -1,0 +1,80 @@
+// Standalone timing + cross-check of the stream weight-gradient kernel (wgrad_s) against the
+// round-1 row-window kernels (wgrad_w32 / wgrad_win) on one layer shape (analysis aid).
+//   ws_bench H W cin cout [B] [reps] [pro] [force_cw]
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include "../phoneme_contrast_amd/csrc/kernels.h"
+__global__ void fill(float* p, size_t n, unsigned seed, float scale, float off) {
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    for (; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        unsigned h = (unsigned)i * 2654435761u ^ seed;
+        h ^= h >> 13; h *= 0x5bd1e995; h ^= h >> 15;
+        p[i] = off + scale * ((h & 0xffffff) / 16777216.0f - 0.5f);
+    }
+}
+static float timeit(int (*f)(int, pcx::WgradArgs, hipStream_t), int pro, pcx::WgradArgs a, int reps) {
+    hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
+    if (f(pro, a, 0)) { printf("launch failed\n"); exit(1); }
+    (void)hipDeviceSynchronize();
+    (void)hipEventRecord(e0);
+    for (int i = 0; i < reps; ++i) f(pro, a, 0);
+    (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
+    float ms; (void)hipEventElapsedTime(&ms, e0, e1);
+    return ms / reps;
+}
+int main(int argc, char** argv) {
+    int H = atoi(argv[1]), W = atoi(argv[2]), cin = atoi(argv[3]), cout = atoi(argv[4]);
+    int B = argc > 5 ? atoi(argv[5]) : 4096, reps = argc > 6 ? atoi(argv[6]) : 5, pro = argc > 7 ? atoi(argv[7]) : 1;
+    int fcw = argc > 8 ? atoi(argv[8]) : 0;
+    size_t ny = (size_t)B * cout * H * W, nx = (size_t)B * cin * H * W, nw = (size_t)cout * cin * 9;
+    float *dz, *y, *x, *dy1, *dy2, *part, *cfd, *cfx, *g1, *g2;
+    (void)hipMalloc(&dz, ny * 4); (void)hipMalloc(&y, ny * 4); (void)hipMalloc(&dy1, ny * 4); (void)hipMalloc(&dy2, ny * 4);
+    (void)hipMalloc(&x, nx * 4); (void)hipMalloc(&cfd, cout * 16); (void)hipMalloc(&cfx, cin * 16);
+    (void)hipMalloc(&g1, nw * 4); (void)hipMalloc(&g2, nw * 4);
+    fill<<<4096, 256>>>(dz, ny, 1, 2.f, 0.f); fill<<<4096, 256>>>(y, ny, 2, 2.f, 0.f); fill<<<4096, 256>>>(x, nx, 3, 2.f, 0.f);
+    fill<<<1, 256>>>(cfd, cout * 4, 4, 0.5f, 1.f); fill<<<1, 256>>>(cfx, cin * 4, 5, 0.5f, 0.5f);
+    pcx::WgradArgs s{}, o{};
+    if (!pcx::wgrad_s_geometry(B, H, W, cin, cout, &s, fcw)) { printf("no geometry\n"); return 1; }
+    bool w32 = pcx::wgrad_w32_geometry(B, H, W, cin, cout, &o);
+    if (!w32) { o = s; }  // no row-window geometry: compare wgrad_s with itself
+    size_t np = std::max((size_t)s.nslice, (size_t)o.nslice) * nw;
+    (void)hipMalloc(&part, np * 4);
+    for (pcx::WgradArgs* a : {&s, &o}) {
+        a->B = B; a->H = H; a->W = W; a->cin = cin; a->cout = cout;
+        a->dz = dz; a->y = y; a->cf_dy = (const float4*)cfd; a->src = x; a->cf_x = (const float4*)cfx;
+        a->srcH = H; a->srcW = W; a->part = part;
+    }
+    s.dy_out = dy1; o.dy_out = dy2;
+    float ms_s = timeit(pcx::launch_wgrad_s, pro, s, reps);
+    pcx::launch_wgrad_s(pro, s, 0); pcx::launch_sum_slices(part, s.nslice, nw, g1, 0);
+    float ms_o = timeit(w32 ? pcx::launch_wgrad_w32 : pcx::launch_wgrad_s, pro, o, reps);
+    (w32 ? pcx::launch_wgrad_w32 : pcx::launch_wgrad_s)(pro, o, 0); pcx::launch_sum_slices(part, o.nslice, nw, g2, 0);
+    (void)hipDeviceSynchronize();
+    std::vector<float> h1(nw), h2(nw), d1(ny), d2(ny);
+    (void)hipMemcpy(h1.data(), g1, nw * 4, hipMemcpyDeviceToHost); (void)hipMemcpy(h2.data(), g2, nw * 4, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(d1.data(), dy1, ny * 4, hipMemcpyDeviceToHost); (void)hipMemcpy(d2.data(), dy2, ny * 4, hipMemcpyDeviceToHost);
+    std::vector<float> hz(ny), hy(ny), hc(cout * 4);
+    (void)hipMemcpy(hz.data(), dz, ny * 4, hipMemcpyDeviceToHost); (void)hipMemcpy(hy.data(), y, ny * 4, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(hc.data(), cfd, cout * 16, hipMemcpyDeviceToHost);
+    size_t nbad = 0;
+    double dref = 0;  // dy_out of wgrad_s against the BN-backward formula on the host
+    for (size_t i = 0; i < ny; ++i) {
+        const int n = (int)((i / ((size_t)H * W)) % cout);
+        const float a = hc[4 * n], mb = hc[4 * n + 1], mgi = hc[4 * n + 2], mean = hc[4 * n + 3];
+        const float ref = fmaf(a, hz[i], fmaf(-a * mgi, hy[i], a * (mean * mgi - mb)));
+        dref = std::max(dref, (double)std::fabs(d1[i] - ref));
+        if (std::fabs(d1[i] - ref) > 1e-3 && nbad++ < 6)
+            printf("  dy mismatch b%zu n%d h%zu w%zu: %g vs %g\n", i / ((size_t)cout * H * W), n, (i / W) % H, i % W, d1[i], ref);
+    }
+    if (nbad) printf("  %zu dy mismatches of %zu\n", nbad, ny);
+    double emax = 0, gmax = 0, dmax = 0;
+    for (size_t i = 0; i < nw; ++i) { emax = std::max(emax, (double)std::fabs(h1[i] - h2[i])); gmax = std::max(gmax, (double)std::fabs(h2[i])); }
+    for (size_t i = 0; i < ny; ++i) dmax = std::max(dmax, (double)std::fabs(d1[i] - d2[i]));
+    double fl = 2.0 * B * H * W * cin * cout * 9;
+    printf("H%d W%d %d->%d pro%d | s: TM %d CW %d V %d R %d slices %d: %.3f ms %.3f roof | old %s: %.3f ms %.3f roof"
+           " | dW rel %.2e dy-vs-old %.2e dy-vs-host %.2e\n", H, W, cin, cout, pro, s.NPM, s.CW, s.VX, s.R0, s.ntslice, ms_s, fl / ms_s / 1e9 / 157.3,
+           w32 ? "w32" : "s", ms_o, fl / ms_o / 1e9 / 157.3, emax / gmax, dmax, dref);
+    return 0;
+}
