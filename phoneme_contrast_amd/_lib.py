@@ -10,7 +10,7 @@ import threading
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("PCX_LIB", os.path.join(_HERE, "libpcx.so"))
+LIB_PATH = os.path.join(_HERE, "libpcx.so")
 
 PCX_OK = 0
 PCX_EINVAL = -1

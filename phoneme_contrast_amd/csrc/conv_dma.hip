@@ -6,8 +6,12 @@
 //    aligned, dword otherwise) into one of two buffers; chunk k+1 is in flight while the MFMAs of
 //    chunk k run, so staging latency is hidden and costs no VGPRs;
 //  * the prologue (BN+ReLU of the producer; the data gradient reads the dy its weight gradient
-//    materialised, raw) is applied when a B operand is read from LDS, together with the
-//    zero-padding / sample-boundary mask of its tap;
+//    materialised, raw) is applied when a B operand is read from LDS;
+//  * zero padding / sample boundaries without data masks: a tap whose neighbour pixel is outside
+//    the sample reads a reserved 16-byte group at the end of the channel plane instead (0 for raw
+//    operands, NaN for BN+ReLU ones: relu(NaN * s + t) = fmaxf(NaN, 0) = 0).  The choice is one
+//    address select per (tap, pixel group), shared by all k-steps of the tap, in place of a
+//    v_cndmask on every operand (which also cost VALU->MFMA hazard nops);
 //  * one barrier per chunk; all per-chunk tables live in the single dynamic LDS array (no second
 //    __shared__ object, so hipcc does not drain the DMA queue before LDS reads).
 #include "conv_epilogue.h"
@@ -16,14 +20,6 @@ namespace pcx {
 namespace {
 
 typedef __attribute__((address_space(3))) void lds_void;
-
-// Timing-decomposition builds only (scripts/conv_expt.sh compiles this file with
-// -DPCX_CONV_EXPT=bits into a separate library): 1 no DMA after the first chunk, 2 no MFMA,
-// 4 no epilogue, 8 no per-chunk wait / barrier, 16 no prologue / padding masks, 32 no LDS reads of
-// the pixel operand.  Results are garbage in those builds.
-#ifndef PCX_CONV_EXPT
-#define PCX_CONV_EXPT 0
-#endif
 
 __device__ __forceinline__ int fdiv(int n, int d, float inv) {  // n / d, 0 <= n < 2^22
     int q = (int)((float)n * inv);
@@ -80,15 +76,17 @@ __host__ __device__ constexpr int dma_table_floats(int cin, int NR) {
 }
 
 // raw image of one K-chunk: CK channels x NR staged rows x W columns (dense)
+// (channel planes of PL floats: NR * W image floats, padding to 16 bytes, the reserved group)
 template <int VEC>
 __device__ __forceinline__ void issue_raw(const ConvArgs& a, const int2* rinfo, unsigned raw, int c0,
-                                          int wave, int lane, int total, int CK, float invPL,
+                                          int wave, int lane, int total, int PL, float invPL,
                                           float invW) {
-    const int PL = a.NR * a.W;  // floats per channel plane of the image
+    const int PLD = a.NR * a.W;  // image floats per channel plane
     for (int base = wave * 64 * VEC; base < total; base += 4 * 64 * VEC) {
         const int f = min(base + lane * VEC, total - VEC);
         const int cl = fdiv(f, PL, invPL);
         const int rem = f - cl * PL;
+        if (rem >= PLD) continue;  // padding / reserved group: never copied
         const int lr = fdiv(rem, a.W, invW);
         const int w = rem - lr * a.W;
         const int2 ri = rinfo[lr];
@@ -123,8 +121,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_occ(WM)
     constexpr int BP = 4 * WN * 32;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     // channel-plane stride of the staged image: dense rows (NR * W), or with PRE the row segments
-    // of each sample placed at the 16-byte phase of their global address (host-computed bound)
-    const int PL = PRE ? a.RS : a.NR * a.W;
+    // of each sample placed at the 16-byte phase of their global address (host-computed bound);
+    // + padding to 16 bytes + the reserved group at PZ (the value of out-of-sample taps)
+    const int PZ = ((PRE ? a.RS : a.NR * a.W) + 3) & ~3;
+    const int PL = PZ + 4;
     const int rawf = ((CK * PL + 64 * VEC - 1) / (64 * VEC)) * (64 * VEC);
     const int wtsf = ((9 * CK * COUT_T + 255) / 256) * 256;
     float4* cft = reinterpret_cast<float4*>(smem);                        // [cin]
@@ -224,6 +224,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_occ(WM)
     // precomputed copy offsets: raw rows relative to (first sample of the block, channel c0),
     // weights relative to (wpack + c0 * cout + n0)
     unsigned roff[PRE ? DMA_MAXR : 1], woff[PRE ? DMA_MAXW : 1];
+    bool rskip[PRE ? DMA_MAXR : 1];
     if constexpr (PRE) {
         static_assert(!PRE || VEC == 4, "segment layout copies 16-byte groups");
         const int QP = PL / 4, nseg = segt[0].w;
@@ -238,9 +239,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_occ(WM)
                 const int4 st = segt[t];
                 if (k >= st.x) sg = st;
             }
-            // gaps and invalid rows copy the channel's first group (in bounds, never read unmasked)
+            // gaps and invalid rows copy the channel's first group (in bounds, never read); the
+            // reserved group is not copied at all
             const int off = cl * (int)HW + ((sg.z >= 0 && k < sg.y) ? sg.z + 4 * (k - sg.x) : 0);
             roff[j] = 4u * (unsigned)off;
+            rskip[j] = k == QP - 1;
         }
 #pragma unroll
         for (int j = 0; j < DMA_MAXW; ++j) {
@@ -257,7 +260,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_occ(WM)
 #pragma unroll
             for (int j = 0; j < DMA_MAXR; ++j) {
                 const int base = wave * 64 * VEC + j * 256 * VEC;
-                if (base < rawtotal) dma_s<VEC>(sr, roff[j], raw_lds + nb * 4u * rawf + 4u * base);
+                if (base < rawtotal && !rskip[j]) dma_s<VEC>(sr, roff[j], raw_lds + nb * 4u * rawf + 4u * base);
             }
 #pragma unroll
             for (int j = 0; j < DMA_MAXW; ++j) {
@@ -265,20 +268,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_occ(WM)
                 if (base < WTOT) dma_s<4>(sw, woff[j], wts_lds + nb * 4u * wtsf + 4u * base);
             }
         } else {
-            issue_raw<VEC>(a, rinfo, raw_lds + nb * 4u * rawf, c0, wave, lane, rawtotal, CK, invPL, invW);
+            issue_raw<VEC>(a, rinfo, raw_lds + nb * 4u * rawf, c0, wave, lane, rawtotal, PL, invPL, invW);
             issue_wts<WM>(a, wts_lds + nb * 4u * wtsf, c0, n0, wave, lane, CK);
         }
     };
+    // reserved groups of both buffers (ordered before any read by the first chunk barrier; the
+    // copies never write them)
+    for (int i = tid; i < 2 * CK * 4; i += 256) {
+        const int buf = i / (CK * 4), r = i - buf * CK * 4;
+        raw0[buf * rawf + (r >> 2) * PL + PZ + (r & 3)] = PRO == PRO_RAW ? 0.f : __builtin_nanf("");
+    }
     issue(0, 0u);
     for (int k = 0; k < nchunk; ++k) {
         const int c0 = k * CK;
         float* raw = raw0 + (k & 1) * rawf;
         float* wts = wts0 + (k & 1) * wtsf;
-        if (!(PCX_CONV_EXPT & 8) || k == 0) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();  // chunk k visible to all waves; chunk k-1 fully consumed
-        }
-        if (k + 1 < nchunk && !(PCX_CONV_EXPT & 1)) issue(c0 + CK, (unsigned)((k + 1) & 1));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // chunk k visible to all waves; chunk k-1 fully consumed
+        if (k + 1 < nchunk) issue(c0 + CK, (unsigned)((k + 1) & 1));
         float4 cf[CK / 2];
         if (PRO != PRO_RAW) {
 #pragma unroll
@@ -291,13 +298,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_occ(WM)
         float av[2][WM], rv[2][WN];
         auto load = [&](int st, float (&a_)[WM], float (&r_)[WN]) {
             const int tap = st / (CK / 2), s = st % (CK / 2);
-            const int toff = (tap / 3 - 1) * a.W + (tap % 3 - 1);
+            const int dh = tap / 3 - 1, dw = tap % 3 - 1;
+            const int toff = dh * a.W + dw;
 #pragma unroll
             for (int mi = 0; mi < WM; ++mi) a_[mi] = wts[(tap * CK + 2 * s + h) * COUT_T + mi * 32 + l32];
 #pragma unroll
             for (int ni = 0; ni < WN; ++ni) {
-                const int o = (2 * s + h) * PL + pixoff[ni] + toff;
-                r_[ni] = (PCX_CONV_EXPT & 32) ? (float)(o & 7) : raw[o];
+                bool ok = true;
+                if (dh < 0) ok = ok && vup[ni];
+                if (dh > 0) ok = ok && vdn[ni];
+                if (dw < 0) ok = ok && vl[ni];
+                if (dw > 0) ok = ok && vr[ni];
+                r_[ni] = raw[(2 * s + h) * PL + (ok ? pixoff[ni] + toff : PZ)];
             }
         };
         load(0, av[0], rv[0]);
@@ -306,50 +318,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_occ(WM)
             const int cur = st & 1;
             if (st + 1 < NST) load(st + 1, av[cur ^ 1], rv[cur ^ 1]);
             __builtin_amdgcn_sched_barrier(0);
-            const int tap = st / (CK / 2), s = st % (CK / 2);
-            const int dh = tap / 3 - 1, dw = tap % 3 - 1;
+            const int s = st % (CK / 2);
             float bv[WN];
 #pragma unroll
-            for (int ni = 0; ni < WN; ++ni) {
-                float v;
-                if (PRO == PRO_RAW || (PCX_CONV_EXPT & 16)) {
-                    v = rv[cur][ni];
-                } else {  // PRO_BNRELU
-                    v = fmaxf(fmaf(rv[cur][ni], cf[s].x, cf[s].y), 0.f);
-                }
-                bool ok = true;
-                if (PCX_CONV_EXPT & 16) {
-                    bv[ni] = v;
-                    continue;
-                }
-                if (dh < 0) ok = ok && vup[ni];
-                if (dh > 0) ok = ok && vdn[ni];
-                if (dw < 0) ok = ok && vl[ni];
-                if (dw > 0) ok = ok && vr[ni];
-                bv[ni] = ok ? v : 0.f;
-            }
+            for (int ni = 0; ni < WN; ++ni)
+                bv[ni] = PRO == PRO_RAW ? rv[cur][ni] : fmaxf(fmaf(rv[cur][ni], cf[s].x, cf[s].y), 0.f);
 #pragma unroll
             for (int mi = 0; mi < WM; ++mi)
 #pragma unroll
-                for (int ni = 0; ni < WN; ++ni) {
-                    if (PCX_CONV_EXPT & 2) acc[mi][ni][0] = fmaf(av[cur][mi], bv[ni], acc[mi][ni][0]);
-                    else acc[mi][ni] = mfma32(av[cur][mi], bv[ni], acc[mi][ni]);
-                }
+                for (int ni = 0; ni < WN; ++ni) acc[mi][ni] = mfma32(av[cur][mi], bv[ni], acc[mi][ni]);
             __builtin_amdgcn_sched_barrier(0);
         }
     }
     __syncthreads();  // LDS is reused for the cross-wave statistics
-    if (PCX_CONV_EXPT & 4) {
-        float t = 0.f;
-#pragma unroll
-        for (int mi = 0; mi < WM; ++mi)
-#pragma unroll
-            for (int ni = 0; ni < WN; ++ni)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) t += acc[mi][ni][r];
-        if (t == 1234.5f) a.out[tid] = t;
-        return;
-    }
     conv_epilogue<WM, WN, EPI>(a, acc, smem, tile, n0, m0, Mtot, HW, wave, tid, valid, pb, pp);
 }
 
@@ -438,17 +419,19 @@ int launch_conv3x3_dma(int pro, int epi, ConvArgs a, hipStream_t s) {
     // rows span at most NR / H + 2 samples plus an invalid run at either end; each segment costs
     // at most 7 floats of alignment gap.
     const int64_t HW = (int64_t)a.H * a.W;
+    // (channel planes of the staged image carry one more 16-byte group: the reserved value of
+    // out-of-sample taps)
     const int PLseg = ((a.NR * a.W + 8 * (a.NR / a.H + 4)) + 3) & ~3;
-    int ck = conv3x3_dma_ck(a.cout, PLseg, a.NR, a.cin);
-    bool pre = HW % 4 == 0 && a.cin % ck == 0 && ceil_div(ck * PLseg, 1024) <= DMA_MAXR &&
+    int ck = conv3x3_dma_ck(a.cout, PLseg + 4, a.NR, a.cin);
+    bool pre = HW % 4 == 0 && a.cin % ck == 0 && ceil_div(ck * (PLseg + 4), 1024) <= DMA_MAXR &&
                ceil_div(9 * ck * cout_t, 1024) <= DMA_MAXW &&
                (int64_t)((a.NR / a.H + 3) * a.cin) * HW * 4 < ((int64_t)1 << 31);
-    int vec = 4, PL = PLseg;
+    int vec = 4, PL = PLseg + 4;
     if (pre) {
         a.RS = PLseg;
     } else {
         vec = (a.W % 4 == 0) ? 4 : 1;
-        PL = a.NR * a.W;
+        PL = ((a.NR * a.W + 3) & ~3) + 4;
         ck = conv3x3_dma_ck(a.cout, PL, a.NR, a.cin);
     }
     PCX_CHECK_ARG(a.cin % ck == 0, "conv3x3: cin %d not a multiple of %d", a.cin, ck);
