@@ -198,6 +198,266 @@ __global__ __launch_bounds__(256) void wgrad1_kernel(Wgrad1Args a) {
     }
 }
 
+// ------------------------------------------------------------------ 7x7 stem (Cin = 1), cnn_deep
+// PhonemeNetDeep's stem conv (reference phoneme_cnn.py:211-216: Conv2d(1, C0, 7, padding 3)): its
+// output is C0 (64) times the input, so the forward is HBM-write-bound and the weight gradient
+// (reads dz0, y0) HBM-read-bound -- direct VALU kernels instead of the general implicit GEMM
+// (which gathered a 49-long K per pixel: 20-30 % of the MFMA roof).
+//  * a block walks whole samples; each sample's input is staged once in LDS with a zero border
+//    (3 rows, 4 columns), so a lane's 7 x 12 window is 21 unconditional ds_read_b128;
+//  * lanes own pixel quads; forward: a wave owns CPW output channels whose weights are
+//    wave-uniform scalar loads (SGPR operands); BN partial statistics shifted sums in the same
+//    pass; weight gradient: a wave owns 2 output channels x 49 taps of accumulators and computes
+//    dy = BN backward of (dz0, y0) from its 16-byte loads (no dy pass);
+//  * BF16 (precision "bf16"): operands rounded to bf16 as the bf16 implicit GEMM rounds them
+//    (input, weights, dy), products exact, float32 sums.
+constexpr int ST_K = 7, ST_T = 49, ST_WCPW = 2;
+
+__device__ __forceinline__ float bf16r(float v) { return (float)(__bf16)v; }
+typedef const __attribute__((address_space(4))) float* cfloat4p;  // constant space: scalar loads
+
+__host__ __device__ constexpr int st_rw(int W) { return ((W + 8) + 3) & ~3; }  // LDS row: 4 | W | >= 4
+
+// LDS image of one sample: [H + 6][RW] with the input at (row 3, column 4) and zeros around.
+// The border never changes: st_zero clears the whole image once per block, st_stage rewrites
+// the interior per sample (16-byte loads, all issued before the LDS writes, when W % 4 == 0).
+__device__ __forceinline__ void st_zero(int H, int W, float* xs) {
+    const int n = (H + 6) * st_rw(W);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) xs[i] = 0.f;
+}
+
+template <bool BF>
+__device__ __forceinline__ void st_stage(const float* xb, int H, int W, float* xs) {
+    const int RW = st_rw(W);
+    if ((W & 3) == 0) {
+        const int nq = W >> 2, n = H * nq;
+        constexpr int U = 8;
+        for (int base = 0; base < n; base += U * 256) {
+            float4 t[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const int i = base + k * 256 + (int)threadIdx.x;
+                t[k] = i < n ? ld4(xb + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const int i = base + k * 256 + (int)threadIdx.x;
+                if (i < n) {
+                    const int r = i / nq, q = i - r * nq;
+                    float4 v = t[k];
+                    if (BF) { v.x = bf16r(v.x); v.y = bf16r(v.y); v.z = bf16r(v.z); v.w = bf16r(v.w); }
+                    *reinterpret_cast<float4*>(xs + (r + 3) * RW + 4 + 4 * q) = v;
+                }
+            }
+        }
+    } else {
+        const int n = H * W;
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            const int r = i / W, c = i - r * W;
+            const float v = xb[i];
+            xs[(r + 3) * RW + 4 + c] = BF ? bf16r(v) : v;
+        }
+    }
+}
+
+// window of the quad at (hh, w0): v[dh][e] = x[hh + dh - 3][w0 - 4 + e], e < 12
+__device__ __forceinline__ void st_window(const float* xs, int RW, int hh, int w0, float (&v)[ST_K][12]) {
+#pragma unroll
+    for (int dh = 0; dh < ST_K; ++dh) {
+        const float* r = xs + (hh + dh) * RW + w0;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const float4 t = *reinterpret_cast<const float4*>(r + 4 * q);
+            v[dh][4 * q] = t.x; v[dh][4 * q + 1] = t.y; v[dh][4 * q + 2] = t.z; v[dh][4 * q + 3] = t.w;
+        }
+    }
+}
+
+template <bool BF, int CPW>
+__global__ __launch_bounds__(256) void stem_fwd_kernel(StemArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float xs[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int H = a.H, W = a.W, HW = H * W, RW = st_rw(W);
+    const int nq = (W + 3) >> 2, ntask = H * nq;
+    const int cg = wave * CPW;  // a.cout == 4 CPW
+    cfloat4p w = (cfloat4p)a.w;  // [C][49] (bf16-rounded for BF)
+    float K[CPW], s1[CPW], s2[CPW];
+#pragma unroll
+    for (int j = 0; j < CPW; ++j) s1[j] = s2[j] = 0.f;
+    int nsamp = 0;
+    st_zero(H, W, xs);
+    for (int b = blockIdx.x; b < a.B; b += gridDim.x, ++nsamp) {
+        __syncthreads();
+        st_stage<BF>(a.x + (int64_t)b * HW, H, W, xs);
+        __syncthreads();
+        if (b == (int)blockIdx.x) {  // shift for the one-pass variance: the block's first output
+            float v[ST_K][12];
+            st_window(xs, RW, 0, 0, v);
+#pragma unroll
+            for (int j = 0; j < CPW; ++j) {
+                float acc = 0.f;
+#pragma unroll
+                for (int t = 0; t < ST_T; ++t) acc = fmaf(w[(cg + j) * ST_T + t], v[t / ST_K][4 + t % ST_K - 3], acc);
+                K[j] = acc;
+            }
+        }
+        float* ob = a.out + ((int64_t)b * a.cout + cg) * HW;
+        for (int t = lane; t < ntask; t += 64) {
+            const int hh = t / nq, w0 = 4 * (t - hh * nq);
+            float v[ST_K][12];
+            st_window(xs, RW, hh, w0, v);
+#pragma unroll
+            for (int j = 0; j < CPW; ++j) {
+                // an opaque zero keeps the weight loads inside the task loop: 49 SGPRs live per
+                // channel instead of CPW x 49 hoisted ones spilling to VGPR lanes
+                int z;
+                asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+                const cfloat4p wj = w + (cg + j) * ST_T + z;
+                float o[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int tp = 0; tp < ST_T; ++tp) {
+                    const float wt = wj[tp];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) o[e] = fmaf(wt, v[tp / ST_K][e + 4 + tp % ST_K - 3], o[e]);
+                }
+                float* op = ob + (int64_t)j * HW + hh * W + w0;
+                if ((W & 3) == 0) {
+                    st4(op, make_float4(o[0], o[1], o[2], o[3]));
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float d = o[e] - K[j];
+                        s1[j] += d;
+                        s2[j] = fmaf(d, d, s2[j]);
+                    }
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (w0 + e < W) {
+                            op[e] = o[e];
+                            const float d = o[e] - K[j];
+                            s1[j] += d;
+                            s2[j] = fmaf(d, d, s2[j]);
+                        }
+                }
+            }
+        }
+    }
+    const float n = (float)nsamp * (float)HW;
+#pragma unroll
+    for (int j = 0; j < CPW; ++j) {
+        const float t1 = wave_sum(s1[j]), t2 = wave_sum(s2[j]);
+        if (lane == 0) {
+            a.part0[(int64_t)(cg + j) * a.nblk + blockIdx.x] = n * K[j] + t1;
+            a.part1[(int64_t)(cg + j) * a.nblk + blockIdx.x] = n > 0.f ? fmaxf(t2 - t1 * t1 / n, 0.f) : 0.f;
+        }
+    }
+    if (threadIdx.x == 0) a.partn[blockIdx.x] = n;
+}
+
+template <bool BF>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void stem_wgrad_kernel(StemArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float xs[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int H = a.H, W = a.W, HW = H * W, RW = st_rw(W);
+    const int nq = (W + 3) >> 2, ntask = H * nq;
+    const int slice = blockIdx.y;
+    const int b0 = slice * a.rows_per_blk, b1 = min(a.B, b0 + a.rows_per_blk);  // samples of the slice
+    const int cg = (blockIdx.x * 4 + wave) * ST_WCPW;
+    const bool live = cg < a.cout;  // (a.cout % ST_WCPW == 0)
+    float acc[ST_WCPW][ST_T];
+    float A1[ST_WCPW], A2[ST_WCPW], A3[ST_WCPW];
+#pragma unroll
+    for (int j = 0; j < ST_WCPW; ++j) {
+        const float4 k = a.cf_dy[live ? cg + j : 0];  // dy = a (dz - mb - (y - mean) mgi)
+        A1[j] = k.x;
+        A2[j] = -k.x * k.z;
+        A3[j] = k.x * (k.w * k.z - k.y);
+#pragma unroll
+        for (int t = 0; t < ST_T; ++t) acc[j][t] = 0.f;
+    }
+    st_zero(H, W, xs);
+    for (int b = b0; b < b1; ++b) {
+        __syncthreads();
+        st_stage<BF>(a.x + (int64_t)b * HW, H, W, xs);
+        __syncthreads();
+        if (!live) continue;
+        const float* dzb = a.dz + ((int64_t)b * a.cout + cg) * HW;
+        const float* yb = a.y + ((int64_t)b * a.cout + cg) * HW;
+        // (dz, y) of the lane's next task are in flight while the current one accumulates
+        float4 cz[ST_WCPW], cy[ST_WCPW];
+        auto fetch = [&](int t, float4 (&z)[ST_WCPW], float4 (&y)[ST_WCPW]) {
+            const int hh = t / nq, w0 = 4 * (t - hh * nq);
+#pragma unroll
+            for (int j = 0; j < ST_WCPW; ++j) {
+                const int o = j * HW + hh * W + w0;
+                if ((W & 3) == 0) {
+                    z[j] = ld4(dzb + o);
+                    y[j] = ld4(yb + o);
+                } else {
+                    z[j].x = dzb[o];
+                    y[j].x = yb[o];
+                    z[j].y = w0 + 1 < W ? dzb[o + 1] : 0.f;
+                    y[j].y = w0 + 1 < W ? yb[o + 1] : 0.f;
+                    z[j].z = w0 + 2 < W ? dzb[o + 2] : 0.f;
+                    y[j].z = w0 + 2 < W ? yb[o + 2] : 0.f;
+                    z[j].w = w0 + 3 < W ? dzb[o + 3] : 0.f;
+                    y[j].w = w0 + 3 < W ? yb[o + 3] : 0.f;
+                }
+            }
+        };
+        if (lane < ntask) fetch(lane, cz, cy);
+        for (int t = lane; t < ntask; t += 64) {
+            const int hh = t / nq, w0 = 4 * (t - hh * nq);
+            float dy[ST_WCPW][4];
+#pragma unroll
+            for (int j = 0; j < ST_WCPW; ++j) {
+                const float dz[4] = {cz[j].x, cz[j].y, cz[j].z, cz[j].w};
+                const float yy[4] = {cy[j].x, cy[j].y, cy[j].z, cy[j].w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float d = fmaf(A1[j], dz[e], fmaf(A2[j], yy[e], A3[j]));
+                    if ((W & 3) != 0 && w0 + e >= W) d = 0.f;
+                    dy[j][e] = BF ? bf16r(d) : d;
+                }
+            }
+            if (t + 64 < ntask) fetch(t + 64, cz, cy);
+            // one window row at a time: 12 registers of input instead of 84
+#pragma unroll
+            for (int dh = 0; dh < ST_K; ++dh) {
+                const float* r = xs + (hh + dh) * RW + w0;
+                float v[12];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    const float4 t4 = *reinterpret_cast<const float4*>(r + 4 * q);
+                    v[4 * q] = t4.x; v[4 * q + 1] = t4.y; v[4 * q + 2] = t4.z; v[4 * q + 3] = t4.w;
+                }
+#pragma unroll
+                for (int j = 0; j < ST_WCPW; ++j)
+#pragma unroll
+                    for (int k = 0; k < ST_K; ++k)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            acc[j][dh * ST_K + k] = fmaf(dy[j][e], v[e + 1 + k], acc[j][dh * ST_K + k]);
+            }
+        }
+    }
+    if (!live) return;
+#pragma unroll
+    for (int j = 0; j < ST_WCPW; ++j)
+#pragma unroll
+        for (int t = 0; t < ST_T; ++t) {
+            const float v = wave_sum(acc[j][t]);
+            if (lane == 0) a.part[((int64_t)slice * a.cout + cg + j) * ST_T + t] = v;
+        }
+}
+
+__global__ void round_bf16_kernel(const float* __restrict__ in, float* __restrict__ out, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = bf16r(in[i]);
+}
+
 // out[e] = sum_k part[k][e]: a block owns 32 consecutive outputs; its 8 thread groups sum slices
 // g, g + 8, ... (coalesced 128-byte rows), then the 8 group sums are added in a fixed order
 // (deterministic; the previous one-thread-per-output form left most of the chip idle for the
@@ -255,6 +515,63 @@ size_t conv3x3_nblk(int B, int H, int W, int cout) {
     return (size_t)ceil_div(M, 4 * wn * 32);
 }
 
+
+// forward: blocks walk samples b = block, block + nblk, ...; weight gradient: slices of samples
+int stem_nblk(int B, int H, int* rows_per_blk) {
+    (void)H;
+    *rows_per_blk = 1;
+    return std::min(B, 2048);
+}
+
+int stem_wgrad_nslice(int B, int H, int* rows_per_slice) {
+    (void)H;
+    const int sps = std::max(1, B / 256);  // samples per slice
+    *rows_per_slice = sps;
+    return ceil_div(B, sps);
+}
+
+static size_t stem_smem(int H, int W) { return (size_t)(H + 6) * st_rw(W) * 4; }
+
+int launch_stem_fwd(StemArgs a, int bf16, float* wround, hipStream_t s) {
+    PCX_CHECK_ARG(a.cout == 8 || a.cout == 16 || a.cout % 64 == 0 && a.cout <= 64,
+                  "stem: cout %d unsupported (8, 16, 64)", a.cout);
+    PCX_CHECK_ARG((int64_t)a.B * a.cout * a.H * a.W < ((int64_t)1 << 40) && stem_smem(a.H, a.W) <= 160 * 1024,
+                  "stem: %dx%d input too large", a.H, a.W);
+    if (bf16) {  // the GEMM's bf16 operand rounding, applied to the weights once
+        const int n = a.cout * ST_T;
+        round_bf16_kernel<<<ceil_div(n, 256), 256, 0, s>>>(a.w, wround, n);
+        PCX_LAUNCH_CHECK("round_bf16_kernel");
+        a.w = wround;
+    }
+    const size_t sm = stem_smem(a.H, a.W);
+#define PCX_STEM_F(B_, C_)                                                                          \
+    if ((bf16 != 0) == B_ && a.cout == 4 * C_) {                                                    \
+        (void)hipFuncSetAttribute((const void*)stem_fwd_kernel<B_, C_>,                              \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);             \
+        stem_fwd_kernel<B_, C_><<<a.nblk, 256, sm, s>>>(a);                                         \
+    }
+    PCX_STEM_F(false, 16) PCX_STEM_F(true, 16) PCX_STEM_F(false, 4) PCX_STEM_F(true, 4)
+    PCX_STEM_F(false, 2) PCX_STEM_F(true, 2)
+#undef PCX_STEM_F
+    PCX_LAUNCH_CHECK("stem_fwd_kernel");
+    return PCX_OK;
+}
+
+int launch_stem_wgrad(StemArgs a, int bf16, hipStream_t s) {
+    PCX_CHECK_ARG(a.cout % ST_WCPW == 0, "stem: cout %d must be even", a.cout);
+    PCX_CHECK_ARG(stem_smem(a.H, a.W) <= 160 * 1024, "stem: %dx%d input too large", a.H, a.W);
+    const size_t sm = stem_smem(a.H, a.W);
+    dim3 grid((unsigned)ceil_div(a.cout, 4 * ST_WCPW), (unsigned)a.nblk);
+    if (bf16) {
+        (void)hipFuncSetAttribute((const void*)stem_wgrad_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+        stem_wgrad_kernel<true><<<grid, 256, sm, s>>>(a);
+    } else {
+        (void)hipFuncSetAttribute((const void*)stem_wgrad_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+        stem_wgrad_kernel<false><<<grid, 256, sm, s>>>(a);
+    }
+    PCX_LAUNCH_CHECK("stem_wgrad_kernel");
+    return PCX_OK;
+}
 
 int conv1_nblk(int B, int H, int* rows_per_blk) {
     int64_t nrows = (int64_t)B * H;

@@ -35,6 +35,8 @@ struct DeepPlan {
     int h[4];
     int H0, W0, H1, W1;
     size_t y0, a0, cf0, cfb0, dz0, mparg;
+    size_t stemw;                  // bf16-rounded stem weights (precision "bf16")
+    int stem_nblk, stem_rows, stem_ns, stem_srows;  // stem forward blocks / weight-gradient slices
     size_t wpk, identw;           // packed 3x3 weights of a routed conv; identity BN coefficients
     size_t wpk16;                 // packed GEMM weights of the current general-engine conv
     int cmax;
@@ -85,8 +87,12 @@ int build_deep(Plan& p) {
         int ns = chan_slices(B, C, &bps);
         stat = std::max(stat, (size_t)3 * C * ns + ns);
     };
-    stat_need(C0);
-    wg_need(1, C0, 7, d.H0, d.W0);
+    // the 7x7 stem runs on its own direct kernels (conv.hip): forward partials, gradient slices
+    d.stem_nblk = stem_nblk(B, d.H0, &d.stem_rows);
+    d.stem_ns = stem_wgrad_nslice(B, d.H0, &d.stem_srows);
+    stat = std::max(stat, (size_t)3 * C0 * d.stem_nblk + d.stem_nblk);
+    wg = std::max(wg, (size_t)d.stem_ns * C0 * 49);
+    d.stemw = p.carve("stem_w16", (size_t)C0 * 49 * 4);
     size_t wpk = 0;
     int cmax = 0;
     for (int i = 0; i < 4; ++i) cmax = std::max(cmax, d.h[i]);
@@ -368,9 +374,27 @@ int deep_forward(const Plan& p, const float* const* P, float* const* bnstat, int
     auto bnp = [&](int idx, int j) { return bnstat[2 * idx + j]; };
     auto nb = [&](int idx) { return nbt ? nbt[idx] : nullptr; };
     const int C0 = d.h[0];
-    // stem
-    RC(conv_bn_fwd(c, "conv_fwd", 0, x, 1, d.H0, d.W0, 7, 1, 3, P[0], c.w<float>(d.y0), C0, d.H0, d.W0, P[2], P[3],
-                   P[1], bnp(0, 0), bnp(0, 1), nb(0), train, c.w<float4>(d.cf0)));
+    // stem: direct 7x7 kernel with the BN partials in the same pass, then the BN finaliser
+    {
+        StemArgs sa{};
+        sa.B = B; sa.H = d.H0; sa.W = d.W0; sa.cout = C0;
+        sa.x = x; sa.w = P[0]; sa.out = c.w<float>(d.y0);
+        sa.nblk = d.stem_nblk; sa.rows_per_blk = d.stem_rows;
+        float* part = c.w<float>(d.stat);
+        sa.part0 = part;
+        sa.part1 = part + (size_t)C0 * sa.nblk;
+        sa.partn = part + (size_t)2 * C0 * sa.nblk;
+        { Scope sc(&p.prof, s, "conv_fwd", 0); RC(launch_stem_fwd(sa, d.bf16, c.w<float>(d.stemw), s)); }
+        BnFwdArgs f{};
+        f.C = C0; f.nblk = sa.nblk;
+        f.part0 = sa.part0; f.part1 = sa.part1; f.partn = sa.partn;
+        f.gamma = P[2]; f.beta = P[3]; f.bias = P[1];
+        f.rmean = bnp(0, 0); f.rvar = bnp(0, 1); f.nbt = nb(0);
+        f.momentum = 0.1f; f.eps = 1e-5f; f.train = train;
+        f.cf = c.w<float4>(d.cf0);
+        Scope sc(&p.prof, s, "bn_fwd_finalize");
+        RC(launch_bn_fwd_finalize(f, s));
+    }
     {
         Scope sc(&p.prof, s, "maxpool_fwd");
         RC(launch_maxpool3_fwd(c.w<float>(d.y0), c.w<float4>(d.cf0), c.w<float>(d.a0), c.w<uint8_t>(d.mparg), B, C0,
@@ -645,18 +669,19 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
         RC(bn_bwd(c, C0, ns, b.p_g, b.p_x1, P[2], c.w<float4>(d.cf0), G[2], G[3], c.w<float4>(d.cfb0),
                   (double)B * P0));
     }
-    // the stem's dy feeds only its weight gradient: the fp32 engine applies the BN backward while
-    // staging (one pass over y0 / g instead of three); the bf16 engine's pixel-pair staging is
-    // faster on a materialised dy (measured: 3.3 ms + apply vs 11 ms fused)
-    if (!d.bf16) {
-        RC(conv_wgrad(c, 0, x, 1, d.H0, d.W0, 7, 1, 3, nullptr, C0, d.H0, d.W0, G[0], G[1], nullptr, dz0,
-                      c.w<float>(d.y0), c.w<float4>(d.cfb0)));
-    } else {
-        {
-            Scope sc(&p.prof, s, "bn_bwd_apply");
-            RC(launch_bn_bwd_apply(dz0, c.w<float>(d.y0), c.w<float4>(d.cfb0), dz0, B, C0, P0, s));
-        }
-        RC(conv_wgrad(c, 0, x, 1, d.H0, d.W0, 7, 1, 3, dz0, C0, d.H0, d.W0, G[0], G[1]));
+    // the stem's dy feeds only its weight gradient: the direct stem kernel applies the BN backward
+    // to (dz0, y0) as it loads them (no dy pass)
+    {
+        StemArgs sa{};
+        sa.B = B; sa.H = d.H0; sa.W = d.W0; sa.cout = C0;
+        sa.x = x; sa.dz = dz0; sa.y = c.w<float>(d.y0); sa.cf_dy = c.w<float4>(d.cfb0);
+        float* wgp = c.w<float>(d.wgp);
+        sa.part = wgp;
+        sa.nblk = d.stem_ns; sa.rows_per_blk = d.stem_srows;
+        { Scope sc(&p.prof, s, "wgrad", 0); RC(launch_stem_wgrad(sa, d.bf16, s)); }
+        RC(launch_sum_slices(wgp, sa.nblk, (int64_t)C0 * 49, G[0], s));
+        // the stem conv feeds a train-mode BN: its bias gradient is exactly 0
+        RC(hip_status_ok(hipMemsetAsync(G[1], 0, (size_t)C0 * 4, s), "memset bias grad"));
     }
     p.buckets.mark(0, s);
     return PCX_OK;

@@ -97,6 +97,27 @@ int launch_wgrad_w32(int pro, WgradArgs a, hipStream_t s);
 bool wgrad_s_geometry(int B, int H, int W, int cin, int cout, WgradArgs* a, int force_cw = 0);
 int launch_wgrad_s(int pro, WgradArgs a, hipStream_t s);
 
+// PhonemeNetDeep 7x7 stem (Cin = 1, pad 3): direct forward + BN partials, weight gradient with the
+// BN backward of (dz, y) in its loads (conv.hip)
+struct StemArgs {
+    int B, H, W, cout;
+    const float* x;       // [B][1][H][W]
+    const float* w;       // [cout][1][7][7]
+    float* out;           // forward: y [B][cout][H][W]
+    float* part0;         // forward: BN partials [cout][nblk] (sum, M2), counts [nblk]
+    float* part1;
+    float* partn;
+    const float* dz;      // weight gradient: dz0, y0 and the BN-backward coefficients
+    const float* y;
+    const float4* cf_dy;
+    float* part;          // weight gradient: [nblk slices][cout][49]
+    int nblk, rows_per_blk;
+};
+int stem_nblk(int B, int H, int* rows_per_blk);
+int stem_wgrad_nslice(int B, int H, int* rows_per_slice);
+int launch_stem_fwd(StemArgs a, int bf16, float* wround, hipStream_t s);  // wround: [cout][49] scratch (bf16)
+int launch_stem_wgrad(StemArgs a, int bf16, hipStream_t s);
+
 // first-layer (Cin = 1) weight gradient
 struct Wgrad1Args {
     int B, H, W, cout;
