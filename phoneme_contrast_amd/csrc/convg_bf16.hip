@@ -443,6 +443,8 @@ int launch_convg_bf16(ConvGArgs a, hipStream_t s) {
                                                                            Kp, K);
         PCX_LAUNCH_CHECK("pack_wbf16_kernel");
     }
+    // channel-last operands supplied: the convn.hip engine (same packed weights, same rounding)
+    if (a.mode == 2 ? (a.xn && a.dyn) : a.mode == 0 ? a.xn != nullptr : a.dyn != nullptr) return launch_convn(a, s);
     dim3 grid((unsigned)nblocks);
 #define PCX_CB(MODE_, KH_, WM_)                                                                 \
     if (a.mode == MODE_ && a.KH == KH_ && wm == WM_) {                                          \
@@ -476,8 +478,24 @@ size_t convg_bf16_wpack_bytes(int mode, int cin, int cout, int k) {
 // ---------------------------------------------------------------------------------------------
 // The cnn_deep convolution engine as a standalone operation (include/pcx.h: pcx_conv2d): used by
 // the kernel-level parity tests of both precisions and by micro-benchmarks.
-extern "C" size_t pcx_conv2d_workspace_bytes(int mode, int precision, int B, int cin, int cout, int OH, int OW,
-                                             int k) {
+namespace {
+// channel-last scratch of the bf16 engine (convn.hip) behind pcx_conv2d: x image, dy image
+struct Conv2dNhwc {
+    bool on;
+    size_t xb, dyb;
+};
+Conv2dNhwc conv2d_nhwc(int mode, int precision, int B, int cin, int cout, int IH, int IW, int OH, int OW, int k,
+                       int pad) {
+    pcx::ConvGArgs a{};
+    a.mode = mode; a.cin = cin; a.cout = cout; a.KH = a.KW = k; a.pad = pad;
+    Conv2dNhwc r{false, 0, 0};
+    if (!precision || !pcx::convn_fits(a)) return r;
+    r.on = true;
+    if (mode != 1) r.xb = (pcx::nhwc_bytes(B, cin, IH, IW) + 255) / 256 * 256;
+    if (mode != 0) r.dyb = (pcx::nhwc_bytes(B, cout, OH, OW) + 255) / 256 * 256;
+    return r;
+}
+size_t conv2d_base_bytes(int mode, int precision, int B, int cin, int cout, int OH, int OW, int k) {
     if (mode != 2)
         return ((precision ? pcx::convg_bf16_wpack_bytes(mode, cin, cout, k) : pcx::convg_wpack_bytes(mode, cin, cout, k)) +
                 255) / 256 * 256;
@@ -485,7 +503,18 @@ extern "C" size_t pcx_conv2d_workspace_bytes(int mode, int precision, int B, int
     a.B = B; a.cin = cin; a.cout = cout; a.OH = OH; a.OW = OW; a.KH = a.KW = k;
     int64_t ks;
     const int ns = pcx::convg_nslice(a, &ks);
-    return (size_t)ns * cout * cin * k * k * 4;
+    return ((size_t)ns * cout * cin * k * k * 4 + 255) / 256 * 256;
+}
+}  // namespace
+
+// (the input resolution is implied: the bf16 channel-last scratch is sized for stride 1, the larger)
+extern "C" size_t pcx_conv2d_workspace_bytes(int mode, int precision, int B, int cin, int cout, int OH, int OW,
+                                             int k) {
+    const size_t base = conv2d_base_bytes(mode, precision, B, cin, cout, OH, OW, k);
+    if (!precision) return base;
+    // upper bound of the input image over strides 1 and 2: IH <= 2 OH + k, IW <= 2 OW + k
+    const Conv2dNhwc n = conv2d_nhwc(mode, precision, B, cin, cout, 2 * OH + k, 2 * OW + k, OH, OW, k, 1);
+    return base + n.xb + n.dyb;
 }
 
 extern "C" int pcx_conv2d(int mode, int precision, int B, int cin, int cout, int IH, int IW, int OH, int OW, int k,
@@ -507,16 +536,33 @@ extern "C" int pcx_conv2d(int mode, int precision, int B, int cin, int cout, int
     a.x = x; a.w = w; a.dy = dy; a.out = out;
     a.accumulate = accumulate;
     a.bf16 = precision;
-    const size_t need = pcx_conv2d_workspace_bytes(mode, precision, B, cin, cout, OH, OW, k);
+    const size_t base = conv2d_base_bytes(mode, precision, B, cin, cout, OH, OW, k);
+    const Conv2dNhwc n = conv2d_nhwc(mode, precision, B, cin, cout, IH, IW, OH, OW, k, pad);
+    const size_t need = base + n.xb + n.dyb;
     PCX_CHECK_ARG(need == 0 || (ws && ws_bytes >= need), "pcx_conv2d: needs %zu workspace bytes, got %zu", need,
                   ws_bytes);
+    if (n.on) {  // channel-last bf16 operands for convn.hip
+        char* nb = static_cast<char*>(ws) + base;
+        if (n.xb) {
+            NhwcArgs t{};
+            t.op = NHWC_COPY; t.B = B; t.C = cin; t.H = IH; t.W = IW; t.src = x; t.dst = nb;
+            const int rc = launch_to_nhwc(t, stream);
+            if (rc != PCX_OK) return rc;
+            a.xn = nb;
+        }
+        if (n.dyb) {
+            NhwcArgs t{};
+            t.op = NHWC_COPY; t.B = B; t.C = cout; t.H = OH; t.W = OW; t.src = dy; t.dst = nb + n.xb;
+            const int rc = launch_to_nhwc(t, stream);
+            if (rc != PCX_OK) return rc;
+            a.dyn = nb + n.xb;
+        }
+    }
     if (mode != 2) {
         a.wpack = ws;
         return launch_convg(a, stream);
     }
     a.nslice = convg_nslice(a, &a.kslice);
-    PCX_CHECK_ARG(ws && ws_bytes >= need, "pcx_conv2d: weight gradient needs %zu workspace bytes, got %zu", need,
-                  ws_bytes);
     a.out = static_cast<float*>(ws);
     const int rc = launch_convg(a, stream);
     if (rc != PCX_OK) return rc;

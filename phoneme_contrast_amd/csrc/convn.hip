@@ -1,0 +1,511 @@
+// Channel-last bf16 convolution engine for PhonemeNetDeep with precision "bf16" (SURVEY 8(f) row 2).
+//
+// The general bf16 implicit GEMM (convg_bf16.hip) gathers its operands from planar NCHW float32:
+// every k of a GEMM row is a different channel plane, so each element is its own 4-byte load and
+// the kernel runs at ~10 % of the bf16 MFMA roof.  Here each conv operand is first written once as a
+// zero-padded channel-last bf16 image
+//
+//     xn[b][h + 1][w + 1][c]   (h in [-1, H], w in [-1, W]; the ring is zero = the conv padding)
+//
+// by to_nhwc_kernel (optionally applying the BN backward dy = a (g - mb - (y - mean) mgi) on the
+// way, which replaces the float32 dy pass), and the GEMMs read it in 16-byte runs of 8 channels:
+//  * forward (mode 0) / data gradient (mode 1, stride 1; mode 3, one parity class of stride 2):
+//    M = output channels, N = pixels, K = taps x channels (tap-major, 32 channels per chunk).  A
+//    pixel's operand row for a tap is one contiguous 64-byte run at a tap offset that is the same
+//    for every pixel, so the B tile costs two 16-byte loads per thread and no bounds tests (the
+//    ring supplies the zeros);
+//  * weight gradient (mode 2): M = cout, N = taps x cin, K = pixels.  Both operands are staged
+//    pixel-major ([k][channels], 16-byte runs) and read K-contiguous by ds_read_b64_tr_b16.
+// Operand rounding (bf16 round-to-nearest-even of the float32 value) and float32 accumulation are
+// those of convg_bf16; only the summation order differs.
+#include "kernels.h"
+
+namespace pcx {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int NKB = 32;  // k per chunk
+constexpr int NRS = 40;  // LDS row stride (bf16) of k-contiguous tiles: 80 B, conflict-free ds_read_b128
+
+__device__ __forceinline__ bf16x8 ld16(const __bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+
+__device__ __forceinline__ f32x16 mfma_bf16(bf16x8 a, bf16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// ------------------------------------------------------------------ NCHW float32 -> padded NHWC bf16
+// Block: one sample x 64 channels, row by row, each row transposed through LDS.  The value written is
+//   NHWC_COPY   src
+//   NHWC_BNBWD  a (src - mb - (y - mean) mgi)                 (BN backward, cf = {a, mb, mgi, mean})
+//   NHWC_ACT    drop[b,c] relu(src s + t + res')  res' = res rs + rt | res | 0   (bn_act, cf = {s, t})
+// and NHWC_ACT can also store its float32 NCHW result (out32).  Each thread issues its V-wide loads
+// of a batch before any LDS write, so a block's reads are all in flight together.
+template <int V, int OP>
+__global__ __launch_bounds__(256) void to_nhwc_kernel(NhwcArgs a) {
+    extern __shared__ float t[];  // [64][W + 1]
+    typedef float fv __attribute__((ext_vector_type(V)));
+    const int Hp = a.H + 2, Wp = a.W + 2;
+    const int b = blockIdx.x;
+    const int c0 = blockIdx.y * 64, nc = min(64, a.C - c0), ng = nc >> 3;
+    __bf16* dimg = static_cast<__bf16*>(a.dst) + (int64_t)b * Hp * Wp * a.C + c0;
+    // per-channel coefficients in LDS first: the element loop then waits on nothing but its loads
+    __shared__ float4 kc[64], kr[64];
+    __shared__ float kd[64];
+    if (OP != NHWC_COPY && threadIdx.x < nc) {
+        const int c = c0 + threadIdx.x;
+        kc[threadIdx.x] = a.cf[c];
+        if (OP == NHWC_ACT) {
+            kr[threadIdx.x] = a.rcf ? a.rcf[c] : make_float4(1.f, 0.f, 0.f, 0.f);
+            kd[threadIdx.x] = a.drop ? a.drop[(int64_t)b * a.C + c] : 1.f;
+        }
+    }
+    // the zero ring rows
+    for (int i = threadIdx.x; i < 2 * Wp * ng; i += 256) {
+        const int r = i / (Wp * ng), j = i - r * (Wp * ng);
+        const int wp = j / ng, g = j - wp * ng;
+        *reinterpret_cast<bf16x8*>(dimg + ((int64_t)r * (Hp - 1) * Wp + wp) * a.C + 8 * g) = bf16x8{};
+    }
+    const int W = a.W, TW = W + 1, nv = W / V, n = nc * nv;
+    const int64_t HW = (int64_t)a.H * W;
+    const int64_t pbase = ((int64_t)b * a.C + c0) * HW;
+    constexpr int U = 4;
+    // the block walks its sample's rows: consecutive rows of the same 64 planes (page / line reuse)
+    for (int h = 0; h < a.H; ++h) {
+        const int64_t base = pbase + (int64_t)h * W;
+        __syncthreads();  // (coefficients ready; previous row's LDS reads done)
+        for (int i0 = 0; i0 < n; i0 += U * 256) {
+            fv x[U], y2[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {  // (tail items load a valid element and are dropped below)
+                const int i = min(i0 + u * 256 + (int)threadIdx.x, n - 1);
+                const int c = i / nv, w0 = (i - c * nv) * V;
+                const int64_t o = base + c * HW + w0;
+                x[u] = *reinterpret_cast<const fv*>(a.src + o);
+                if (OP == NHWC_BNBWD) y2[u] = *reinterpret_cast<const fv*>(a.y + o);
+                if (OP == NHWC_ACT) y2[u] = a.res ? *reinterpret_cast<const fv*>(a.res + o) : fv{};
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = i0 + u * 256 + (int)threadIdx.x;
+                if (i < n) {
+                    const int c = i / nv, w0 = (i - c * nv) * V;
+                    fv v = x[u];
+                    if (OP == NHWC_BNBWD) {
+                        const float4 k = kc[c];
+#pragma unroll
+                        for (int e = 0; e < V; ++e) v[e] = k.x * (v[e] - k.y - (y2[u][e] - k.w) * k.z);
+                    } else if (OP == NHWC_ACT) {
+                        const float4 k = kc[c], rk = kr[c];
+                        const float d = kd[c];
+#pragma unroll
+                        for (int e = 0; e < V; ++e) {
+                            float r = fmaf(v[e], k.x, k.y);
+                            if (a.res) r += fmaf(y2[u][e], rk.x, rk.y);
+                            v[e] = d * fmaxf(r, 0.f);
+                        }
+                        if (a.out32) *reinterpret_cast<fv*>(a.out32 + base + c * HW + w0) = v;
+                    }
+#pragma unroll
+                    for (int e = 0; e < V; ++e) t[c * TW + w0 + e] = v[e];
+                }
+            }
+        }
+        __syncthreads();
+        __bf16* drow = dimg + (int64_t)(h + 1) * Wp * a.C;
+        for (int i = threadIdx.x; i < Wp * ng; i += 256) {
+            const int wp = i / ng, g = i - wp * ng;
+            bf16x8 o{};
+            if (wp > 0 && wp <= W) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) o[j] = (__bf16)t[(8 * g + j) * TW + wp - 1];
+            }
+            *reinterpret_cast<bf16x8*>(drow + (int64_t)wp * a.C + 8 * g) = o;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ forward / data gradient
+template <int MODE, int WM>
+__global__ __launch_bounds__(256) void convn_kernel(ConvGArgs a) {
+    constexpr int WN = 2;
+    constexpr int BM = 64 * WM, BN = 64 * WN;
+    __shared__ __attribute__((aligned(16))) __bf16 As[2][BM][NRS];
+    __shared__ __attribute__((aligned(16))) __bf16 Bs[2][BN][NRS];
+
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+    const int wave = tid >> 6, wr = wave >> 1, wc = wave & 1;
+    const int s = a.stride, pad = a.pad;
+    const int ph = a.par >> 1, pw = a.par & 1;
+    const int kh0 = (ph + pad) & 1, kw0 = (pw + pad) & 1;
+    const int64_t OHW = (int64_t)a.OH * a.OW, IHW = (int64_t)a.IH * a.IW;
+    const int IHc = (a.IH - ph + 1) / 2, IWc = (a.IW - pw + 1) / 2;
+    const int64_t CHW = (int64_t)IHc * IWc;
+    int CK, Hp, Wp, nth, ntw;
+    int64_t M, N;
+    if (MODE == 0) {
+        CK = a.cin; Hp = a.IH + 2; Wp = a.IW + 2; M = a.cout; N = a.B * OHW; nth = a.KH; ntw = a.KW;
+    } else {
+        CK = a.cout; Hp = a.OH + 2; Wp = a.OW + 2; M = a.cin;
+        if (MODE == 1) { N = a.B * IHW; nth = a.KH; ntw = a.KW; }
+        else { N = a.B * CHW; nth = (a.KH - kh0 + 1) / 2; ntw = (a.KW - kw0 + 1) / 2; }
+    }
+    const int cpt = CK / NKB, nch = nth * ntw * cpt;
+    const int64_t K = (int64_t)nth * ntw * CK;  // packed row length (a multiple of 32)
+    const int64_t mt = (M + BM - 1) / BM;
+    const int64_t tm = blockIdx.x % mt, tn = blockIdx.x / mt;
+    const int64_t m0 = tm * BM, n0 = tn * BN;
+
+    // B staging: pixel bp of the tile, channels 16 bh .. 16 bh + 15 of every chunk
+    const int bp = tid >> 1, bh = tid & 1;
+    int64_t nn = n0 + bp;
+    if (nn >= N) nn = N - 1;  // tail pixels load a valid row; their columns are never stored
+    int64_t pb;               // image element of the pixel's operand row at tap 0
+    if (MODE == 0) {
+        const int64_t b = nn / OHW;
+        const int r = (int)(nn - b * OHW), oh = r / a.OW, ow = r - oh * a.OW;
+        pb = ((b * Hp + oh * s - pad + 1) * Wp + ow * s - pad + 1) * CK;
+    } else if (MODE == 1) {
+        const int64_t b = nn / IHW;
+        const int r = (int)(nn - b * IHW), ih = r / a.IW, iw = r - ih * a.IW;
+        pb = ((b * Hp + ih + pad + 1) * Wp + iw + pad + 1) * CK;
+    } else {
+        const int64_t b = nn / CHW;
+        const int r = (int)(nn - b * CHW), ihc = r / IWc, iwc = r - ihc * IWc;
+        const int oh0 = (2 * ihc + ph + pad - kh0) >> 1, ow0 = (2 * iwc + pw + pad - kw0) >> 1;
+        pb = ((b * Hp + oh0 + 1) * Wp + ow0 + 1) * CK;
+    }
+    const __bf16* xb = static_cast<const __bf16*>(MODE == 0 ? a.xn : a.dyn) + pb + 16 * bh;
+    // A staging: packed weight rows am, am + 64, k 8 aq .. 8 aq + 7 of every chunk
+    const int am = tid >> 2, aq = tid & 3;
+    const __bf16* ap[WM];
+    bool av[WM];
+#pragma unroll
+    for (int j = 0; j < WM; ++j) {
+        const int64_t row = m0 + am + 64 * j;
+        av[j] = row < M;
+        ap[j] = static_cast<const __bf16*>(a.wpack) + (av[j] ? row : 0) * K + 8 * aq;
+    }
+
+    bf16x8 ra[WM], rb[2];
+    auto gather = [&](int ch) {
+        const int tap = ch / cpt, c0 = (ch - tap * cpt) * NKB;
+        const int th = tap / ntw, tw = tap - th * ntw;
+        const int toff = (MODE == 0 ? 1 : -1) * (th * Wp + tw) * CK + c0;
+        rb[0] = ld16(xb + toff);
+        rb[1] = ld16(xb + toff + 8);
+#pragma unroll
+        for (int j = 0; j < WM; ++j) ra[j] = av[j] ? ld16(ap[j] + (int64_t)ch * NKB) : bf16x8{};
+    };
+    auto stash = [&](int buf) {
+#pragma unroll
+        for (int j = 0; j < WM; ++j) *reinterpret_cast<bf16x8*>(&As[buf][am + 64 * j][8 * aq]) = ra[j];
+        *reinterpret_cast<bf16x8*>(&Bs[buf][bp][16 * bh]) = rb[0];
+        *reinterpret_cast<bf16x8*>(&Bs[buf][bp][16 * bh + 8]) = rb[1];
+    };
+
+    f32x16 acc[WM][WN];
+#pragma unroll
+    for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < WN; ++ni) acc[mi][ni] = f32x16{0.f};
+
+    if (nch > 0) {
+        gather(0);
+        stash(0);
+    }
+    __syncthreads();
+    for (int ch = 0; ch < nch; ++ch) {
+        const int buf = ch & 1;
+        if (ch + 1 < nch) gather(ch + 1);
+#pragma unroll
+        for (int ks = 0; ks < NKB / 16; ++ks) {
+            bf16x8 av8[WM], bv8[WN];
+#pragma unroll
+            for (int mi = 0; mi < WM; ++mi)
+                av8[mi] = *reinterpret_cast<const bf16x8*>(&As[buf][wr * 32 * WM + mi * 32 + l32][16 * ks + 8 * h]);
+#pragma unroll
+            for (int ni = 0; ni < WN; ++ni)
+                bv8[ni] = *reinterpret_cast<const bf16x8*>(&Bs[buf][wc * 32 * WN + ni * 32 + l32][16 * ks + 8 * h]);
+#pragma unroll
+            for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < WN; ++ni) acc[mi][ni] = mfma_bf16(av8[mi], bv8[ni], acc[mi][ni]);
+        }
+        if (ch + 1 < nch) stash(buf ^ 1);
+        __syncthreads();
+    }
+
+    // ---- epilogue: planar NCHW float32 (columns = pixels: 128-byte rows per MFMA output row)
+#pragma unroll
+    for (int ni = 0; ni < WN; ++ni) {
+        const int64_t col = n0 + wc * 32 * WN + ni * 32 + l32;
+        if (col >= N) continue;
+        int64_t obase, ostride;
+        if (MODE == 0) {
+            const int64_t b = col / OHW;
+            obase = b * a.cout * OHW + (col - b * OHW);
+            ostride = OHW;
+        } else if (MODE == 1) {
+            const int64_t b = col / IHW;
+            obase = b * a.cin * IHW + (col - b * IHW);
+            ostride = IHW;
+        } else {
+            const int64_t b = col / CHW, p = col - b * CHW;
+            const int ihc = (int)(p / IWc), iwc = (int)(p - (int64_t)(p / IWc) * IWc);
+            obase = b * a.cin * IHW + (int64_t)(2 * ihc + ph) * a.IW + 2 * iwc + pw;
+            ostride = IHW;
+        }
+#pragma unroll
+        for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int64_t row = m0 + wr * 32 * WM + mi * 32 + acc_row(r, h);
+                if (row < M) {
+                    float* o = a.out + obase + row * ostride;
+                    if (MODE != 0 && a.accumulate) *o += acc[mi][ni][r];
+                    else *o = acc[mi][ni][r];
+                }
+            }
+    }
+}
+
+// ------------------------------------------------------------------ weight gradient
+// Tiles are staged pixel-major, As[k][cout], Bs[k][(tap, cin)], and the MFMA operands (8
+// consecutive k of one row) are read with ds_read_b64_tr_b16: per 16-lane group, 4 k-rows x 16
+// columns delivered column-major.  Row strides of 48 / 80 dwords (= 16 mod 64) put the four k-rows
+// of a read on disjoint bank quarters: conflict-free.
+template <int WM>
+__global__ __launch_bounds__(256) void convn_wgrad_kernel(ConvGArgs a) {
+    constexpr int WN = 2;
+    constexpr int BM = 64 * WM, BN = 64 * WN;
+    constexpr int AS = BM + 32, BS = BN + 32;
+    __shared__ __attribute__((aligned(16))) __bf16 As[2][NKB][AS];
+    __shared__ __attribute__((aligned(16))) __bf16 Bs[2][NKB][BS];
+
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+    const int wave = tid >> 6, wr = wave >> 1, wc = wave & 1;
+    const int s = a.stride, pad = a.pad;
+    const int KK = a.KH * a.KW;
+    const int64_t OHW = (int64_t)a.OH * a.OW;
+    const int64_t M = a.cout, N = (int64_t)a.cin * KK, K = a.B * OHW;
+    const int Hp = a.IH + 2, Wp = a.IW + 2, Hq = a.OH + 2, Wq = a.OW + 2;
+    const int64_t mt = (M + BM - 1) / BM, nt = (N + BN - 1) / BN;
+    int64_t bid = blockIdx.x;
+    const int64_t tm = bid % mt;
+    bid /= mt;
+    const int64_t tn = bid % nt;
+    const int slice = (int)(bid / nt);
+    const int64_t m0 = tm * BM, n0 = tn * BN;
+    const int64_t k_begin = (int64_t)slice * a.kslice, k_end = min(K, k_begin + a.kslice);
+    const int nch = (int)((k_end - k_begin + NKB - 1) / NKB);
+
+    // staging: pixel rows kk = (tid >> 4) + 16 r, 16-byte column group g = tid & 15
+    const int kk0 = tid >> 4, g = tid & 15;
+    // B: columns n0 + 8 g .. + 7 = one tap, 8 input channels
+    const int64_t nb = n0 + 8 * g;
+    const bool bval = nb < N;
+    int xtoff;  // (tap-major columns: n = tap * cin + ci)
+    {
+        const int tap = bval ? (int)(nb / a.cin) : 0, ci = bval ? (int)(nb - (int64_t)tap * a.cin) : 0;
+        const int kh = tap / a.KW, kw = tap - kh * a.KW;
+        xtoff = (kh * Wp + kw) * a.cin + ci;
+    }
+    // A: BM = 128: output channels m0 + 8 g of both rows; BM = 64: row r = g >> 3, channels m0 + 8 (g & 7)
+    constexpr int NA = WM == 2 ? 2 : 1;
+    const int ag = WM == 2 ? g : (g & 7);
+    const int arr = WM == 2 ? 0 : (g >> 3);
+    const bool aval = m0 + 8 * ag < M;
+    const int dytoff = (int)(m0 + 8 * ag);
+
+    const __bf16* xn = static_cast<const __bf16*>(a.xn);
+    const __bf16* dyn = static_cast<const __bf16*>(a.dyn);
+    struct PixPos { int64_t b; int oh, ow; };
+    PixPos pp[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const int64_t q = k_begin + kk0 + 16 * r;
+        pp[r].b = q / OHW;
+        const int rr = (int)(q - pp[r].b * OHW);
+        pp[r].oh = rr / a.OW;
+        pp[r].ow = rr - pp[r].oh * a.OW;
+    }
+    auto advance = [&](PixPos& p) {  // + 32 pixels
+        p.ow += NKB;
+        while (p.ow >= a.OW) {
+            p.ow -= a.OW;
+            if (++p.oh == a.OH) { p.oh = 0; ++p.b; }
+        }
+    };
+
+    bf16x8 rx[2], rd[NA];
+    auto gather = [&](int ch) {
+        const int64_t kb = k_begin + (int64_t)ch * NKB + kk0;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const bool v = kb + 16 * r < k_end;
+            const PixPos& p = pp[r];
+            const int64_t xo = ((p.b * Hp + p.oh * s - pad + 1) * Wp + p.ow * s - pad + 1) * a.cin + xtoff;
+            rx[r] = (v && bval) ? ld16(xn + xo) : bf16x8{};
+        }
+        int64_t yo[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) yo[r] = ((pp[r].b * Hq + pp[r].oh + 1) * Wq + pp[r].ow + 1) * a.cout + dytoff;
+#pragma unroll
+        for (int r = 0; r < NA; ++r) {
+            const bool sel = WM == 2 ? r != 0 : arr != 0;  // (a select, not a dynamic index)
+            const bool v = kb + (sel ? 16 : 0) < k_end;
+            rd[r] = (v && aval) ? ld16(dyn + (sel ? yo[1] : yo[0])) : bf16x8{};
+        }
+        advance(pp[0]);
+        advance(pp[1]);
+    };
+    auto stash = [&](int buf) {
+#pragma unroll
+        for (int r = 0; r < 2; ++r) *reinterpret_cast<bf16x8*>(&Bs[buf][kk0 + 16 * r][8 * g]) = rx[r];
+#pragma unroll
+        for (int r = 0; r < NA; ++r) {
+            const int rr = WM == 2 ? r : arr;
+            *reinterpret_cast<bf16x8*>(&As[buf][kk0 + 16 * rr][8 * ag]) = rd[r];
+        }
+    };
+
+    // transposed-read lane roles: group grp = lane >> 4 -> k-block hh, column half cc; within the
+    // group lane 4q + p addresses k-row q, columns 4p .. 4p + 3
+    const int grp = lane >> 4, hh = grp >> 1, cc = grp & 1, q4 = (lane & 15) >> 2, p4 = lane & 3;
+    auto tr_operand = [&](const __bf16* tile, int stride, int col, int krow) {
+        typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+        const __bf16* p0 = tile + (krow + q4) * stride + col + 4 * p4;
+        const __bf16* p1 = p0 + 4 * stride;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p1));
+        const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        return __builtin_bit_cast(bf16x8, v);
+    };
+
+    f32x16 acc[WM][WN];
+#pragma unroll
+    for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < WN; ++ni) acc[mi][ni] = f32x16{0.f};
+
+    if (nch > 0) {
+        gather(0);
+        stash(0);
+    }
+    __syncthreads();
+    for (int ch = 0; ch < nch; ++ch) {
+        const int buf = ch & 1;
+        if (ch + 1 < nch) gather(ch + 1);
+#pragma unroll
+        for (int ks = 0; ks < NKB / 16; ++ks) {
+            bf16x8 av8[WM], bv8[WN];
+#pragma unroll
+            for (int mi = 0; mi < WM; ++mi)
+                av8[mi] = tr_operand(&As[buf][0][0], AS, wr * 32 * WM + mi * 32 + 16 * cc, 16 * ks + 8 * hh);
+#pragma unroll
+            for (int ni = 0; ni < WN; ++ni)
+                bv8[ni] = tr_operand(&Bs[buf][0][0], BS, wc * 32 * WN + ni * 32 + 16 * cc, 16 * ks + 8 * hh);
+#pragma unroll
+            for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < WN; ++ni) acc[mi][ni] = mfma_bf16(av8[mi], bv8[ni], acc[mi][ni]);
+        }
+        if (ch + 1 < nch) stash(buf ^ 1);
+        __syncthreads();
+    }
+
+    // ---- epilogue: slice partial in the reference layout [cout][cin][KH][KW]
+#pragma unroll
+    for (int ni = 0; ni < WN; ++ni) {
+        const int64_t col = n0 + wc * 32 * WN + ni * 32 + l32;
+        if (col >= N) continue;
+        const int tap = (int)(col / a.cin), c = (int)(col - (int64_t)tap * a.cin);
+        const int64_t obase = (int64_t)slice * M * N + (int64_t)c * KK + tap;
+#pragma unroll
+        for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int64_t row = m0 + wr * 32 * WM + mi * 32 + acc_row(r, h);
+                if (row < M) a.out[obase + row * N] = acc[mi][ni][r];
+            }
+    }
+}
+
+}  // namespace
+
+size_t nhwc_bytes(int B, int C, int H, int W) { return (size_t)B * (H + 2) * (W + 2) * C * 2; }
+
+int launch_to_nhwc(NhwcArgs a, hipStream_t s) {
+    PCX_CHECK_ARG(a.C % 8 == 0 && a.B > 0 && a.H > 0 && a.W > 0, "to_nhwc: C %d must be a multiple of 8", a.C);
+    PCX_CHECK_ARG(a.op == NHWC_COPY || a.op == NHWC_BNBWD || a.op == NHWC_ACT, "to_nhwc: op %d", a.op);
+    PCX_CHECK_ARG(a.op != NHWC_BNBWD || (a.y && a.cf), "to_nhwc: BN backward needs y and cf");
+    PCX_CHECK_ARG(a.op != NHWC_ACT || a.cf, "to_nhwc: activation needs cf");
+    const size_t sm = (size_t)64 * (a.W + 1) * 4;
+    PCX_CHECK_ARG(sm <= 64 * 1024, "to_nhwc: row of %d pixels too long", a.W);
+    dim3 grid((unsigned)a.B, (unsigned)ceil_div(a.C, 64));
+    const int v = a.W % 4 == 0 ? 4 : a.W % 2 == 0 ? 2 : 1;
+#define PCX_TN(V_, OP_) \
+    if (v == V_ && a.op == OP_) to_nhwc_kernel<V_, OP_><<<grid, 256, sm, s>>>(a);
+    PCX_TN(4, NHWC_COPY) PCX_TN(2, NHWC_COPY) PCX_TN(1, NHWC_COPY)
+    PCX_TN(4, NHWC_BNBWD) PCX_TN(2, NHWC_BNBWD) PCX_TN(1, NHWC_BNBWD)
+    PCX_TN(4, NHWC_ACT) PCX_TN(2, NHWC_ACT) PCX_TN(1, NHWC_ACT)
+#undef PCX_TN
+    PCX_LAUNCH_CHECK("to_nhwc_kernel");
+    return PCX_OK;
+}
+
+bool convn_fits(const ConvGArgs& a) {
+    if (a.KH != a.KW || (a.KH != 1 && a.KH != 3) || a.pad > 1 || a.pad < 0) return false;
+    if (a.mode == 2) return a.cin % 8 == 0 && a.cout % 8 == 0;
+    return (a.mode == 0 ? a.cin : a.cout) % NKB == 0;
+}
+
+// called by launch_convg_bf16 once the weights are packed (modes 0 / 1 / 3)
+int launch_convn(const ConvGArgs& a, hipStream_t s) {
+    PCX_CHECK_ARG(convn_fits(a), "convn: shape unsupported (k %d, pad %d, channels %d / %d)", a.KH, a.pad, a.cin, a.cout);
+    const int64_t IHW = (int64_t)a.IH * a.IW, OHW = (int64_t)a.OH * a.OW;
+    if (a.mode == 2) {
+        PCX_CHECK_ARG(a.xn && a.dyn && a.kslice % NKB == 0 && a.nslice >= 1, "convn: bad weight-gradient arguments");
+        const int64_t M = a.cout, N = (int64_t)a.cin * a.KH * a.KW;
+        const int wm = M >= 128 ? 2 : 1;
+        const int64_t nblocks = ceil_div(M, 64 * wm) * ceil_div(N, 128) * a.nslice;
+        PCX_CHECK_ARG(nblocks < ((int64_t)1 << 31), "convn: grid too large");
+        if (wm == 2) convn_wgrad_kernel<2><<<(unsigned)nblocks, 256, 0, s>>>(a);
+        else convn_wgrad_kernel<1><<<(unsigned)nblocks, 256, 0, s>>>(a);
+        PCX_LAUNCH_CHECK("convn_wgrad_kernel");
+        return PCX_OK;
+    }
+    PCX_CHECK_ARG(a.mode == 0 ? a.xn != nullptr : a.dyn != nullptr, "convn: missing channel-last operand");
+    PCX_CHECK_ARG(a.wpack != nullptr, "convn: packed weights required");
+    int64_t M, N;
+    if (a.mode == 0) { M = a.cout; N = a.B * OHW; }
+    else if (a.mode == 1) { M = a.cin; N = a.B * IHW; }
+    else {
+        M = a.cin;
+        N = a.B * (int64_t)((a.IH - (a.par >> 1) + 1) / 2) * ((a.IW - (a.par & 1) + 1) / 2);
+    }
+    if (N == 0) return PCX_OK;
+    if (a.mode == 3 && a.accumulate) {  // a parity class without taps (1x1 stride 2) adds nothing
+        const int kh0 = ((a.par >> 1) + a.pad) & 1, kw0 = ((a.par & 1) + a.pad) & 1;
+        if ((a.KH - kh0 + 1) / 2 == 0 || (a.KW - kw0 + 1) / 2 == 0) return PCX_OK;
+    }
+    const int wm = M >= 128 ? 2 : 1;
+    const int64_t nblocks = ceil_div(M, 64 * wm) * ceil_div(N, 128);
+    PCX_CHECK_ARG(nblocks < ((int64_t)1 << 31), "convn: grid too large");
+    dim3 grid((unsigned)nblocks);
+#define PCX_CN(MODE_, WM_)                                                                     \
+    if (a.mode == MODE_ && wm == WM_) {                                                        \
+        convn_kernel<MODE_, WM_><<<grid, 256, 0, s>>>(a);                                      \
+        PCX_LAUNCH_CHECK("convn_kernel");                                                      \
+        return PCX_OK;                                                                         \
+    }
+    PCX_CN(0, 1) PCX_CN(0, 2) PCX_CN(1, 1) PCX_CN(1, 2) PCX_CN(3, 1) PCX_CN(3, 2)
+#undef PCX_CN
+    set_error("convn: mode %d unsupported", a.mode);
+    return PCX_EINVAL;
+}
+
+}  // namespace pcx

@@ -27,6 +27,10 @@ struct DeepBlock {
     bool dma1, dma2, w32_1, w32_2;
     WgradArgs wg1, wg2;
     int nblk1, nblk2;
+    // precision "bf16" with channel counts the channel-last engine takes (convn.hip): padded NHWC
+    // bf16 images of the block input (conv1, shortcut) and of d1 (conv2), kept for the backward
+    bool cn;
+    size_t an, d1n;
 };
 
 struct DeepPlan {
@@ -42,6 +46,7 @@ struct DeepPlan {
     int cmax;
     DeepBlock blk[4];
     size_t g, dyA, dyB, dd, hdz;   // backward scratch
+    size_t dyn1, dyn2;             // channel-last bf16 dy images (conv1 / conv2, shortcut)
     size_t stat, wgp, ident;
     int ia, ip;                    // attention / projection parameter indices
     int bn_proj;
@@ -50,6 +55,15 @@ struct DeepPlan {
 namespace {
 
 int64_t planes(int B, int C, int H, int W) { return (int64_t)B * C * H * W; }
+
+NhwcArgs nhwc_args(int op, int B, int C, int H, int W, const float* src, void* dst) {
+    NhwcArgs a{};
+    a.op = op;
+    a.B = B; a.C = C; a.H = H; a.W = W;
+    a.src = src;
+    a.dst = dst;
+    return a;
+}
 
 }  // namespace
 
@@ -74,7 +88,7 @@ int build_deep(Plan& p) {
     d.cf0 = p.carve("cf0", C0 * 16);
     d.cfb0 = p.carve("cfb0", C0 * 16);
     int pidx = 4, bnidx = 1, cin = C0, H = d.H1, W = d.W1;
-    size_t gmax = 0, stat = 0, wg = 0;
+    size_t gmax = 0, stat = 0, wg = 0, dynmax = 0;
     auto wg_need = [&](int ci, int co, int k, int oh, int ow) {
         ConvGArgs a{};
         a.B = B; a.cin = ci; a.cout = co; a.KH = a.KW = k; a.OH = oh; a.OW = ow;
@@ -137,6 +151,13 @@ int build_deep(Plan& p) {
         wg_need(k.cin, k.cout, 3, k.Ho, k.Wo);
         wg_need(k.cout, k.cout, 3, k.Ho, k.Wo);
         if (k.sc) wg_need(k.cin, k.cout, 1, k.Ho, k.Wo);
+        k.cn = d.bf16 && k.cin % 32 == 0 && k.cout % 32 == 0;
+        k.an = k.d1n = 0;
+        if (k.cn) {
+            k.an = p.carve("nhwc_a", nhwc_bytes(B, k.cin, k.Hi, k.Wi));
+            k.d1n = p.carve("nhwc_d1", nhwc_bytes(B, k.cout, k.Ho, k.Wo));
+            dynmax = std::max(dynmax, nhwc_bytes(B, k.cout, k.Ho, k.Wo));
+        }
         k.dma1 = k.w32_1 = false;
         k.nblk1 = 0;
         if (k.stride == 1) plan_routed(k.cin, k.cout, k.Ho, k.Wo, &k.dma1, &k.w32_1, &k.wg1, &k.nblk1);
@@ -147,6 +168,8 @@ int build_deep(Plan& p) {
     d.dyA = p.carve("dyA", gmax);
     d.dyB = p.carve("dyB", gmax);
     d.dd = p.carve("dd", gmax);
+    d.dyn1 = dynmax ? p.carve("nhwc_dy1", dynmax) : 0;
+    d.dyn2 = dynmax ? p.carve("nhwc_dy2", dynmax) : 0;
     const int C4 = d.h[3];
     p.C6 = C4;
     p.P6 = H * W;
@@ -217,7 +240,8 @@ struct Ctx {
 // forward conv (raw output, no bias) + train-mode statistics + BN finalise -> cf
 int conv_bn_fwd(const Ctx& c, const char* label, int layer, const float* x, int cin, int IH, int IW, int k, int stride,
                 int pad, const float* wgt, float* y, int cout, int OH, int OW, const float* gamma, const float* beta,
-                const float* bias, float* rmean, float* rvar, int64_t* nbt, int train, float4* cf, int dma_nblk = 0) {
+                const float* bias, float* rmean, float* rvar, int64_t* nbt, int train, float4* cf, int dma_nblk = 0,
+                const void* xn = nullptr) {
     float* part = c.w<float>(c.d.stat);
     int ns = 1;
     BnFwdArgs f{};
@@ -249,6 +273,7 @@ int conv_bn_fwd(const Ctx& c, const char* label, int layer, const float* x, int 
         a.x = x; a.w = wgt; a.out = y;
         a.bf16 = c.d.bf16;
         a.wpack = c.w<void>(c.d.wpk16);
+        a.xn = xn;
         Scope sc(&c.p.prof, c.s, label, layer);
         RC(launch_convg(a, c.s));
     }
@@ -274,7 +299,8 @@ int conv_bn_fwd(const Ctx& c, const char* label, int layer, const float* x, int 
 // weight gradient of a conv into G (partials summed deterministically) + zero bias gradient
 int conv_wgrad(const Ctx& c, int layer, const float* x, int cin, int IH, int IW, int k, int stride, int pad,
                const float* dy, int cout, int OH, int OW, float* gw, float* gb, const WgradArgs* w32 = nullptr,
-               const float* bn_g = nullptr, const float* bn_y = nullptr, const float4* bn_cf = nullptr) {
+               const float* bn_g = nullptr, const float* bn_y = nullptr, const float4* bn_cf = nullptr,
+               const void* xn = nullptr, const void* dyn = nullptr) {
     if (w32) {  // stride-1 3x3: pixel-stream (wgrad_s.hip, MT 16) or 32x32 row-window (wgrad_w32.hip) kernel
         WgradArgs w = *w32;
         w.B = c.p.B; w.H = OH; w.W = OW; w.cin = cin; w.cout = cout;
@@ -311,6 +337,8 @@ int conv_wgrad(const Ctx& c, int layer, const float* x, int cin, int IH, int IW,
         a.bn_cf = bn_cf;
     }
     a.bf16 = c.d.bf16;
+    a.xn = xn;    // channel-last images (both set: convn.hip)
+    a.dyn = dyn;
     a.nslice = convg_nslice(a, &a.kslice);
     float* wgp = c.w<float>(c.d.wgp);
     a.out = wgp;
@@ -321,7 +349,8 @@ int conv_wgrad(const Ctx& c, int layer, const float* x, int cin, int IH, int IW,
 }
 
 int conv_dgrad(const Ctx& c, int layer, const float* dy, int cout, int OH, int OW, int k, int stride, int pad,
-               const float* wgt, float* dx, int cin, int IH, int IW, int accumulate, bool dma = false) {
+               const float* wgt, float* dx, int cin, int IH, int IW, int accumulate, bool dma = false,
+               const void* dyn = nullptr) {
     if (dma) {  // stride-1 3x3: the LDS-DMA conv on flipped weights, plain store / accumulate
         float* wp = c.w<float>(c.d.wpk);
         RC(launch_pack_dgrad(wgt, wp, cout, cin, c.s));
@@ -345,6 +374,7 @@ int conv_dgrad(const Ctx& c, int layer, const float* dy, int cout, int OH, int O
     a.w = wgt; a.dy = dy; a.out = dx; a.accumulate = accumulate;
     a.bf16 = c.d.bf16;
     a.wpack = c.w<void>(c.d.wpk16);
+    a.dyn = dyn;
     Scope sc(&c.p.prof, c.s, "conv_dgrad", layer);
     return launch_convg(a, c.s);
 }
@@ -404,24 +434,37 @@ int deep_forward(const Plan& p, const float* const* P, float* const* bnstat, int
     for (int i = 0; i < 4; ++i) {
         const DeepBlock& k = d.blk[i];
         const int q = k.pidx, L = 2 * i + 1;
+        const void* an = k.cn ? c.w<void>(k.an) : nullptr;
+        const void* d1n = k.cn ? c.w<void>(k.d1n) : nullptr;
+        if (k.cn && (i == 0 || !d.blk[i - 1].cn)) {  // (otherwise written by the previous block's activation)
+            Scope sc(&p.prof, s, "to_nhwc");
+            RC(launch_to_nhwc(nhwc_args(NHWC_COPY, B, k.cin, k.Hi, k.Wi, a, c.w<void>(k.an)), s));
+        }
         RC(conv_bn_fwd(c, "conv_fwd", L, a, k.cin, k.Hi, k.Wi, 3, k.stride, 1, P[q], c.w<float>(k.y1), k.cout, k.Ho,
                        k.Wo, P[q + 2], P[q + 3], P[q + 1], bnp(k.bnidx, 0), bnp(k.bnidx, 1), nb(k.bnidx), train,
-                       c.w<float4>(k.cf1), k.dma1 ? k.nblk1 : 0));
+                       c.w<float4>(k.cf1), k.dma1 ? k.nblk1 : 0, an));
         const int64_t P2 = (int64_t)k.Ho * k.Wo;
         {
             Scope sc(&p.prof, s, "bn_act");
-            RC(launch_bn_act(c.w<float>(k.y1), c.w<float4>(k.cf1), nullptr, nullptr,
-                             d.residual ? dmask[i] : nullptr, c.w<float>(k.d1), B, k.cout, P2, s));
+            if (k.cn) {  // d1 feeds only conv2 (forward and weight gradient): its channel-last image alone
+                NhwcArgs t = nhwc_args(NHWC_ACT, B, k.cout, k.Ho, k.Wo, c.w<float>(k.y1), c.w<void>(k.d1n));
+                t.cf = c.w<float4>(k.cf1);
+                t.drop = d.residual ? dmask[i] : nullptr;
+                RC(launch_to_nhwc(t, s));
+            } else {
+                RC(launch_bn_act(c.w<float>(k.y1), c.w<float4>(k.cf1), nullptr, nullptr,
+                                 d.residual ? dmask[i] : nullptr, c.w<float>(k.d1), B, k.cout, P2, s));
+            }
         }
         RC(conv_bn_fwd(c, "conv_fwd", L + 1, c.w<float>(k.d1), k.cout, k.Ho, k.Wo, 3, 1, 1, P[q + 4], c.w<float>(k.y2),
                        k.cout, k.Ho, k.Wo, P[q + 6], P[q + 7], P[q + 5], bnp(k.bnidx + 1, 0), bnp(k.bnidx + 1, 1),
-                       nb(k.bnidx + 1), train, c.w<float4>(k.cf2), k.dma2 ? k.nblk2 : 0));
+                       nb(k.bnidx + 1), train, c.w<float4>(k.cf2), k.dma2 ? k.nblk2 : 0, d1n));
         const float* res = nullptr;
         const float4* rcf = nullptr;
         if (k.sc) {
             RC(conv_bn_fwd(c, "shortcut_fwd", i, a, k.cin, k.Hi, k.Wi, 1, k.stride, 0, P[q + 8], c.w<float>(k.ysc),
                            k.cout, k.Ho, k.Wo, P[q + 10], P[q + 11], P[q + 9], bnp(k.bnidx + 2, 0),
-                           bnp(k.bnidx + 2, 1), nb(k.bnidx + 2), train, c.w<float4>(k.cfsc)));
+                           bnp(k.bnidx + 2, 1), nb(k.bnidx + 2), train, c.w<float4>(k.cfsc), 0, an));
             res = c.w<float>(k.ysc);
             rcf = c.w<float4>(k.cfsc);
         } else if (d.residual) {
@@ -429,8 +472,18 @@ int deep_forward(const Plan& p, const float* const* P, float* const* bnstat, int
         }
         {
             Scope sc(&p.prof, s, "bn_act");
-            RC(launch_bn_act(c.w<float>(k.y2), c.w<float4>(k.cf2), res, rcf, d.residual ? nullptr : dmask[i],
-                             c.w<float>(k.out), B, k.cout, P2, s));
+            if (i < 3 && d.blk[i + 1].cn) {  // the block output and the next block's channel-last input
+                NhwcArgs t = nhwc_args(NHWC_ACT, B, k.cout, k.Ho, k.Wo, c.w<float>(k.y2), c.w<void>(d.blk[i + 1].an));
+                t.cf = c.w<float4>(k.cf2);
+                t.res = res;
+                t.rcf = rcf;
+                t.drop = d.residual ? nullptr : dmask[i];
+                t.out32 = c.w<float>(k.out);
+                RC(launch_to_nhwc(t, s));
+            } else {
+                RC(launch_bn_act(c.w<float>(k.y2), c.w<float4>(k.cf2), res, rcf, d.residual ? nullptr : dmask[i],
+                                 c.w<float>(k.out), B, k.cout, P2, s));
+            }
         }
         a = c.w<float>(k.out);
     }
@@ -578,7 +631,24 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
                 RC(bn_bwd(c, k.cout, ns, b.p_g, b.p_x2, P[q + 10], c.w<float4>(k.cfsc), G[q + 10], G[q + 11],
                           c.w<float4>(k.cfbsc), count));
         }
-        {
+        // channel-last bf16 dy images: the BN backward applied while converting (no float32 dy)
+        const void* an = k.cn ? c.w<void>(k.an) : nullptr;
+        const void* d1n = k.cn ? c.w<void>(k.d1n) : nullptr;
+        void* dyn1 = k.cn ? c.w<void>(d.dyn1) : nullptr;
+        void* dyn2 = k.cn ? c.w<void>(d.dyn2) : nullptr;
+        if (k.cn) {
+            Scope sc(&p.prof, s, "dy_nhwc");
+            NhwcArgs t = nhwc_args(NHWC_BNBWD, B, k.cout, k.Ho, k.Wo, g, dyn1);
+            t.y = c.w<float>(k.y2);
+            t.cf = c.w<float4>(k.cfb2);
+            RC(launch_to_nhwc(t, s));
+            if (k.sc) {
+                t.y = c.w<float>(k.ysc);
+                t.cf = c.w<float4>(k.cfbsc);
+                t.dst = dyn2;
+                RC(launch_to_nhwc(t, s));
+            }
+        } else {
             Scope sc(&p.prof, s, "bn_bwd_apply");
             // (a routed conv2's dy is produced by its weight-gradient kernel's staging)
             if (!k.w32_2) RC(launch_bn_bwd_apply(g, c.w<float>(k.y2), c.w<float4>(k.cfb2), dy2, B, k.cout, P2, s));
@@ -586,9 +656,9 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
         }
         // ---- conv2
         RC(conv_wgrad(c, L + 1, c.w<float>(k.d1), k.cout, k.Ho, k.Wo, 3, 1, 1, dy2, k.cout, k.Ho, k.Wo, G[q + 4],
-                      G[q + 5], k.w32_2 ? &k.wg2 : nullptr, g, c.w<float>(k.y2), c.w<float4>(k.cfb2)));
+                      G[q + 5], k.w32_2 ? &k.wg2 : nullptr, g, c.w<float>(k.y2), c.w<float4>(k.cfb2), d1n, dyn1));
         float* dd = c.w<float>(d.dd);
-        RC(conv_dgrad(c, L + 1, dy2, k.cout, k.Ho, k.Wo, 3, 1, 1, P[q + 4], dd, k.cout, k.Ho, k.Wo, 0, k.dma2));
+        RC(conv_dgrad(c, L + 1, dy2, k.cout, k.Ho, k.Wo, 3, 1, 1, P[q + 4], dd, k.cout, k.Ho, k.Wo, 0, k.dma2, dyn1));
         // ---- through Dropout2d / ReLU / BN1
         {
             BwdPrepArgs b{};
@@ -609,14 +679,20 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
             RC(bn_bwd(c, k.cout, ns, b.p_g, b.p_x1, P[q + 2], c.w<float4>(k.cf1), G[q + 2], G[q + 3],
                       c.w<float4>(k.cfb1), count));
         }
-        float* dy1 = dy2;  // dy2 is dead after conv2's gradients
-        {
+        float* dy1 = dy2;  // dy2 (and its image) are dead after conv2's gradients
+        if (k.cn) {
+            Scope sc(&p.prof, s, "dy_nhwc");
+            NhwcArgs t = nhwc_args(NHWC_BNBWD, B, k.cout, k.Ho, k.Wo, dd, dyn1);
+            t.y = c.w<float>(k.y1);
+            t.cf = c.w<float4>(k.cfb1);
+            RC(launch_to_nhwc(t, s));
+        } else {
             Scope sc(&p.prof, s, "bn_bwd_apply");
             if (!k.w32_1) RC(launch_bn_bwd_apply(dd, c.w<float>(k.y1), c.w<float4>(k.cfb1), dy1, B, k.cout, P2, s));
         }
         // ---- conv1 (+ shortcut): gradients of the weights and of the block input
         RC(conv_wgrad(c, L, a_in, k.cin, k.Hi, k.Wi, 3, k.stride, 1, dy1, k.cout, k.Ho, k.Wo, G[q], G[q + 1],
-                      k.w32_1 ? &k.wg1 : nullptr, dd, c.w<float>(k.y1), c.w<float4>(k.cfb1)));
+                      k.w32_1 ? &k.wg1 : nullptr, dd, c.w<float>(k.y1), c.w<float4>(k.cfb1), an, dyn1));
         float* da = c.w<float>(k.da);
         int acc = 0;
         if (d.residual && !k.sc) {  // identity shortcut: the block input receives g directly
@@ -624,11 +700,12 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
                              "copy shortcut grad"));
             acc = 1;
         }
-        RC(conv_dgrad(c, L, dy1, k.cout, k.Ho, k.Wo, 3, k.stride, 1, P[q], da, k.cin, k.Hi, k.Wi, acc, k.dma1));
+        RC(conv_dgrad(c, L, dy1, k.cout, k.Ho, k.Wo, 3, k.stride, 1, P[q], da, k.cin, k.Hi, k.Wi, acc, k.dma1, dyn1));
         if (k.sc) {
             RC(conv_wgrad(c, 100 + i, a_in, k.cin, k.Hi, k.Wi, 1, k.stride, 0, dysc, k.cout, k.Ho, k.Wo, G[q + 8],
-                          G[q + 9]));
-            RC(conv_dgrad(c, 100 + i, dysc, k.cout, k.Ho, k.Wo, 1, k.stride, 0, P[q + 8], da, k.cin, k.Hi, k.Wi, 1));
+                          G[q + 9], nullptr, nullptr, nullptr, nullptr, an, dyn2));
+            RC(conv_dgrad(c, 100 + i, dysc, k.cout, k.Ho, k.Wo, 1, k.stride, 0, P[q + 8], da, k.cin, k.Hi, k.Wi, 1,
+                          false, dyn2));
         }
         dout = da;
         masked = false;

@@ -257,7 +257,34 @@ struct ConvGArgs {
     const float* bn_g;
     const float* bn_y;
     const float4* bn_cf;
+    // bf16 only: zero-padded channel-last bf16 images [B][H + 2][W + 2][C] of x (modes 0, 2) and dy
+    // (modes 1, 2) written by launch_to_nhwc; when set, the channel-last engine (convn.hip) runs
+    const void* xn;
+    const void* dyn;
 };
+// NCHW float32 -> zero-padded NHWC bf16 (convn.hip), optionally through the BN backward or the
+// BN + residual + ReLU + dropout activation on the way
+enum NhwcOp {
+    NHWC_COPY = 0,   // src
+    NHWC_BNBWD = 1,  // a (src - mb - (y - mean) mgi), cf = {a, mb, mgi, mean}
+    NHWC_ACT = 2,    // drop[b,c] relu(src s + t + res'), res' = res rs + rt (rcf) | res | 0; cf = {s, t}
+};
+struct NhwcArgs {
+    int op;
+    int B, C, H, W;
+    const float* src;
+    const float* y;        // NHWC_BNBWD
+    const float4* cf;
+    const float* res;      // NHWC_ACT (optional)
+    const float4* rcf;
+    const float* drop;     // [B][C] or NULL
+    float* out32;          // NHWC_ACT: optional float32 NCHW copy of the result
+    void* dst;             // [B][H + 2][W + 2][C] bf16
+};
+size_t nhwc_bytes(int B, int C, int H, int W);
+int launch_to_nhwc(NhwcArgs a, hipStream_t s);
+bool convn_fits(const ConvGArgs& a);
+int launch_convn(const ConvGArgs& a, hipStream_t s);
 size_t convg_bf16_wpack_bytes(int mode, int cin, int cout, int k);
 size_t convg_wpack_bytes(int mode, int cin, int cout, int k);  // fp32 packed weights (wpack)
 int launch_convg(ConvGArgs a, hipStream_t s);

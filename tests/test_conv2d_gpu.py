@@ -20,6 +20,11 @@ SHAPES = [  # B, cin, cout, IH, IW, k, stride, pad
     (2, 64, 128, 10, 25, 3, 2, 1),
     (2, 16, 32, 10, 25, 1, 2, 0),   # 1x1 stride-2 shortcut
     (2, 48, 40, 7, 9, 3, 1, 1),
+    # channel-last bf16 engine (convn.hip) at block shapes: 64-row and 128-row tiles, ragged tails
+    (3, 64, 64, 20, 100, 3, 1, 1),
+    (2, 128, 256, 10, 50, 3, 2, 1),
+    (2, 256, 256, 5, 25, 3, 1, 1),
+    (2, 256, 512, 5, 25, 1, 2, 0),
 ]
 
 
