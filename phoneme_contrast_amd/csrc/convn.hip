@@ -128,10 +128,10 @@ __global__ __launch_bounds__(256) void to_nhwc_kernel(NhwcArgs a) {
 }
 
 // ------------------------------------------------------------------ forward / data gradient
-template <int MODE, int WM>
+template <int MODE, int WM, int WN>
 __global__ __launch_bounds__(256) void convn_kernel(ConvGArgs a) {
-    constexpr int WN = 2;
     constexpr int BM = 64 * WM, BN = 64 * WN;
+    constexpr int TPP = 256 / BN, NBL = 4 / TPP;  // staging threads per pixel, 16-byte loads per thread
     __shared__ __attribute__((aligned(16))) __bf16 As[2][BM][NRS];
     __shared__ __attribute__((aligned(16))) __bf16 Bs[2][BN][NRS];
 
@@ -158,8 +158,8 @@ __global__ __launch_bounds__(256) void convn_kernel(ConvGArgs a) {
     const int64_t tm = blockIdx.x % mt, tn = blockIdx.x / mt;
     const int64_t m0 = tm * BM, n0 = tn * BN;
 
-    // B staging: pixel bp of the tile, channels 16 bh .. 16 bh + 15 of every chunk
-    const int bp = tid >> 1, bh = tid & 1;
+    // B staging: pixel bp of the tile, channels 8 NBL bh .. of every chunk
+    const int bp = tid / TPP, bh = tid % TPP;
     int64_t nn = n0 + bp;
     if (nn >= N) nn = N - 1;  // tail pixels load a valid row; their columns are never stored
     int64_t pb;               // image element of the pixel's operand row at tap 0
@@ -177,7 +177,7 @@ __global__ __launch_bounds__(256) void convn_kernel(ConvGArgs a) {
         const int oh0 = (2 * ihc + ph + pad - kh0) >> 1, ow0 = (2 * iwc + pw + pad - kw0) >> 1;
         pb = ((b * Hp + oh0 + 1) * Wp + ow0 + 1) * CK;
     }
-    const __bf16* xb = static_cast<const __bf16*>(MODE == 0 ? a.xn : a.dyn) + pb + 16 * bh;
+    const __bf16* xb = static_cast<const __bf16*>(MODE == 0 ? a.xn : a.dyn) + pb + 8 * NBL * bh;
     // A staging: packed weight rows am, am + 64, k 8 aq .. 8 aq + 7 of every chunk
     const int am = tid >> 2, aq = tid & 3;
     const __bf16* ap[WM];
@@ -189,21 +189,26 @@ __global__ __launch_bounds__(256) void convn_kernel(ConvGArgs a) {
         ap[j] = static_cast<const __bf16*>(a.wpack) + (av[j] ? row : 0) * K + 8 * aq;
     }
 
-    bf16x8 ra[WM], rb[2];
-    auto gather = [&](int ch) {
+    // one register stage, stashed at the top of the next iteration: a chunk's loads have a whole
+    // iteration (MFMAs + barrier) to land before anything waits on them
+    struct Stage {
+        bf16x8 a[WM], b[NBL];
+    };
+    Stage st;
+    auto gather = [&](int ch, Stage& r) {
         const int tap = ch / cpt, c0 = (ch - tap * cpt) * NKB;
         const int th = tap / ntw, tw = tap - th * ntw;
         const int toff = (MODE == 0 ? 1 : -1) * (th * Wp + tw) * CK + c0;
-        rb[0] = ld16(xb + toff);
-        rb[1] = ld16(xb + toff + 8);
 #pragma unroll
-        for (int j = 0; j < WM; ++j) ra[j] = av[j] ? ld16(ap[j] + (int64_t)ch * NKB) : bf16x8{};
+        for (int j = 0; j < NBL; ++j) r.b[j] = ld16(xb + toff + 8 * j);
+#pragma unroll
+        for (int j = 0; j < WM; ++j) r.a[j] = av[j] ? ld16(ap[j] + (int64_t)ch * NKB) : bf16x8{};
     };
-    auto stash = [&](int buf) {
+    auto stash = [&](int buf, const Stage& r) {
 #pragma unroll
-        for (int j = 0; j < WM; ++j) *reinterpret_cast<bf16x8*>(&As[buf][am + 64 * j][8 * aq]) = ra[j];
-        *reinterpret_cast<bf16x8*>(&Bs[buf][bp][16 * bh]) = rb[0];
-        *reinterpret_cast<bf16x8*>(&Bs[buf][bp][16 * bh + 8]) = rb[1];
+        for (int j = 0; j < WM; ++j) *reinterpret_cast<bf16x8*>(&As[buf][am + 64 * j][8 * aq]) = r.a[j];
+#pragma unroll
+        for (int j = 0; j < NBL; ++j) *reinterpret_cast<bf16x8*>(&Bs[buf][bp][8 * NBL * bh + 8 * j]) = r.b[j];
     };
 
     f32x16 acc[WM][WN];
@@ -213,13 +218,15 @@ __global__ __launch_bounds__(256) void convn_kernel(ConvGArgs a) {
         for (int ni = 0; ni < WN; ++ni) acc[mi][ni] = f32x16{0.f};
 
     if (nch > 0) {
-        gather(0);
-        stash(0);
+        gather(0, st);
+        stash(0, st);
+        if (nch > 1) gather(1, st);
     }
     __syncthreads();
     for (int ch = 0; ch < nch; ++ch) {
         const int buf = ch & 1;
-        if (ch + 1 < nch) gather(ch + 1);
+        if (ch + 1 < nch) stash(buf ^ 1, st);  // (buf ^ 1 was last read before the previous barrier)
+        if (ch + 2 < nch) gather(ch + 2, st);
 #pragma unroll
         for (int ks = 0; ks < NKB / 16; ++ks) {
             bf16x8 av8[WM], bv8[WN];
@@ -234,7 +241,6 @@ __global__ __launch_bounds__(256) void convn_kernel(ConvGArgs a) {
 #pragma unroll
                 for (int ni = 0; ni < WN; ++ni) acc[mi][ni] = mfma_bf16(av8[mi], bv8[ni], acc[mi][ni]);
         }
-        if (ch + 1 < nch) stash(buf ^ 1);
         __syncthreads();
     }
 
@@ -394,11 +400,13 @@ __global__ __launch_bounds__(256) void convn_wgrad_kernel(ConvGArgs a) {
     if (nch > 0) {
         gather(0);
         stash(0);
+        if (nch > 1) gather(1);
     }
     __syncthreads();
-    for (int ch = 0; ch < nch; ++ch) {
+    for (int ch = 0; ch < nch; ++ch) {  // (stash at the top, as convn_kernel)
         const int buf = ch & 1;
-        if (ch + 1 < nch) gather(ch + 1);
+        if (ch + 1 < nch) stash(buf ^ 1);
+        if (ch + 2 < nch) gather(ch + 2);
 #pragma unroll
         for (int ks = 0; ks < NKB / 16; ++ks) {
             bf16x8 av8[WM], bv8[WN];
@@ -413,7 +421,6 @@ __global__ __launch_bounds__(256) void convn_wgrad_kernel(ConvGArgs a) {
 #pragma unroll
                 for (int ni = 0; ni < WN; ++ni) acc[mi][ni] = mfma_bf16(av8[mi], bv8[ni], acc[mi][ni]);
         }
-        if (ch + 1 < nch) stash(buf ^ 1);
         __syncthreads();
     }
 
@@ -493,16 +500,17 @@ int launch_convn(const ConvGArgs& a, hipStream_t s) {
         if ((a.KH - kh0 + 1) / 2 == 0 || (a.KW - kw0 + 1) / 2 == 0) return PCX_OK;
     }
     const int wm = M >= 128 ? 2 : 1;
-    const int64_t nblocks = ceil_div(M, 64 * wm) * ceil_div(N, 128);
+    constexpr int wn = 2;  // (128 x 256 tiles measured slower: 2 blocks per CU instead of 4)
+    const int64_t nblocks = ceil_div(M, 64 * wm) * ceil_div(N, 64 * wn);
     PCX_CHECK_ARG(nblocks < ((int64_t)1 << 31), "convn: grid too large");
     dim3 grid((unsigned)nblocks);
-#define PCX_CN(MODE_, WM_)                                                                     \
-    if (a.mode == MODE_ && wm == WM_) {                                                        \
-        convn_kernel<MODE_, WM_><<<grid, 256, 0, s>>>(a);                                      \
+#define PCX_CN(MODE_, WM_, WN_)                                                                \
+    if (a.mode == MODE_ && wm == WM_ && wn == WN_) {                                           \
+        convn_kernel<MODE_, WM_, WN_><<<grid, 256, 0, s>>>(a);                                 \
         PCX_LAUNCH_CHECK("convn_kernel");                                                      \
         return PCX_OK;                                                                         \
     }
-    PCX_CN(0, 1) PCX_CN(0, 2) PCX_CN(1, 1) PCX_CN(1, 2) PCX_CN(3, 1) PCX_CN(3, 2)
+    PCX_CN(0, 1, 2) PCX_CN(0, 2, 2) PCX_CN(1, 1, 2) PCX_CN(1, 2, 2) PCX_CN(3, 1, 2) PCX_CN(3, 2, 2)
 #undef PCX_CN
     set_error("convn: mode %d unsupported", a.mode);
     return PCX_EINVAL;
