@@ -429,6 +429,8 @@ int launch_convg_bf16(ConvGArgs a, hipStream_t s) {
     if (a.mode == 2) PCX_CHECK_ARG(a.kslice % KB == 0 && a.nslice >= 1, "convg_bf16: bad weight-gradient split");
     // (mode 2 reuses the flag: false = dy computed as the BN backward of (bn_g, bn_y) while staging)
     const bool fk = a.mode == 2 ? a.bn_g == nullptr : (a.mode == 0 ? a.cin : a.cout) % KB == 0;
+    // channel-last operands supplied: the convn.hip engine (packs its own weight rows)
+    if (a.mode == 2 ? (a.xn && a.dyn) : a.mode == 0 ? a.xn != nullptr : a.dyn != nullptr) return launch_convn(a, s);
     if (a.mode != 2 && a.wpack) {
         const int64_t KK = (int64_t)a.KH * a.KW;
         int64_t K = a.mode == 0 ? a.cin * KK : a.cout * KK;
@@ -443,8 +445,6 @@ int launch_convg_bf16(ConvGArgs a, hipStream_t s) {
                                                                            Kp, K);
         PCX_LAUNCH_CHECK("pack_wbf16_kernel");
     }
-    // channel-last operands supplied: the convn.hip engine (same packed weights, same rounding)
-    if (a.mode == 2 ? (a.xn && a.dyn) : a.mode == 0 ? a.xn != nullptr : a.dyn != nullptr) return launch_convn(a, s);
     dim3 grid((unsigned)nblocks);
 #define PCX_CB(MODE_, KH_, WM_)                                                                 \
     if (a.mode == MODE_ && a.KH == KH_ && wm == WM_) {                                          \

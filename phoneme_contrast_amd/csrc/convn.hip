@@ -28,7 +28,6 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int NKB = 32;  // k per chunk
-constexpr int NRS = 40;  // LDS row stride (bf16) of k-contiguous tiles: 80 B, conflict-free ds_read_b128
 
 __device__ __forceinline__ bf16x8 ld16(const __bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
@@ -128,15 +127,33 @@ __global__ __launch_bounds__(256) void to_nhwc_kernel(NhwcArgs a) {
 }
 
 // ------------------------------------------------------------------ forward / data gradient
-template <int MODE, int WM, int WN>
+// Operand tiles are copied HBM/L2 -> LDS by global_load_lds_dwordx4 (no VGPR staging, no LDS store
+// instructions), double-buffered: the copy of chunk k + 1 runs under the MFMAs of chunk k.  A DMA
+// wave-instruction fills 1 KB of LDS contiguously (lane L -> byte 16 L), i.e. 16 rows of 64 bytes
+// (32 bf16 of k); each lane picks the global 16-byte run that belongs in its slot, which lets the
+// rows be XOR-swizzled instead of padded: logical run q of row r sits in slot q ^ ((r >> 2) & 3),
+// so the MFMA operand reads (ds_read_b128, rows l32, run 2 ks + h) are conflict-free.
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ void dma16(const __bf16* g, unsigned lds_byte_addr) {
+    // inline asm: the builtin would make the waitcnt pass wait for every DMA before each ds_read
+    const unsigned m0 = __builtin_amdgcn_readfirstlane(lds_byte_addr);
+    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" :: "v"(g), "{m0}"(m0) : "memory");
+}
+
+__device__ __forceinline__ int swz(int r, int q) { return r * 64 + 16 * (q ^ ((r >> 2) & 3)); }
+
+template <int MODE, int WM>
 __global__ __launch_bounds__(256) void convn_kernel(ConvGArgs a) {
+    constexpr int WN = 2;
     constexpr int BM = 64 * WM, BN = 64 * WN;
-    constexpr int TPP = 256 / BN, NBL = 4 / TPP;  // staging threads per pixel, 16-byte loads per thread
-    __shared__ __attribute__((aligned(16))) __bf16 As[2][BM][NRS];
-    __shared__ __attribute__((aligned(16))) __bf16 Bs[2][BN][NRS];
+    constexpr int ABYTES = BM * 64, STAGE = (BM + BN) * 64;
+    constexpr int NA = BM / 64, NB = BN / 64;  // DMA instructions per wave and chunk
+    __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+    const unsigned lds0 = (unsigned)(uintptr_t)(lds_void*)smem;
 
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
-    const int wave = tid >> 6, wr = wave >> 1, wc = wave & 1;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), wr = wave >> 1, wc = wave & 1;
     const int s = a.stride, pad = a.pad;
     const int ph = a.par >> 1, pw = a.par & 1;
     const int kh0 = (ph + pad) & 1, kw0 = (pw + pad) & 1;
@@ -152,63 +169,55 @@ __global__ __launch_bounds__(256) void convn_kernel(ConvGArgs a) {
         if (MODE == 1) { N = a.B * IHW; nth = a.KH; ntw = a.KW; }
         else { N = a.B * CHW; nth = (a.KH - kh0 + 1) / 2; ntw = (a.KW - kw0 + 1) / 2; }
     }
-    const int cpt = CK / NKB, nch = nth * ntw * cpt;
-    const int64_t K = (int64_t)nth * ntw * CK;  // packed row length (a multiple of 32)
+    const int T = nth * ntw, nch = T * (CK / NKB);
+    const int64_t K = (int64_t)T * CK;  // packed row length (a multiple of 32)
     const int64_t mt = (M + BM - 1) / BM;
     const int64_t tm = blockIdx.x % mt, tn = blockIdx.x / mt;
     const int64_t m0 = tm * BM, n0 = tn * BN;
 
-    // B staging: pixel bp of the tile, channels 8 NBL bh .. of every chunk
-    const int bp = tid / TPP, bh = tid % TPP;
-    int64_t nn = n0 + bp;
-    if (nn >= N) nn = N - 1;  // tail pixels load a valid row; their columns are never stored
-    int64_t pb;               // image element of the pixel's operand row at tap 0
-    if (MODE == 0) {
-        const int64_t b = nn / OHW;
-        const int r = (int)(nn - b * OHW), oh = r / a.OW, ow = r - oh * a.OW;
-        pb = ((b * Hp + oh * s - pad + 1) * Wp + ow * s - pad + 1) * CK;
-    } else if (MODE == 1) {
-        const int64_t b = nn / IHW;
-        const int r = (int)(nn - b * IHW), ih = r / a.IW, iw = r - ih * a.IW;
-        pb = ((b * Hp + ih + pad + 1) * Wp + iw + pad + 1) * CK;
-    } else {
-        const int64_t b = nn / CHW;
-        const int r = (int)(nn - b * CHW), ihc = r / IWc, iwc = r - ihc * IWc;
-        const int oh0 = (2 * ihc + ph + pad - kh0) >> 1, ow0 = (2 * iwc + pw + pad - kw0) >> 1;
-        pb = ((b * Hp + oh0 + 1) * Wp + ow0 + 1) * CK;
-    }
-    const __bf16* xb = static_cast<const __bf16*>(MODE == 0 ? a.xn : a.dyn) + pb + 8 * NBL * bh;
-    // A staging: packed weight rows am, am + 64, k 8 aq .. 8 aq + 7 of every chunk
-    const int am = tid >> 2, aq = tid & 3;
-    const __bf16* ap[WM];
-    bool av[WM];
+    // DMA roles: wave instruction j covers tile rows 16 (wave + 4 j) .. + 15; lane -> row lr, slot ls
+    const int lr = lane >> 2, ls = lane & 3;
+    const __bf16* asrc[NA];
 #pragma unroll
-    for (int j = 0; j < WM; ++j) {
-        const int64_t row = m0 + am + 64 * j;
-        av[j] = row < M;
-        ap[j] = static_cast<const __bf16*>(a.wpack) + (av[j] ? row : 0) * K + 8 * aq;
+    for (int j = 0; j < NA; ++j) {
+        const int r = 16 * (wave + 4 * j) + lr;
+        const int64_t row = m0 + r;  // rows past M copy row 0: finite, never stored
+        asrc[j] = static_cast<const __bf16*>(a.wpack) + (row < M ? row : 0) * K + 8 * (ls ^ ((r >> 2) & 3));
     }
-
-    // one register stage, stashed at the top of the next iteration: a chunk's loads have a whole
-    // iteration (MFMAs + barrier) to land before anything waits on them
-    struct Stage {
-        bf16x8 a[WM], b[NBL];
-    };
-    Stage st;
-    auto gather = [&](int ch, Stage& r) {
-        const int tap = ch / cpt, c0 = (ch - tap * cpt) * NKB;
+    const __bf16* bsrc[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+        const int r = 16 * (wave + 4 * j) + lr;
+        int64_t nn = n0 + r;
+        if (nn >= N) nn = N - 1;  // tail pixels copy a valid row; their columns are never stored
+        int64_t pb;               // image element of the pixel's operand row at tap 0
+        if (MODE == 0) {
+            const int64_t b = nn / OHW;
+            const int rr = (int)(nn - b * OHW), oh = rr / a.OW, ow = rr - oh * a.OW;
+            pb = ((b * Hp + oh * s - pad + 1) * Wp + ow * s - pad + 1) * CK;
+        } else if (MODE == 1) {
+            const int64_t b = nn / IHW;
+            const int rr = (int)(nn - b * IHW), ih = rr / a.IW, iw = rr - ih * a.IW;
+            pb = ((b * Hp + ih + pad + 1) * Wp + iw + pad + 1) * CK;
+        } else {
+            const int64_t b = nn / CHW;
+            const int rr = (int)(nn - b * CHW), ihc = rr / IWc, iwc = rr - ihc * IWc;
+            const int oh0 = (2 * ihc + ph + pad - kh0) >> 1, ow0 = (2 * iwc + pw + pad - kw0) >> 1;
+            pb = ((b * Hp + oh0 + 1) * Wp + ow0 + 1) * CK;
+        }
+        bsrc[j] = static_cast<const __bf16*>(MODE == 0 ? a.xn : a.dyn) + pb + 8 * (ls ^ ((r >> 2) & 3));
+    }
+    // K walks channel-major (32 channels x every tap, then the next 32): the taps of a channel
+    // group re-read one halo of the image back to back, out of L2
+    auto issue = [&](int ch, int stage) {
+        const int cc = ch / T, tap = ch - cc * T, c0 = cc * NKB;
         const int th = tap / ntw, tw = tap - th * ntw;
         const int toff = (MODE == 0 ? 1 : -1) * (th * Wp + tw) * CK + c0;
+        const unsigned base = lds0 + (unsigned)(stage * STAGE);
 #pragma unroll
-        for (int j = 0; j < NBL; ++j) r.b[j] = ld16(xb + toff + 8 * j);
+        for (int j = 0; j < NA; ++j) dma16(asrc[j] + (int64_t)ch * NKB, base + (unsigned)(16 * (wave + 4 * j) * 64));
 #pragma unroll
-        for (int j = 0; j < WM; ++j) r.a[j] = av[j] ? ld16(ap[j] + (int64_t)ch * NKB) : bf16x8{};
-    };
-    auto stash = [&](int buf, const Stage& r) {
-#pragma unroll
-        for (int j = 0; j < WM; ++j) *reinterpret_cast<bf16x8*>(&As[buf][am + 64 * j][8 * aq]) = r.a[j];
-#pragma unroll
-        for (int j = 0; j < NBL; ++j) *reinterpret_cast<bf16x8*>(&Bs[buf][bp][8 * NBL * bh + 8 * j]) = r.b[j];
+        for (int j = 0; j < NB; ++j) dma16(bsrc[j] + toff, base + (unsigned)(ABYTES + 16 * (wave + 4 * j) * 64));
     };
 
     f32x16 acc[WM][WN];
@@ -217,31 +226,26 @@ __global__ __launch_bounds__(256) void convn_kernel(ConvGArgs a) {
 #pragma unroll
         for (int ni = 0; ni < WN; ++ni) acc[mi][ni] = f32x16{0.f};
 
-    if (nch > 0) {
-        gather(0, st);
-        stash(0, st);
-        if (nch > 1) gather(1, st);
-    }
-    __syncthreads();
+    if (nch > 0) issue(0, 0);
     for (int ch = 0; ch < nch; ++ch) {
-        const int buf = ch & 1;
-        if (ch + 1 < nch) stash(buf ^ 1, st);  // (buf ^ 1 was last read before the previous barrier)
-        if (ch + 2 < nch) gather(ch + 2, st);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // chunk ch in LDS for every wave; the other stage's readers are done
+        if (ch + 1 < nch) issue(ch + 1, (ch + 1) & 1);
+        const char* st = smem + (ch & 1) * STAGE;
 #pragma unroll
         for (int ks = 0; ks < NKB / 16; ++ks) {
             bf16x8 av8[WM], bv8[WN];
 #pragma unroll
             for (int mi = 0; mi < WM; ++mi)
-                av8[mi] = *reinterpret_cast<const bf16x8*>(&As[buf][wr * 32 * WM + mi * 32 + l32][16 * ks + 8 * h]);
+                av8[mi] = *reinterpret_cast<const bf16x8*>(st + swz(wr * 32 * WM + mi * 32 + l32, 2 * ks + h));
 #pragma unroll
             for (int ni = 0; ni < WN; ++ni)
-                bv8[ni] = *reinterpret_cast<const bf16x8*>(&Bs[buf][wc * 32 * WN + ni * 32 + l32][16 * ks + 8 * h]);
+                bv8[ni] = *reinterpret_cast<const bf16x8*>(st + ABYTES + swz(wc * 32 * WN + ni * 32 + l32, 2 * ks + h));
 #pragma unroll
             for (int mi = 0; mi < WM; ++mi)
 #pragma unroll
                 for (int ni = 0; ni < WN; ++ni) acc[mi][ni] = mfma_bf16(av8[mi], bv8[ni], acc[mi][ni]);
         }
-        __syncthreads();
     }
 
     // ---- epilogue: planar NCHW float32 (columns = pixels: 128-byte rows per MFMA output row)
@@ -441,6 +445,22 @@ __global__ __launch_bounds__(256) void convn_wgrad_kernel(ConvGArgs a) {
     }
 }
 
+// weight rows of the forward / data-gradient kernel: row m, k = (c / 32) (T 32) + t 32 + c % 32 over
+// the T (class) taps t = th ntw + tw, kernel tap (kh0 + step th, kw0 + step tw), step 2 for mode 3
+__global__ __launch_bounds__(256) void convn_pack_kernel(const float* __restrict__ w, __bf16* __restrict__ wp, int mode,
+                                                         int cin, int cout, int KH, int KW, int kh0, int kw0, int step,
+                                                         int ntw, int T, int64_t M, int64_t K) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= M * K) return;
+    const int64_t m = i / K;
+    const int k = (int)(i - m * K);
+    const int cc = k / (T * NKB), rem = k - cc * T * NKB, t = rem / NKB, c = cc * NKB + rem - t * NKB;
+    const int kh = kh0 + step * (t / ntw), kw = kw0 + step * (t % ntw);
+    const float v = mode == 0 ? w[((m * cin + c) * KH + kh) * KW + kw]            // [cout = m][cin = c]
+                              : w[(((int64_t)c * cin + m) * KH + kh) * KW + kw];  // [cout = c][cin = m]
+    wp[i] = (__bf16)v;
+}
+
 }  // namespace
 
 size_t nhwc_bytes(int B, int C, int H, int W) { return (size_t)B * (H + 2) * (W + 2) * C * 2; }
@@ -495,22 +515,37 @@ int launch_convn(const ConvGArgs& a, hipStream_t s) {
         N = a.B * (int64_t)((a.IH - (a.par >> 1) + 1) / 2) * ((a.IW - (a.par & 1) + 1) / 2);
     }
     if (N == 0) return PCX_OK;
-    if (a.mode == 3 && a.accumulate) {  // a parity class without taps (1x1 stride 2) adds nothing
-        const int kh0 = ((a.par >> 1) + a.pad) & 1, kw0 = ((a.par & 1) + a.pad) & 1;
-        if ((a.KH - kh0 + 1) / 2 == 0 || (a.KW - kw0 + 1) / 2 == 0) return PCX_OK;
+    int kh0 = 0, kw0 = 0, nth = a.KH, ntw = a.KW, step = 1;
+    if (a.mode == 3) {
+        kh0 = ((a.par >> 1) + a.pad) & 1;
+        kw0 = ((a.par & 1) + a.pad) & 1;
+        nth = (a.KH - kh0 + 1) / 2;
+        ntw = (a.KW - kw0 + 1) / 2;
+        step = 2;
+        // a parity class without taps (1x1 stride 2) adds nothing
+        if ((nth == 0 || ntw == 0) && a.accumulate) return PCX_OK;
+    }
+    {
+        const int64_t K = (int64_t)nth * ntw * (a.mode == 0 ? a.cin : a.cout);
+        if (M * K > 0) {
+            convn_pack_kernel<<<(unsigned)ceil_div(M * K, 256), 256, 0, s>>>(
+                a.w, static_cast<__bf16*>(const_cast<void*>(a.wpack)), a.mode == 0 ? 0 : 1, a.cin, a.cout, a.KH, a.KW,
+                kh0, kw0, step, ntw, nth * ntw, M, K);
+            PCX_LAUNCH_CHECK("convn_pack_kernel");
+        }
     }
     const int wm = M >= 128 ? 2 : 1;
     constexpr int wn = 2;  // (128 x 256 tiles measured slower: 2 blocks per CU instead of 4)
     const int64_t nblocks = ceil_div(M, 64 * wm) * ceil_div(N, 64 * wn);
     PCX_CHECK_ARG(nblocks < ((int64_t)1 << 31), "convn: grid too large");
     dim3 grid((unsigned)nblocks);
-#define PCX_CN(MODE_, WM_, WN_)                                                                \
-    if (a.mode == MODE_ && wm == WM_ && wn == WN_) {                                           \
-        convn_kernel<MODE_, WM_, WN_><<<grid, 256, 0, s>>>(a);                                 \
+#define PCX_CN(MODE_, WM_)                                                                     \
+    if (a.mode == MODE_ && wm == WM_) {                                                        \
+        convn_kernel<MODE_, WM_><<<grid, 256, 0, s>>>(a);                                      \
         PCX_LAUNCH_CHECK("convn_kernel");                                                      \
         return PCX_OK;                                                                         \
     }
-    PCX_CN(0, 1, 2) PCX_CN(0, 2, 2) PCX_CN(1, 1, 2) PCX_CN(1, 2, 2) PCX_CN(3, 1, 2) PCX_CN(3, 2, 2)
+    PCX_CN(0, 1) PCX_CN(0, 2) PCX_CN(1, 1) PCX_CN(1, 2) PCX_CN(3, 1) PCX_CN(3, 2)
 #undef PCX_CN
     set_error("convn: mode %d unsupported", a.mode);
     return PCX_EINVAL;

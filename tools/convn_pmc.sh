@@ -1,23 +1,30 @@
 #!/bin/bash
-# SQ stall counters of the channel-last conv kernels on one block-0 shape (analysis aid).
-set -eo pipefail
+# PMC passes (one counter group per run, counters only) over the channel-last conv micro-benchmark;
+# prints the counters of the last convn_kernel dispatch of each pass.  Analysis aid.
 export TMPDIR=/tmp
 ROOT=$(pwd)
 OUT=gpurun_out/convn_pmc
-mkdir -p $OUT
-for m in 0 1 2; do
-  timeout -k 10 120 python3 tools/convn_bench.py --mode $m --shape ${SHAPE:-4096,64,64,20,100,3,1,1}
-done
-timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
-    SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT -f csv -d "$ROOT/$OUT/sq" -o run -- \
-    python3 "$ROOT/tools/convn_bench.py" --mode 0 --iters 2 --shape ${SHAPE:-4096,64,64,20,100,3,1,1} > /dev/null 2> $OUT/sq.err
+SHAPE=${SHAPE:-2048,256,256,20,100,3,1,1}
+MODE=${MODE:-0}
+rm -rf $OUT; mkdir -p $OUT
+pass() {
+  local name=$1; shift
+  timeout -s KILL 60 rocprofv3 --pmc "$@" -f csv -d "$ROOT/$OUT/$name" -o run -- \
+      python3 "$ROOT/tools/convn_bench.py" --mode $MODE --iters 2 --shape $SHAPE > /dev/null 2> $OUT/$name.err
+  echo "pass $name rc=$?"
+}
+pass sq SQ_INSTS_VMEM_RD SQ_INST_LEVEL_VMEM SQ_INSTS_LDS SQ_INST_LEVEL_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_ANY
+pass tcp TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum
+pass tcc TCC_HIT_sum TCC_MISS_sum
+pass ta TA_ADDR_STALLED_BY_TC_CYCLES_sum TA_DATA_STALLED_BY_TC_CYCLES_sum
 python3 - $OUT <<'PY'
 import csv, glob, sys, collections
-f = glob.glob(sys.argv[1] + "/sq/**/*counter_collection.csv", recursive=True)[0]
-acc = collections.defaultdict(lambda: collections.defaultdict(float))
-for r in csv.DictReader(open(f)):
-    if "convn_kernel" in r["Kernel_Name"]:
-        acc[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
-for d, c in list(acc.items())[-1:]:
-    for k, v in sorted(c.items()): print("%-28s %.4g" % (k, v))
+for f in sorted(glob.glob(sys.argv[1] + "/*/**/*counter_collection.csv", recursive=True)):
+    acc = collections.OrderedDict()
+    for r in csv.DictReader(open(f)):
+        if "convn_kernel" in r["Kernel_Name"]:
+            acc.setdefault(r["Dispatch_Id"], collections.defaultdict(float))[r["Counter_Name"]] += float(r["Counter_Value"])
+    if acc:
+        d = list(acc.values())[-1]
+        print(" ".join("%s=%.4g" % kv for kv in sorted(d.items())))
 PY
