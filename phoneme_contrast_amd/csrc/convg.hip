@@ -376,39 +376,49 @@ struct PlaneWalk {
     }
 };
 
-// Forward BN partials of y [B][C][P]: block (c, slice) -> (sum, M2 about the block mean, count),
-// accumulated in float64 about a shift (first element) — consumed by launch_bn_fwd_finalize.
+// Forward BN partials of y [B][C][P]: block (c, slice) -> (sum, M2 about the block mean, count).
+// Elements are walked in units of V (16-byte loads when P % 4 == 0), U units in flight per thread;
+// a unit's shifted values are summed in float32, the running sums are float64 about a shift (the
+// slice's first element) — consumed by launch_bn_fwd_finalize.
+template <int V, int U>
 __global__ __launch_bounds__(256) void chan_stats_kernel(const float* __restrict__ y, int B, int C, int64_t P64,
                                                          int bps, float* part0, float* part1, float* partn) {
+    typedef float fv __attribute__((ext_vector_type(V)));
     __shared__ double red[4];
     const int c = blockIdx.x, sl = blockIdx.y, nsl = gridDim.y;
     const int b0 = sl * bps, b1 = min(B, b0 + bps);
-    const int P = (int)P64;
-    const double K = b0 < B ? (double)y[((int64_t)b0 * C + c) * P] : 0.0;
+    const int P = (int)P64, PV = P / V;
+    const float K = b0 < B ? y[((int64_t)b0 * C + c) * P] : 0.f;
     double s1 = 0.0, s2 = 0.0;
-    PlaneWalk w(b0, P);
-    while (w.b < b1) {  // 4 independent loads in flight per thread
-        float v[4];
-        bool ok[4];
+    PlaneWalk w(b0, PV);
+    while (w.b < b1) {
+        fv v[U];
+        bool ok[U];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < U; ++u) {
             ok[u] = w.b < b1;
-            v[u] = ok[u] ? y[((int64_t)w.b * C + c) * P + w.p] : 0.f;
-            w.next(P);
+            v[u] = ok[u] ? *reinterpret_cast<const fv*>(y + ((int64_t)w.b * C + c) * P + (int64_t)w.p * V) : fv{};
+            w.next(PV);
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < U; ++u)
             if (ok[u]) {
-                const double d = (double)v[u] - K;
-                s1 += d;
-                s2 += d * d;
+                float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+                for (int e = 0; e < V; ++e) {
+                    const float d = v[u][e] - K;
+                    t1 += d;
+                    t2 = fmaf(d, d, t2);
+                }
+                s1 += (double)t1;
+                s2 += (double)t2;
             }
     }
     s1 = block_sum(s1, red);
     s2 = block_sum(s2, red);
     if (threadIdx.x == 0) {
         const double n = (double)(b1 > b0 ? b1 - b0 : 0) * (double)P;
-        part0[(int64_t)c * nsl + sl] = (float)(n * K + s1);
+        part0[(int64_t)c * nsl + sl] = (float)(n * (double)K + s1);
         part1[(int64_t)c * nsl + sl] = n > 0 ? (float)fmax(s2 - s1 * s1 / n, 0.0) : 0.f;
         if (c == 0) partn[sl] = (float)n;
     }
@@ -416,48 +426,56 @@ __global__ __launch_bounds__(256) void chan_stats_kernel(const float* __restrict
 
 // Backward BN partials: g = d (+ d2) masked, written to g; sums of g and g*xhat_k for up to two
 // BNs (the main-path BN and the shortcut BN of a residual block share the same upstream g).
+// Units of V elements (16-byte accesses when P % 4 == 0), U units in flight per thread.
+template <int V, int U>
 __global__ __launch_bounds__(256) void bwd_prep_kernel(BwdPrepArgs a) {
+    typedef float fv __attribute__((ext_vector_type(V)));
     __shared__ double red[4];
     const int c = blockIdx.x, sl = blockIdx.y, nsl = gridDim.y;
     const int b0 = sl * a.bps, b1 = min(a.B, b0 + a.bps);
-    const int P = (int)a.P;
+    const int P = (int)a.P, PV = P / V;
     const float4 mc = a.mask_cf ? a.mask_cf[c] : make_float4(1.f, 0.f, 0.f, 1.f);
     const float4 c1 = a.cf1 ? a.cf1[c] : make_float4(0.f, 0.f, 0.f, 0.f);
     const float4 c2 = a.cf2 ? a.cf2[c] : make_float4(0.f, 0.f, 0.f, 0.f);
     double sg = 0.0, sx1 = 0.0, sx2 = 0.0;
-    PlaneWalk w(b0, P);
-    while (w.b < b1) {  // 2 elements per iteration: their loads are issued together
-        int64_t o[2], bc[2];
-        bool ok[2];
-        float g[2], m[2], y1v[2], y2v[2];
+    PlaneWalk w(b0, PV);
+    while (w.b < b1) {
+        int64_t o[U], bc[U];
+        bool ok[U];
+        fv g[U], m[U], y1v[U], y2v[U];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < U; ++u) {
             ok[u] = w.b < b1;
             bc[u] = (int64_t)(ok[u] ? w.b : b0) * a.C + c;
-            o[u] = bc[u] * P + (ok[u] ? w.p : 0);
-            w.next(P);
+            o[u] = bc[u] * P + (ok[u] ? (int64_t)w.p * V : 0);
+            w.next(PV);
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            g[u] = a.d[o[u]];
-            if (a.d2) g[u] += a.d2[o[u]];
-            m[u] = a.mask_mode != MASK_NONE ? a.mask_src[o[u]] : 0.f;
-            y1v[u] = a.y1 ? a.y1[o[u]] : 0.f;
-            y2v[u] = a.y2 ? a.y2[o[u]] : 0.f;
+        for (int u = 0; u < U; ++u) {
+            g[u] = *reinterpret_cast<const fv*>(a.d + o[u]);
+            if (a.d2) g[u] += *reinterpret_cast<const fv*>(a.d2 + o[u]);
+            m[u] = a.mask_mode != MASK_NONE ? *reinterpret_cast<const fv*>(a.mask_src + o[u]) : fv{};
+            y1v[u] = a.y1 ? *reinterpret_cast<const fv*>(a.y1 + o[u]) : fv{};
+            y2v[u] = a.y2 ? *reinterpret_cast<const fv*>(a.y2 + o[u]) : fv{};
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < U; ++u) {
             if (!ok[u]) continue;
-            float gv = g[u];
-            if (a.mask_mode == MASK_OUT) {
-                gv = m[u] > 0.f ? gv : 0.f;
-            } else if (a.mask_mode == MASK_BN) {
-                gv = fmaf(m[u], mc.x, mc.y) > 0.f ? gv * (a.drop ? a.drop[bc[u]] : 1.f) : 0.f;
+            const float dr = a.mask_mode == MASK_BN && a.drop ? a.drop[bc[u]] : 1.f;
+            fv gv = g[u];
+            float tg = 0.f, t1 = 0.f, t2 = 0.f;
+#pragma unroll
+            for (int e = 0; e < V; ++e) {
+                if (a.mask_mode == MASK_OUT) gv[e] = m[u][e] > 0.f ? gv[e] : 0.f;
+                else if (a.mask_mode == MASK_BN) gv[e] = fmaf(m[u][e], mc.x, mc.y) > 0.f ? gv[e] * dr : 0.f;
+                tg += gv[e];
+                if (a.y1) t1 = fmaf(gv[e], (y1v[u][e] - c1.z) * c1.w, t1);
+                if (a.y2) t2 = fmaf(gv[e], (y2v[u][e] - c2.z) * c2.w, t2);
             }
-            a.g[o[u]] = gv;
-            sg += (double)gv;
-            if (a.y1) sx1 += (double)gv * (double)((y1v[u] - c1.z) * c1.w);
-            if (a.y2) sx2 += (double)gv * (double)((y2v[u] - c2.z) * c2.w);
+            *reinterpret_cast<fv*>(a.g + o[u]) = gv;
+            sg += (double)tg;
+            sx1 += (double)t1;
+            sx2 += (double)t2;
         }
     }
     sg = block_sum(sg, red);
@@ -853,7 +871,8 @@ int launch_chan_stats(const float* y, int B, int C, int64_t P, float* part0, flo
     int bps;
     const int ns = chan_slices(B, C, &bps);
     *nslice = ns;
-    chan_stats_kernel<<<dim3(C, ns), 256, 0, s>>>(y, B, C, P, bps, part0, part1, partn);
+    if (P % 4 == 0) chan_stats_kernel<4, 4><<<dim3(C, ns), 256, 0, s>>>(y, B, C, P, bps, part0, part1, partn);
+    else chan_stats_kernel<1, 8><<<dim3(C, ns), 256, 0, s>>>(y, B, C, P, bps, part0, part1, partn);
     PCX_LAUNCH_CHECK("chan_stats_kernel");
     return PCX_OK;
 }
@@ -861,7 +880,8 @@ int launch_chan_stats(const float* y, int B, int C, int64_t P, float* part0, flo
 int launch_bwd_prep(BwdPrepArgs a, int* nslice, hipStream_t s) {
     const int ns = chan_slices(a.B, a.C, &a.bps);
     *nslice = ns;
-    bwd_prep_kernel<<<dim3(a.C, ns), 256, 0, s>>>(a);
+    if (a.P % 4 == 0) bwd_prep_kernel<4, 2><<<dim3(a.C, ns), 256, 0, s>>>(a);
+    else bwd_prep_kernel<1, 4><<<dim3(a.C, ns), 256, 0, s>>>(a);
     PCX_LAUNCH_CHECK("bwd_prep_kernel");
     return PCX_OK;
 }
