@@ -141,14 +141,20 @@ __device__ __forceinline__ void dma16(const __bf16* g, unsigned lds_byte_addr) {
     asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" :: "v"(g), "{m0}"(m0) : "memory");
 }
 
-__device__ __forceinline__ int swz(int r, int q) { return r * 64 + 16 * (q ^ ((r >> 2) & 3)); }
+// rows of KC bf16 (64 / 128 bytes): logical 16-byte run q of row r in slot q ^ f(r); f spreads the
+// rows one ds_read_b128 lane group reads over all 64 banks
+template <int KC>
+__device__ __forceinline__ int swz(int r, int q) {
+    return KC == 32 ? r * 64 + 16 * (q ^ ((r >> 2) & 3)) : r * 128 + 16 * (q ^ ((r >> 1) & 7));
+}
 
-template <int MODE, int WM>
+template <int MODE, int WM, int KC>
 __global__ __launch_bounds__(256) void convn_kernel(ConvGArgs a) {
     constexpr int WN = 2;
     constexpr int BM = 64 * WM, BN = 64 * WN;
-    constexpr int ABYTES = BM * 64, STAGE = (BM + BN) * 64;
-    constexpr int NA = BM / 64, NB = BN / 64;  // DMA instructions per wave and chunk
+    constexpr int RB = 2 * KC, RPI = 1024 / RB, SPR = RB / 16;  // row bytes, rows per DMA instruction, runs per row
+    constexpr int ABYTES = BM * RB, STAGE = (BM + BN) * RB;
+    constexpr int NA = BM / RPI / 4, NB = BN / RPI / 4;  // DMA instructions per wave and chunk
     __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
     const unsigned lds0 = (unsigned)(uintptr_t)(lds_void*)smem;
 
@@ -169,25 +175,26 @@ __global__ __launch_bounds__(256) void convn_kernel(ConvGArgs a) {
         if (MODE == 1) { N = a.B * IHW; nth = a.KH; ntw = a.KW; }
         else { N = a.B * CHW; nth = (a.KH - kh0 + 1) / 2; ntw = (a.KW - kw0 + 1) / 2; }
     }
-    const int T = nth * ntw, nch = T * (CK / NKB);
+    const int T = nth * ntw, nch = T * (CK / KC);
     const int64_t K = (int64_t)T * CK;  // packed row length (a multiple of 32)
     const int64_t mt = (M + BM - 1) / BM;
     const int64_t tm = blockIdx.x % mt, tn = blockIdx.x / mt;
     const int64_t m0 = tm * BM, n0 = tn * BN;
 
-    // DMA roles: wave instruction j covers tile rows 16 (wave + 4 j) .. + 15; lane -> row lr, slot ls
-    const int lr = lane >> 2, ls = lane & 3;
+    // DMA roles: wave instruction j covers tile rows RPI (wave + 4 j) ..; lane -> row lr, slot ls
+    const int lr = lane / SPR, ls = lane % SPR;
+    auto slot_run = [&](int r) { return KC == 32 ? ls ^ ((r >> 2) & 3) : ls ^ ((r >> 1) & 7); };
     const __bf16* asrc[NA];
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
-        const int r = 16 * (wave + 4 * j) + lr;
+        const int r = RPI * (wave + 4 * j) + lr;
         const int64_t row = m0 + r;  // rows past M copy row 0: finite, never stored
-        asrc[j] = static_cast<const __bf16*>(a.wpack) + (row < M ? row : 0) * K + 8 * (ls ^ ((r >> 2) & 3));
+        asrc[j] = static_cast<const __bf16*>(a.wpack) + (row < M ? row : 0) * K + 8 * slot_run(r);
     }
     const __bf16* bsrc[NB];
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-        const int r = 16 * (wave + 4 * j) + lr;
+        const int r = RPI * (wave + 4 * j) + lr;
         int64_t nn = n0 + r;
         if (nn >= N) nn = N - 1;  // tail pixels copy a valid row; their columns are never stored
         int64_t pb;               // image element of the pixel's operand row at tap 0
@@ -205,19 +212,19 @@ __global__ __launch_bounds__(256) void convn_kernel(ConvGArgs a) {
             const int oh0 = (2 * ihc + ph + pad - kh0) >> 1, ow0 = (2 * iwc + pw + pad - kw0) >> 1;
             pb = ((b * Hp + oh0 + 1) * Wp + ow0 + 1) * CK;
         }
-        bsrc[j] = static_cast<const __bf16*>(MODE == 0 ? a.xn : a.dyn) + pb + 8 * (ls ^ ((r >> 2) & 3));
+        bsrc[j] = static_cast<const __bf16*>(MODE == 0 ? a.xn : a.dyn) + pb + 8 * slot_run(r);
     }
     // K walks channel-major (32 channels x every tap, then the next 32): the taps of a channel
     // group re-read one halo of the image back to back, out of L2
     auto issue = [&](int ch, int stage) {
-        const int cc = ch / T, tap = ch - cc * T, c0 = cc * NKB;
+        const int cc = ch / T, tap = ch - cc * T, c0 = cc * KC;
         const int th = tap / ntw, tw = tap - th * ntw;
         const int toff = (MODE == 0 ? 1 : -1) * (th * Wp + tw) * CK + c0;
         const unsigned base = lds0 + (unsigned)(stage * STAGE);
 #pragma unroll
-        for (int j = 0; j < NA; ++j) dma16(asrc[j] + (int64_t)ch * NKB, base + (unsigned)(16 * (wave + 4 * j) * 64));
+        for (int j = 0; j < NA; ++j) dma16(asrc[j] + (int64_t)ch * KC, base + (unsigned)(RPI * (wave + 4 * j) * RB));
 #pragma unroll
-        for (int j = 0; j < NB; ++j) dma16(bsrc[j] + toff, base + (unsigned)(ABYTES + 16 * (wave + 4 * j) * 64));
+        for (int j = 0; j < NB; ++j) dma16(bsrc[j] + toff, base + (unsigned)(ABYTES + RPI * (wave + 4 * j) * RB));
     };
 
     f32x16 acc[WM][WN];
@@ -233,14 +240,14 @@ __global__ __launch_bounds__(256) void convn_kernel(ConvGArgs a) {
         if (ch + 1 < nch) issue(ch + 1, (ch + 1) & 1);
         const char* st = smem + (ch & 1) * STAGE;
 #pragma unroll
-        for (int ks = 0; ks < NKB / 16; ++ks) {
+        for (int ks = 0; ks < KC / 16; ++ks) {
             bf16x8 av8[WM], bv8[WN];
 #pragma unroll
             for (int mi = 0; mi < WM; ++mi)
-                av8[mi] = *reinterpret_cast<const bf16x8*>(st + swz(wr * 32 * WM + mi * 32 + l32, 2 * ks + h));
+                av8[mi] = *reinterpret_cast<const bf16x8*>(st + swz<KC>(wr * 32 * WM + mi * 32 + l32, 2 * ks + h));
 #pragma unroll
             for (int ni = 0; ni < WN; ++ni)
-                bv8[ni] = *reinterpret_cast<const bf16x8*>(st + ABYTES + swz(wc * 32 * WN + ni * 32 + l32, 2 * ks + h));
+                bv8[ni] = *reinterpret_cast<const bf16x8*>(st + ABYTES + swz<KC>(wc * 32 * WN + ni * 32 + l32, 2 * ks + h));
 #pragma unroll
             for (int mi = 0; mi < WM; ++mi)
 #pragma unroll
@@ -445,16 +452,16 @@ __global__ __launch_bounds__(256) void convn_wgrad_kernel(ConvGArgs a) {
     }
 }
 
-// weight rows of the forward / data-gradient kernel: row m, k = (c / 32) (T 32) + t 32 + c % 32 over
+// weight rows of the forward / data-gradient kernel: row m, k = (c / KC) (T KC) + t KC + c % KC over
 // the T (class) taps t = th ntw + tw, kernel tap (kh0 + step th, kw0 + step tw), step 2 for mode 3
 __global__ __launch_bounds__(256) void convn_pack_kernel(const float* __restrict__ w, __bf16* __restrict__ wp, int mode,
                                                          int cin, int cout, int KH, int KW, int kh0, int kw0, int step,
-                                                         int ntw, int T, int64_t M, int64_t K) {
+                                                         int ntw, int T, int KC, int64_t M, int64_t K) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= M * K) return;
     const int64_t m = i / K;
     const int k = (int)(i - m * K);
-    const int cc = k / (T * NKB), rem = k - cc * T * NKB, t = rem / NKB, c = cc * NKB + rem - t * NKB;
+    const int cc = k / (T * KC), rem = k - cc * T * KC, t = rem / KC, c = cc * KC + rem - t * KC;
     const int kh = kh0 + step * (t / ntw), kw = kw0 + step * (t % ntw);
     const float v = mode == 0 ? w[((m * cin + c) * KH + kh) * KW + kw]            // [cout = m][cin = c]
                               : w[(((int64_t)c * cin + m) * KH + kh) * KW + kw];  // [cout = c][cin = m]
@@ -483,6 +490,10 @@ int launch_to_nhwc(NhwcArgs a, hipStream_t s) {
     PCX_LAUNCH_CHECK("to_nhwc_kernel");
     return PCX_OK;
 }
+
+// K per chunk of the forward / data-gradient kernel: 64 channels (128-byte rows: whole-line requests,
+// 14 % faster than 32 on the 256-channel layers) where the channel count allows
+static int convn_kc(int ck) { return ck % 64 == 0 ? 64 : 32; }
 
 bool convn_fits(const ConvGArgs& a) {
     if (a.KH != a.KW || (a.KH != 1 && a.KH != 3) || a.pad > 1 || a.pad < 0) return false;
@@ -525,12 +536,14 @@ int launch_convn(const ConvGArgs& a, hipStream_t s) {
         // a parity class without taps (1x1 stride 2) adds nothing
         if ((nth == 0 || ntw == 0) && a.accumulate) return PCX_OK;
     }
+    const int ck = a.mode == 0 ? a.cin : a.cout;
+    const int kc = convn_kc(ck);
     {
-        const int64_t K = (int64_t)nth * ntw * (a.mode == 0 ? a.cin : a.cout);
+        const int64_t K = (int64_t)nth * ntw * ck;
         if (M * K > 0) {
             convn_pack_kernel<<<(unsigned)ceil_div(M * K, 256), 256, 0, s>>>(
                 a.w, static_cast<__bf16*>(const_cast<void*>(a.wpack)), a.mode == 0 ? 0 : 1, a.cin, a.cout, a.KH, a.KW,
-                kh0, kw0, step, ntw, nth * ntw, M, K);
+                kh0, kw0, step, ntw, nth * ntw, kc, M, K);
             PCX_LAUNCH_CHECK("convn_pack_kernel");
         }
     }
@@ -539,13 +552,14 @@ int launch_convn(const ConvGArgs& a, hipStream_t s) {
     const int64_t nblocks = ceil_div(M, 64 * wm) * ceil_div(N, 64 * wn);
     PCX_CHECK_ARG(nblocks < ((int64_t)1 << 31), "convn: grid too large");
     dim3 grid((unsigned)nblocks);
-#define PCX_CN(MODE_, WM_)                                                                     \
-    if (a.mode == MODE_ && wm == WM_) {                                                        \
-        convn_kernel<MODE_, WM_><<<grid, 256, 0, s>>>(a);                                      \
+#define PCX_CN(MODE_, WM_, KC_)                                                                \
+    if (a.mode == MODE_ && wm == WM_ && kc == KC_) {                                           \
+        convn_kernel<MODE_, WM_, KC_><<<grid, 256, 0, s>>>(a);                                 \
         PCX_LAUNCH_CHECK("convn_kernel");                                                      \
         return PCX_OK;                                                                         \
     }
-    PCX_CN(0, 1) PCX_CN(0, 2) PCX_CN(1, 1) PCX_CN(1, 2) PCX_CN(3, 1) PCX_CN(3, 2)
+    PCX_CN(0, 1, 32) PCX_CN(0, 2, 32) PCX_CN(1, 1, 32) PCX_CN(1, 2, 32) PCX_CN(3, 1, 32) PCX_CN(3, 2, 32)
+    PCX_CN(0, 1, 64) PCX_CN(0, 2, 64) PCX_CN(1, 1, 64) PCX_CN(1, 2, 64) PCX_CN(3, 1, 64) PCX_CN(3, 2, 64)
 #undef PCX_CN
     set_error("convn: mode %d unsupported", a.mode);
     return PCX_EINVAL;
