@@ -1,0 +1,714 @@
+// 3x3 / stride 1 / pad 1 convolution (forward and data gradient) as Winograd F(2x2, 3x3) on fp32
+// MFMA (v_mfma_f32_16x16x4_f32).  Same contract as conv3x3_dma (ConvArgs, prologues, epilogues),
+// 16 multiplies per 2x2 output tile instead of 36: 4/9 of the direct conv's MFMA work, all of it
+// in exact fp32 (the transforms are additions; the weight transform is evaluated in float64).
+//
+//   Y = A^T [ U (.) V ] A,   U = G g G^T (weights, once per call),   V = B^T d B (4x4 input patch)
+//
+// Per Winograd element xi (16 of them) the tile contraction is a GEMM over input channels:
+// M_xi[cout][tile] = sum_c U_xi[cout][c] V_xi[c][tile].  MFMA orientation: A = U (16 couts x 4
+// channels), B = V (4 channels x 16 tiles), so lane l owns the (channel l >> 4, tile l & 15)
+// patch: it reads the 4x4 patch from LDS, applies the producer's BN + ReLU, transforms it in
+// registers and feeds the 16 values to 16 MFMAs (x 2 cout sub-tiles).  The accumulators of lane l
+// hold, for every xi, the same (cout, tile) positions, so the output transform is also per lane.
+//
+// Layout / staging (MI355X-first):
+//  * persistent workgroups (two per CU) walk units = (64 consecutive tiles of one sample in row-major
+//    tile order, 32 output channels); consecutive units (neighbouring rows, the other channel groups
+//    of the same tiles) run on one XCD, so the halo rows they share come from that XCD's L2;
+//  * wave w owns tiles 16 w .. 16 w + 15 of the unit: one or two row segments of one or two tile
+//    rows.  Its LDS slot holds, per input channel, the 4 input rows of those segments side by side
+//    (<= 36 columns), so every patch of the wave is a 4 x 4 window of one slot at a per-lane column;
+//  * the slot of a K-chunk (CK channels) is copied HBM/L2 -> LDS by buffer_load_dword ... lds with
+//    per-lane offsets computed once per unit (the channel is the buffer base), double buffered
+//    across chunks and units (the next unit's first chunk lands during this unit's last chunk and
+//    epilogue); out-of-image positions carry an out-of-range offset and copy a 0 (BN+ReLU operands
+//    of border waves are zeroed again after the prologue by per-row / per-column factors);
+//  * slot plane stride = 32 mod 64 floats: the 32 lanes of a ds_read_b64 group (16 consecutive
+//    tiles x 2 channels) cover the 64 banks once;
+//  * transformed weights U are packed [cout / 32][cin][4][32][4] (xi = 4 q + e innermost), one
+//    contiguous run per K-chunk: dwordx4 DMA, conflict-free ds_read_b128 A operands;
+//  * epilogue: the 16 lanes of a row hold 16 consecutive tiles, so output rows are stored (and the
+//    producer's y / pooled windows loaded) as 128- / 256-byte runs.
+#include <type_traits>
+
+#include "conv_epilogue.h"
+
+namespace pcx {
+namespace {
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// global -> LDS copy (saddr form): global = uniform base + per-lane byte offset, LDS = M0 + lane * 4 * VEC
+template <int VEC>
+__device__ __forceinline__ void wdma(const float* sbase, unsigned voff, unsigned lds_byte_addr) {
+    const unsigned m0 = __builtin_amdgcn_readfirstlane(lds_byte_addr);
+    if constexpr (VEC == 4)
+        asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" :: "v"(voff), "s"(sbase), "{m0}"(m0) : "memory");
+    else
+        asm volatile("s_nop 0\n\tglobal_load_lds_dword %0, %1" :: "v"(voff), "s"(sbase), "{m0}"(m0) : "memory");
+}
+
+__device__ __forceinline__ const float* wuniform(const float* p) {
+    const uint64_t v = (uint64_t)(uintptr_t)p;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+    return (const float*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
+
+// per-wave staging slot: CK channel planes of 4 rows x WSW columns (two row segments: the wave's
+// 16 tiles in row-major order span at most two tile rows), plane stride WSP = 32 mod 64 floats
+constexpr int WSW = 36, WSP = 160;
+
+// LDS DMA of one dword per lane from a buffer resource (out-of-range offsets write 0);
+// LDS destination = M0 + 4 * lane.  HALF: only lanes 0..15 take part (exec set inside the asm).
+template <bool HALF>
+__device__ __forceinline__ void bdma(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned lds_byte_addr) {
+    const unsigned m0 = __builtin_amdgcn_readfirstlane(lds_byte_addr);
+    if constexpr (HALF) {
+        unsigned long long save;
+        asm volatile("s_mov_b64 %0, exec\n\ts_mov_b64 exec, 0xffff\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds\n\ts_mov_b64 exec, %0"
+                     : "=&s"(save) : "v"(voff), "s"(r), "{m0}"(m0) : "memory");
+    } else {
+        asm volatile("s_nop 0\n\tbuffer_load_dword %0, %1, 0 offen lds" :: "v"(voff), "s"(r), "{m0}"(m0) : "memory");
+    }
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wrsrc(const float* base, int bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, bytes, 0x00020000);
+}
+
+// sum over the 16 lanes of a row (lanes sharing l >> 4)
+__device__ __forceinline__ float row16_sum(float v) {
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    v += __shfl_xor(v, 4, 64);
+    v += __shfl_xor(v, 8, 64);
+    return v;
+}
+// transposed butterfly: v[j] (j < 8) summed over the 16 lanes of a row in 8 shuffles; lane n
+// returns the total of j = (n >> 1) & 7
+__device__ __forceinline__ float row16_xsum8(const float (&v)[8], int n) {
+    const bool b3 = n & 8, b2 = n & 4, b1 = n & 2;
+    float w4[4], w2[2];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w4[j] = (b3 ? v[j + 4] : v[j]) + __shfl_xor(b3 ? v[j] : v[j + 4], 8, 64);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) w2[j] = (b2 ? w4[j + 2] : w4[j]) + __shfl_xor(b2 ? w4[j] : w4[j + 2], 4, 64);
+    const float w1 = (b1 ? w2[1] : w2[0]) + __shfl_xor(b1 ? w2[0] : w2[1], 2, 64);
+    return w1 + __shfl_xor(w1, 1, 64);
+}
+
+// select v[(n >> 1) & 7] with the butterfly's lane bits (no shuffles)
+__device__ __forceinline__ float row16_xsel8(const float (&v)[8], int n) {
+    const bool b3 = n & 8, b2 = n & 4, b1 = n & 2;
+    float w4[4], w2[2];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w4[j] = b3 ? v[j + 4] : v[j];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) w2[j] = b2 ? w4[j + 2] : w4[j];
+    return b1 ? w2[1] : w2[0];
+}
+
+__device__ __forceinline__ void st2(float* p, float x, float y) { *reinterpret_cast<float2*>(p) = make_float2(x, y); }
+__device__ __forceinline__ float2 ld2(const float* p) { return *reinterpret_cast<const float2*>(p); }
+
+// Epilogue of one unit.  Lane (n, kq) holds output channels n0 + 16 mi + 4 kq + i (j = 4 mi + i < 8)
+// of its tile (outputs y[j][e] at (2 tr + (e >> 1), 2 tc + (e & 1))).  The 16 lanes of a row hold
+// 16 consecutive tiles of one or two tile rows, so a store of one output row is a 128-byte run.
+// red: 512 floats of LDS private to the epilogue.
+template <int EPI, bool V4>
+__device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y)[8][4], float* red, int b,
+                                              int tb, int n0, int tr, int tc, bool tvalid, int wave, int tid) {
+    const int lane = tid & 63, n = lane & 15, kq = lane >> 4;
+    const int HW = a.H * a.W;
+    const int h0 = 2 * tr, w0 = 2 * tc;
+    const bool okr1 = h0 + 1 < a.H, okc1 = w0 + 1 < a.W;
+    const bool vec = (a.W & 1) == 0;  // output pairs (h, w0..w0+1) are 8-byte aligned and complete
+    bool ok[4];
+    ok[0] = tvalid;
+    ok[1] = tvalid && okc1;
+    ok[2] = tvalid && okr1;
+    ok[3] = ok[1] && okr1;
+    const int pix0 = h0 * a.W + w0;
+    const int poff[4] = {0, 1, a.W, a.W + 1};
+    const int jsel = (n >> 1) & 7;                               // channel this lane reduces
+    const int cosel = 16 * (jsel >> 2) + 4 * kq + (jsel & 3);
+    if (EPI == EPI_FWD) {
+        // store y; per channel Chan statistics of the block: each wave sums about a shift K (the
+        // channel's first output in its row of lanes), reduced with the transposed butterfly
+        float* ob = a.out + ((int64_t)b * a.cout + n0) * HW + pix0;
+        float cnt = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cnt += ok[e] ? 1.f : 0.f;
+        float s1[8], s2[8], kv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float* o = ob + (int64_t)(16 * (j >> 2) + 4 * kq + (j & 3)) * HW;
+            const float* v = y[j];
+            if (vec) {
+                if (ok[0]) st2(o, v[0], v[1]);
+                if (ok[2]) st2(o + a.W, v[2], v[3]);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (ok[e]) o[poff[e]] = v[e];
+            }
+            kv[j] = __shfl(v[0], lane & 48, 64);
+            float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float dd = ok[e] ? v[e] - kv[j] : 0.f;
+                t1 += dd;
+                t2 = fmaf(dd, dd, t2);
+            }
+            s1[j] = t1;
+            s2[j] = t2;
+        }
+        const float T1 = row16_xsum8(s1, n), T2 = row16_xsum8(s2, n);
+        const float K = row16_xsel8(kv, n);
+        cnt = row16_sum(cnt);
+        if (!(n & 1)) {
+            float* d = red + (wave * 32 + cosel) * 3;
+            d[0] = T1; d[1] = T2; d[2] = K;
+        }
+        if (lane == 0) red[384 + wave] = cnt;  // valid outputs of the wave (all channels alike)
+        __syncthreads();
+        if (tid < 32) {
+            float nn = 0.f, mean = 0.f, m2 = 0.f;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const float nw = red[384 + w];
+                if (nw > 0.f) {
+                    const float* d = red + (w * 32 + tid) * 3;
+                    const float mw = d[2] + d[0] / nw, m2w = fmaxf(d[1] - d[0] * d[0] / nw, 0.f);
+                    const float nt = nn + nw, delta = mw - mean;
+                    mean += delta * nw / nt;
+                    m2 += m2w + delta * delta * nn * nw / nt;
+                    nn = nt;
+                }
+            }
+            a.part0[(int64_t)(n0 + tid) * a.nblk + tb] = nn * mean;
+            a.part1[(int64_t)(n0 + tid) * a.nblk + tb] = m2;
+            if (tid == 0 && n0 == 0) a.partn[tb] = nn;
+        }
+    } else if (EPI == EPI_BWD_STORE) {
+        float* ob = a.out + ((int64_t)b * a.cout + n0) * HW + pix0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float* o = ob + (int64_t)(16 * (j >> 2) + 4 * kq + (j & 3)) * HW;
+            const float* v = y[j];
+            if (vec) {
+#pragma unroll
+                for (int rr = 0; rr < 2; ++rr)
+                    if (ok[2 * rr]) {
+                        float* q = o + rr * a.W;
+                        float2 t = make_float2(v[2 * rr], v[2 * rr + 1]);
+                        if (a.accumulate) {
+                            const float2 p = ld2(q);
+                            t.x += p.x;
+                            t.y += p.y;
+                        }
+                        st2(q, t.x, t.y);
+                    }
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (ok[e]) {
+                        float* q = o + poff[e];
+                        *q = a.accumulate ? *q + v[e] : v[e];
+                    }
+            }
+        }
+    } else {
+        // data-gradient epilogues: dz through ReLU (and MaxPool / Dropout2d) of the producer, and the
+        // producer BN's backward sums (dz, dz * xhat) per channel
+        float sz[8], sx[8];
+        if (EPI == EPI_BWD_RELU) {
+            // all loads first (addresses clamped in bounds), then the arithmetic and the stores: one
+            // memory round trip per unit instead of one per channel
+            const int pixc = tvalid ? pix0 : 0;
+            const int row1 = ok[2] ? a.W : 0;
+            const float* yb = a.yprev + ((int64_t)b * a.cout + n0) * HW + pixc;
+            float* ob = a.out + ((int64_t)b * a.cout + n0) * HW + pix0;
+            float4 cf[8];
+            float yy[8][4];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int co = 16 * (j >> 2) + 4 * kq + (j & 3);
+                cf[j] = a.cf_out[n0 + co];
+                const float* yp = yb + (int64_t)co * HW;
+                if (vec) {
+                    const float2 p0 = ld2(yp), p1 = ld2(yp + row1);
+                    yy[j][0] = p0.x; yy[j][1] = p0.y; yy[j][2] = p1.x; yy[j][3] = p1.y;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) yy[j][e] = yp[ok[e] ? poff[e] : 0];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int co = 16 * (j >> 2) + 4 * kq + (j & 3);
+                float* op = ob + (int64_t)co * HW;
+                float dz[4], s_z = 0.f, s_x = 0.f;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    dz[e] = (ok[e] && fmaf(yy[j][e], cf[j].x, cf[j].y) > 0.f) ? y[j][e] : 0.f;
+                    s_z += dz[e];
+                    s_x = fmaf(dz[e], (yy[j][e] - cf[j].z) * cf[j].w, s_x);
+                }
+                if (vec) {
+                    if (ok[0]) st2(op, dz[0], dz[1]);
+                    if (ok[2]) st2(op + a.W, dz[2], dz[3]);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (ok[e]) op[poff[e]] = dz[e];
+                }
+                sz[j] = s_z;
+                sx[j] = s_x;
+            }
+        } else {  // EPI_BWD_POOL: the conv runs at the pooled resolution; dz lives at Hs x Ws
+            const int HWs = a.Hs * a.Ws;
+            const int soff0 = tvalid ? (2 * h0) * a.Ws + 2 * w0 : 0;  // loads clamped in bounds
+            const float* yb = a.yprev + ((int64_t)b * a.cout + n0) * HWs + soff0;
+            float* ob = a.out + ((int64_t)b * a.cout + n0) * HWs + (2 * h0) * a.Ws + 2 * w0;
+#pragma unroll
+            for (int half = 0; half < 4; ++half) {
+                // two channels' windows loaded together (one round trip per pair; registers)
+                float win[2][4][4];
+                float4 cf[2];
+                float dv[2];
+#pragma unroll
+                for (int jj = 0; jj < 2; ++jj) {
+                    const int j = 2 * half + jj;
+                    const int co = 16 * (j >> 2) + 4 * kq + (j & 3);
+                    cf[jj] = a.cf_out[n0 + co];
+                    dv[jj] = a.drop_out ? a.drop_out[(int64_t)b * a.cout + n0 + co] : 1.f;
+                    const float* yp = yb + (int64_t)co * HWs;
+                    if (V4) {  // host-checked: H, W even, Ws % 4 == 0: a tile's window is four 16-byte rows
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const float4 t = ld4(yp + r * a.Ws);
+                            win[jj][r][0] = t.x; win[jj][r][1] = t.y; win[jj][r][2] = t.z; win[jj][r][3] = t.w;
+                        }
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const int r0 = 2 * (e >> 1), c0 = 2 * (e & 1);
+                            const float* q = yp + (ok[e] ? r0 * a.Ws + c0 : 0);
+                            const int dc = ok[e] ? 1 : 0, dr = ok[e] ? a.Ws : 0;
+                            win[jj][r0][c0] = q[0];
+                            win[jj][r0][c0 + 1] = q[dc];
+                            win[jj][r0 + 1][c0] = q[dr];
+                            win[jj][r0 + 1][c0 + 1] = q[dr + dc];
+                        }
+                    }
+                }
+#pragma unroll
+                for (int jj = 0; jj < 2; ++jj) {
+                    const int j = 2 * half + jj;
+                    const int co = 16 * (j >> 2) + 4 * kq + (j & 3);
+                    float* op = ob + (int64_t)co * HWs;
+                    float dzw[4][4];
+                    float s_z = 0.f, s_x = 0.f;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int r0 = 2 * (e >> 1), c0 = 2 * (e & 1);
+                        const float y0 = win[jj][r0][c0], y1 = win[jj][r0][c0 + 1];
+                        const float y2 = win[jj][r0 + 1][c0], y3 = win[jj][r0 + 1][c0 + 1];
+                        const float4 k = cf[jj];
+                        const float q0 = fmaxf(fmaf(y0, k.x, k.y), 0.f), q1 = fmaxf(fmaf(y1, k.x, k.y), 0.f);
+                        const float q2 = fmaxf(fmaf(y2, k.x, k.y), 0.f), q3 = fmaxf(fmaf(y3, k.x, k.y), 0.f);
+                        // first maximum in window scan order, as torch's max_pool2d
+                        int arg = 0;
+                        float best = q0, ya = y0;
+                        if (q1 > best) { best = q1; arg = 1; ya = y1; }
+                        if (q2 > best) { best = q2; arg = 2; ya = y2; }
+                        if (q3 > best) { best = q3; arg = 3; ya = y3; }
+                        const float dd = (ok[e] && best > 0.f) ? y[j][e] * dv[jj] : 0.f;
+                        dzw[r0][c0] = arg == 0 ? dd : 0.f;
+                        dzw[r0][c0 + 1] = arg == 1 ? dd : 0.f;
+                        dzw[r0 + 1][c0] = arg == 2 ? dd : 0.f;
+                        dzw[r0 + 1][c0 + 1] = arg == 3 ? dd : 0.f;
+                        s_z += dd;
+                        s_x = fmaf(dd, (ya - k.z) * k.w, s_x);
+                    }
+                    if (V4) {
+                        if (tvalid)
+#pragma unroll
+                            for (int r = 0; r < 4; ++r)
+                                st4(op + r * a.Ws, make_float4(dzw[r][0], dzw[r][1], dzw[r][2], dzw[r][3]));
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            if (ok[e]) {
+                                const int r0 = 2 * (e >> 1), c0 = 2 * (e & 1);
+                                float* q = op + r0 * a.Ws + c0;
+                                q[0] = dzw[r0][c0];
+                                q[1] = dzw[r0][c0 + 1];
+                                q[a.Ws] = dzw[r0 + 1][c0];
+                                q[a.Ws + 1] = dzw[r0 + 1][c0 + 1];
+                            }
+                    }
+                    sz[j] = s_z;
+                    sx[j] = s_x;
+                }
+                __builtin_amdgcn_sched_barrier(0);  // keep the pairs' loads apart (registers)
+            }
+        }
+        const float tz = row16_xsum8(sz, n), tx = row16_xsum8(sx, n);
+        if (!(n & 1)) {
+            red[(wave * 32 + cosel) * 2] = tz;
+            red[(wave * 32 + cosel) * 2 + 1] = tx;
+        }
+        __syncthreads();
+        if (tid < 32) {
+            float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                s0 += red[(w * 32 + tid) * 2];
+                s1 += red[(w * 32 + tid) * 2 + 1];
+            }
+            a.part0[(int64_t)(n0 + tid) * a.nblk + tb] = s0;
+            a.part1[(int64_t)(n0 + tid) * a.nblk + tb] = s1;
+        }
+    }
+}
+
+// Persistent: each workgroup walks units u = it * G + (XCD-contiguous slot); unit = (64-tile block tb
+// of one sample, 32-channel output group cg).  The first K-chunk of the next unit is copied while the
+// last chunk of the current one is multiplied and during its epilogue.
+template <int PRO, int EPI, int CK, bool V4>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv_wino_kernel(ConvArgs a, WinoGeo g) {
+    constexpr int WSLOT = CK * WSP;           // floats of one wave's slot
+    constexpr int INF = 4 * WSLOT;            // input floats per buffer
+    constexpr int BUFF = INF + CK * 512;      // + transformed weights of the chunk
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int tid = threadIdx.x, lane = tid & 63, n = lane & 15, kq = lane >> 4;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int HW = a.H * a.W;
+    float* cft = smem + 2 * BUFF;             // [cin] float2 {s, t}
+    float* red = cft + 2 * a.cin;             // epilogue scratch (512 floats)
+    const unsigned lds0 = (unsigned)(uintptr_t)(lds_void*)smem;
+    if (PRO != PRO_RAW)
+        for (int c = tid; c < a.cin; c += 256) {
+            const float4 f = a.cf_in[c];
+            cft[2 * c] = f.x;
+            cft[2 * c + 1] = f.y;
+        }
+    const int nunits = a.B * g.BPS * g.ncg;
+    const int G = gridDim.x;
+    // XCD-contiguous slot of this workgroup inside a round (dispatch is round-robin over the 8 XCDs)
+    const int slot = (G & 7) ? (int)blockIdx.x : (int)(blockIdx.x & 7) * (G >> 3) + (int)(blockIdx.x >> 3);
+
+    struct Unit { int b, tb, cg, tw, tr_a, tc_a; };
+    auto unit_of = [&](int u) {
+        Unit x;
+        x.tb = u / g.ncg;
+        x.cg = u - x.tb * g.ncg;
+        x.b = x.tb / g.BPS;
+        x.tw = (x.tb - x.b * g.BPS) * 64 + wave * 16;  // the wave's first tile (within its sample)
+        x.tr_a = x.tw / g.TC;
+        x.tc_a = x.tw - x.tr_a * g.TC;
+        return x;
+    };
+    // Copies: per channel plane three 64-lane dword copies cover slot positions 0..143 (4 rows x WSW
+    // columns; the third uses lanes 0..15).  Lane offsets depend on the unit only (the channel is
+    // the buffer base); out-of-image positions get an out-of-range offset, which copies a 0.
+    unsigned voff[3];
+    auto plan_copies = [&](const Unit& x) {
+        const int segw = 2 * min(16, g.TC - x.tc_a) + 2;
+        const int rb0 = 2 * x.tr_a - 1, rb1 = 2 * x.tr_a + 1;
+        const int cb0 = 2 * x.tc_a - 1, cb1 = -segw - 1;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            const int pos = 64 * p + lane;
+            const int r = pos / WSW, cc = pos - r * WSW;
+            const bool s1 = cc >= segw;
+            const int grow = r + (s1 ? rb1 : rb0), gcol = cc + (s1 ? cb1 : cb0);
+            const bool ok = (unsigned)grow < (unsigned)a.H && (unsigned)gcol < (unsigned)a.W;
+            voff[p] = ok ? 4u * (unsigned)(grow * a.W + gcol) : 0x80000000u;
+        }
+    };
+    auto issue = [&](const Unit& x, int c0, int buf) {
+#if defined(WINO_KO) && (WINO_KO & 1)  // analysis builds only (tools/wino_ko.sh): no operand copies
+        return;
+#endif
+        const float* sb = a.src + ((int64_t)x.b * a.cin + c0) * HW;
+        const unsigned sl = lds0 + 4u * (unsigned)(buf * BUFF + wave * WSLOT);
+#pragma unroll
+        for (int cl = 0; cl < CK; ++cl) {
+            const __amdgpu_buffer_rsrc_t r = wrsrc(sb + (int64_t)cl * HW, 4 * HW);
+            bdma<false>(r, voff[0], sl + 4u * (unsigned)(cl * WSP));
+            bdma<false>(r, voff[1], sl + 4u * (unsigned)(cl * WSP + 64));
+            bdma<true>(r, voff[2], sl + 4u * (unsigned)(cl * WSP + 128));
+        }
+        const float* sw = wuniform(a.wpack + ((int64_t)x.cg * a.cin + c0) * 512);
+        const unsigned wl = lds0 + 4u * (unsigned)(buf * BUFF + INF);
+#pragma unroll
+        for (int j = 0; j < CK / 2; ++j) wdma<4>(sw, 4u * (unsigned)(j * 1024 + tid * 4), wl + 4u * (unsigned)(j * 1024 + wave * 256));
+    };
+
+    const int nchunk = a.cin / CK;
+    int u = slot;
+    Unit cur = unit_of(u < nunits ? u : 0);
+    if (u < nunits) {
+        plan_copies(cur);
+        issue(cur, 0, 0);
+    }
+    int kk = 0;  // chunks issued so far (buffer = kk & 1)
+    while (u < nunits) {
+        const int un = u + G;
+        const Unit nxt = unit_of(un < nunits ? un : u);
+        // this lane's tile of the current unit
+        const int len_a = min(16, g.TC - cur.tc_a);
+        const bool seg1 = n >= len_a;
+        const int tr = seg1 ? cur.tr_a + 1 : cur.tr_a, tc = seg1 ? n - len_a : cur.tc_a + n;
+        const bool tvalid = cur.tw + n < g.NTS;
+        const int pbase = wave * WSLOT + kq * WSP + (seg1 ? 2 * n + 2 : 2 * n);
+        // BN+ReLU operands: out-of-image patch rows / columns must be 0 after the prologue (the copy
+        // wrote raw 0s there); a factor per patch row / column, applied only in waves that touch the
+        // image border
+        float fr0 = 1.f, fr2 = 1.f, fr3 = 1.f, fc0 = 1.f, fc2 = 1.f, fc3 = 1.f;
+        bool border = false;
+        if (PRO != PRO_RAW) {
+            fr0 = tr > 0 ? 1.f : 0.f;
+            fr2 = 2 * tr + 1 < a.H ? 1.f : 0.f;
+            fr3 = 2 * tr + 2 < a.H ? 1.f : 0.f;
+            fc0 = tc > 0 ? 1.f : 0.f;
+            fc2 = 2 * tc + 1 < a.W ? 1.f : 0.f;
+            fc3 = 2 * tc + 2 < a.W ? 1.f : 0.f;
+            border = __builtin_amdgcn_readfirstlane(
+                         (int)(__ballot((fr0 * fr2 * fr3 * fc0 * fc2 * fc3) == 0.f) != 0)) != 0;
+        }
+        f32x4 acc[16][2];
+#pragma unroll
+        for (int x = 0; x < 16; ++x) {
+            acc[x][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+            acc[x][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        auto kloop = [&](auto btag) {
+            constexpr bool BRD = decltype(btag)::value;
+            for (int k = 0; k < nchunk; ++k, ++kk) {
+                const int c0 = k * CK;
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();  // chunk kk visible; chunk kk-1 fully consumed
+                if (k + 1 < nchunk) {
+                    issue(cur, c0 + CK, (kk + 1) & 1);
+                } else if (un < nunits) {
+                    plan_copies(nxt);
+                    issue(nxt, 0, (kk + 1) & 1);
+                }
+                const float* bi = smem + (kk & 1) * BUFF;
+                const float* bw = bi + INF;
+#pragma unroll
+                for (int s = 0; s < CK / 4; ++s) {
+                    const int cl = 4 * s + kq;
+                    float d[4][4];
+                    const float* pp = bi + pbase + 4 * s * WSP;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const f2 u0 = *reinterpret_cast<const f2*>(pp + r * WSW);
+                        const f2 u1 = *reinterpret_cast<const f2*>(pp + r * WSW + 2);
+                        d[r][0] = u0.x; d[r][1] = u0.y; d[r][2] = u1.x; d[r][3] = u1.y;
+                    }
+                    f32x4 av[2][4];
+#pragma unroll
+                    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            av[mi][q] = *reinterpret_cast<const f32x4*>(bw + (((cl * 4 + q) * 32) + 16 * mi + n) * 4);
+                    if (PRO != PRO_RAW) {
+                        const f2 st = *reinterpret_cast<const f2*>(cft + 2 * (c0 + cl));
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+#pragma unroll
+                            for (int c = 0; c < 4; ++c) d[r][c] = fmaxf(fmaf(d[r][c], st.x, st.y), 0.f);
+                        if constexpr (BRD) {
+#pragma unroll
+                            for (int c = 0; c < 4; ++c) {
+                                d[0][c] *= fr0;
+                                d[2][c] *= fr2;
+                                d[3][c] *= fr3;
+                            }
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                d[r][0] *= fc0;
+                                d[r][2] *= fc2;
+                                d[r][3] *= fc3;
+                            }
+                        }
+                    }
+                    // V = B^T d B (rows first, then columns): 32 additions
+                    float e_[4][4], v[16];
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        e_[0][c] = d[0][c] - d[2][c];
+                        e_[1][c] = d[1][c] + d[2][c];
+                        e_[2][c] = d[2][c] - d[1][c];
+                        e_[3][c] = d[1][c] - d[3][c];
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        v[4 * r + 0] = e_[r][0] - e_[r][2];
+                        v[4 * r + 1] = e_[r][1] + e_[r][2];
+                        v[4 * r + 2] = e_[r][2] - e_[r][1];
+                        v[4 * r + 3] = e_[r][1] - e_[r][3];
+                    }
+#pragma unroll
+                    for (int x = 0; x < 16; ++x)
+#pragma unroll
+                        for (int mi = 0; mi < 2; ++mi) acc[x][mi] = mfma16(av[mi][x >> 2][x & 3], v[x], acc[x][mi]);
+                }
+            }
+        };
+        if (border) kloop(std::true_type{});
+        else kloop(std::false_type{});
+
+        // ---- output transform Y = A^T M A: y[j][e] = output (2 tr + (e >> 1), 2 tc + (e & 1)) of
+        // channel j = 4 mi + i
+        float y[8][4];
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float s0[4], s1[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    s0[c] = acc[c][mi][i] + acc[4 + c][mi][i] + acc[8 + c][mi][i];
+                    s1[c] = acc[4 + c][mi][i] - acc[8 + c][mi][i] - acc[12 + c][mi][i];
+                }
+                y[4 * mi + i][0] = s0[0] + s0[1] + s0[2];
+                y[4 * mi + i][1] = s0[1] - s0[2] - s0[3];
+                y[4 * mi + i][2] = s1[0] + s1[1] + s1[2];
+                y[4 * mi + i][3] = s1[1] - s1[2] - s1[3];
+            }
+#if defined(WINO_KO) && (WINO_KO & 2)  // analysis builds only: no epilogue (one guarded store keeps y live)
+        {
+            float t = 0.f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) t += y[j][0] + y[j][1] + y[j][2] + y[j][3];
+            if (t == 1234.5f) a.out[tid] = t;
+        }
+#else
+        wino_epilogue<EPI, V4>(a, y, red, cur.b, cur.tb, cur.cg * 32, tr, tc, tvalid, wave, tid);
+#endif
+        u = un;
+        cur = nxt;
+    }
+}
+
+// U = G g G^T per (GEMM output channel m, GEMM input channel k), evaluated in float64.
+// flip: data-gradient GEMM of forward weights w[K][M][3][3] (g[m][k] = w[k][m] rotated 180 deg).
+__global__ void wino_pack_kernel(const float* __restrict__ w, float* __restrict__ u, int M, int K, int flip) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= M * K) return;
+    const int m = e / K, k = e - m * K;
+    double gg[3][3];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c)
+            gg[r][c] = flip ? (double)w[(((int64_t)k * M + m) * 3 + (2 - r)) * 3 + (2 - c)]
+                            : (double)w[(((int64_t)m * K + k) * 3 + r) * 3 + c];
+    double t[4][3];
+    for (int c = 0; c < 3; ++c) {
+        t[0][c] = gg[0][c];
+        t[1][c] = 0.5 * (gg[0][c] + gg[1][c] + gg[2][c]);
+        t[2][c] = 0.5 * (gg[0][c] - gg[1][c] + gg[2][c]);
+        t[3][c] = gg[2][c];
+    }
+    const int cgi = m >> 5, ml = m & 31;
+    float* dst = u + (((int64_t)cgi * K + k) * 4) * 128 + ml * 4;
+    for (int q = 0; q < 4; ++q) {
+        float4 o;
+        o.x = (float)t[q][0];
+        o.y = (float)(0.5 * (t[q][0] + t[q][1] + t[q][2]));
+        o.z = (float)(0.5 * (t[q][0] - t[q][1] + t[q][2]));
+        o.w = (float)t[q][2];
+        *reinterpret_cast<float4*>(dst + q * 128) = o;
+    }
+}
+
+}  // namespace
+
+// ====================================================================== host side
+static int wino_ck(int cin) { return cin % 8 == 0 ? 8 : 4; }
+
+bool wino_geometry(int B, int H, int W, int cin, int cout, WinoGeo* g) {
+    if (cout % 32 || cin % 4 || H < 1 || W < 31) return false;  // 16 tiles of a wave span <= 2 tile rows
+    WinoGeo r{};
+    r.TR = (H + 1) / 2;
+    r.TC = (W + 1) / 2;
+    r.NTS = r.TR * r.TC;
+    r.BPS = ceil_div(r.NTS, 64);
+    r.ncg = cout / 32;
+    if ((int64_t)B * r.BPS * r.ncg >= ((int64_t)1 << 31)) return false;
+    if ((int64_t)cin * H * W >= ((int64_t)1 << 30)) return false;
+    if ((int64_t)wino_ck(cin) * H * W + 4 * W + 64 >= ((int64_t)1 << 24)) return false;  // packed copy offsets
+    if (g) *g = r;
+    return true;
+}
+
+size_t wino_nblk(int B, int H, int W, int cin, int cout) {
+    WinoGeo g;
+    if (!wino_geometry(B, H, W, cin, cout, &g)) return 0;
+    return (size_t)B * g.BPS;
+}
+
+int launch_wino_pack(const float* w, float* u, int M, int K, int flip, hipStream_t s) {
+    PCX_CHECK_ARG(M % 32 == 0, "wino_pack: %d output channels (multiple of 32 required)", M);
+    const int n = M * K;
+    wino_pack_kernel<<<ceil_div(n, 256), 256, 0, s>>>(w, u, M, K, flip);
+    PCX_LAUNCH_CHECK("wino_pack_kernel");
+    return PCX_OK;
+}
+
+int launch_conv3x3_wino(int pro, int epi, ConvArgs a, hipStream_t s) {
+    WinoGeo g;
+    PCX_CHECK_ARG(wino_geometry(a.B, a.H, a.W, a.cin, a.cout, &g),
+                  "conv3x3_wino: unsupported shape (B %d, %dx%d, cin %d, cout %d)", a.B, a.H, a.W, a.cin, a.cout);
+    PCX_CHECK_ARG(a.nblk == a.B * g.BPS, "conv3x3_wino: partial buffer sized for %d tiles, need %d", a.nblk,
+                  a.B * g.BPS);
+    PCX_CHECK_ARG(pro == PRO_RAW || pro == PRO_BNRELU, "conv3x3_wino: prologue %d", pro);
+    if (epi == EPI_BWD_POOL)
+        PCX_CHECK_ARG(a.Hs >= 2 * a.H && a.Ws >= 2 * a.W, "conv3x3_wino: pooled source %dx%d for %dx%d", a.Hs, a.Ws,
+                      a.H, a.W);
+    const int ck = wino_ck(a.cin);
+    const size_t buff = (size_t)4 * ck * WSP + (size_t)ck * 512;
+    const size_t smem = (2 * buff + 2 * (size_t)a.cin + 512) * 4;
+    PCX_CHECK_ARG(smem <= 160 * 1024, "conv3x3_wino: %zu B of LDS", smem);
+    // persistent workgroups: two per CU (a multiple of 8, one XCD-contiguous run of units each round)
+    const int64_t units = (int64_t)a.B * g.BPS * g.ncg;
+    int64_t nwg = std::min<int64_t>(units, 2 * (int64_t)num_cus());
+    if (nwg >= 8) nwg &= ~(int64_t)7;
+    dim3 grid((unsigned)nwg);
+    // pooled data gradient with 16-byte source rows
+    const bool v4 = epi == EPI_BWD_POOL && (a.Ws & 3) == 0 && !(a.H & 1) && !(a.W & 1);
+#define PCX_WINO_CASE(P_, E_, CK_, V4_)                                                                 \
+    if (pro == P_ && epi == E_ && ck == CK_ && v4 == V4_) {                                             \
+        (void)hipFuncSetAttribute((const void*)conv_wino_kernel<P_, E_, CK_, V4_>,                      \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);               \
+        conv_wino_kernel<P_, E_, CK_, V4_><<<grid, 256, smem, s>>>(a, g);                               \
+        PCX_LAUNCH_CHECK("conv_wino_kernel");                                                           \
+        return PCX_OK;                                                                                  \
+    }
+#define PCX_WINO_CK(P_, E_, V4_) PCX_WINO_CASE(P_, E_, 8, V4_) PCX_WINO_CASE(P_, E_, 4, V4_)
+    PCX_WINO_CK(PRO_RAW, EPI_FWD, false)
+    PCX_WINO_CK(PRO_BNRELU, EPI_FWD, false)
+    PCX_WINO_CK(PRO_RAW, EPI_BWD_RELU, false)
+    PCX_WINO_CK(PRO_RAW, EPI_BWD_POOL, false)
+    PCX_WINO_CK(PRO_RAW, EPI_BWD_POOL, true)
+    PCX_WINO_CK(PRO_RAW, EPI_BWD_STORE, false)
+#undef PCX_WINO_CK
+#undef PCX_WINO_CASE
+    set_error("conv3x3_wino: unsupported combination (pro %d epi %d ck %d)", pro, epi, ck);
+    return PCX_EINVAL;
+}
+
+}  // namespace pcx

@@ -50,6 +50,18 @@ size_t conv3x3_nblk(int B, int H, int W, int cout);
 // Raw rows DMA'd into LDS (global_load_lds, double-buffered), the prologue applied at operand-read
 // time (conv_dma.hip).  Prologues PRO_RAW, PRO_BNRELU.
 int launch_conv3x3_dma(int pro, int epi, ConvArgs a, hipStream_t s);
+// Winograd F(2x2, 3x3) form of the same conv (conv_wino.hip): same ConvArgs / prologues /
+// epilogues, weights transformed by launch_wino_pack into U = G g G^T, packed
+// [cout / 32][cin][4][32][4].  Partials are per 64-tile block: nblk = wino_nblk().
+struct WinoGeo {
+    int TR, TC, NTS, BPS;  // tile rows / columns per sample, tiles per sample, 64-tile blocks per sample
+    int ncg;               // output-channel groups of 32
+};
+bool wino_geometry(int B, int H, int W, int cin, int cout, WinoGeo* g);
+size_t wino_nblk(int B, int H, int W, int cin, int cout);
+// flip = 0: forward weights w[M][K][3][3]; flip = 1: data gradient of forward weights w[K][M][3][3]
+int launch_wino_pack(const float* w, float* u, int M, int K, int flip, hipStream_t s);
+int launch_conv3x3_wino(int pro, int epi, ConvArgs a, hipStream_t s);
 // materialised block tail x = drop * maxpool2(relu(y*s + t)) (feeds PRO_RAW convs)
 int launch_bn_relu_pool(const float* y, const float4* cf, const float* drop, float* x, int B, int C,
                         int Hs, int Ws, hipStream_t s);

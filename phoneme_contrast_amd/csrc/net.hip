@@ -58,9 +58,13 @@ int build_small(Plan& p) {
             L.xp = p.carve(nm, (size_t)B * L.cin * L.H * L.W * 4);
         }
         if (l >= 2) {
-            L.wp = p.carve("wp", (size_t)9 * L.cin * L.cout * 4);
-            L.wpd = p.carve("wpd", (size_t)9 * L.cin * L.cout * 4);
-            L.nblk = (int)conv3x3_nblk(B, L.H, L.W, L.cout);
+            L.wino = wino_geometry(B, L.H, L.W, L.cin, L.cout, nullptr) &&
+                     wino_geometry(B, L.H, L.W, L.cout, L.cin, nullptr);
+            L.wu = p.carve("wu", (size_t)16 * L.cin * L.cout * 4);
+            L.wud = p.carve("wud", (size_t)16 * L.cin * L.cout * 4);
+            // the data gradient's tile blocks are the forward's (same H x W), so one nblk serves both
+            L.nblk = L.wino ? (int)wino_nblk(B, L.H, L.W, L.cin, L.cout)
+                            : (int)std::max(conv3x3_nblk(B, L.H, L.W, L.cout), conv3x3_nblk(B, L.H, L.W, L.cin));
             PCX_CHECK_ARG(wgrad_s_geometry(B, L.H, L.W, L.cin, L.cout, &L.wg),
                           "PhonemeNet: no weight-gradient geometry for layer %d (%dx%d)", l, L.H, L.W);
             wg = std::max(wg, (size_t)L.wg.nslice * L.cout * L.cin * 9);
@@ -125,14 +129,14 @@ int small_forward(const Plan& p, const float* const* P, float* const* bnstat, in
         for (int i = 0; i < 3; ++i) dmask[i] = drop[i];
     float* part = at<float>(ws, p.stat_part);
 
-    auto finalize = [&](int l) {
+    auto finalize = [&](int l, int nblk) {
         const Layer& L = p.L[l];
         BnFwdArgs f{};
         f.C = L.cout;
-        f.nblk = L.nblk;
+        f.nblk = nblk;
         f.part0 = part;
-        f.part1 = part + (size_t)L.cout * L.nblk;
-        f.partn = part + (size_t)2 * L.cout * L.nblk;
+        f.part1 = part + (size_t)L.cout * nblk;
+        f.partn = part + (size_t)2 * L.cout * nblk;
         f.gamma = P[p_bn_g(l)];
         f.beta = P[p_bn_b(l)];
         f.bias = P[p_conv_b(l)];
@@ -161,24 +165,25 @@ int small_forward(const Plan& p, const float* const* P, float* const* bnstat, in
         c.nblk = L.nblk;
         c.rows_per_blk = p.conv1_rows;
         { Scope sc(&p.prof, s, "conv1_fwd", 1); RC(launch_conv1_fwd(c, s)); }
-        RC(finalize(1));
+        RC(finalize(1, L.nblk));
     }
     for (int l = 2; l <= 6; ++l) {
         const Layer& L = p.L[l];
         const Layer& Lp = p.L[l - 1];
-        RC(launch_pack_fwd(P[p_conv_w(l)], at<float>(ws, L.wp), L.cout, L.cin, s));
+        if (L.wino) RC(launch_wino_pack(P[p_conv_w(l)], at<float>(ws, L.wu), L.cout, L.cin, 0, s));
+        else RC(launch_pack_fwd(P[p_conv_w(l)], at<float>(ws, L.wu), L.cout, L.cin, s));
         ConvArgs c{};
         c.B = B; c.H = L.H; c.W = L.W; c.cin = L.cin; c.cout = L.cout;
         c.src = at<float>(ws, Lp.y);
         c.cf_in = at<float4>(ws, Lp.cf);
         c.drop_in = L.pooled_in ? dmask[L.drop_idx] : nullptr;
         c.srcH = L.srcH; c.srcW = L.srcW;
-        c.wpack = at<float>(ws, L.wp);
+        c.wpack = at<float>(ws, L.wu);
         c.out = at<float>(ws, L.y);
         c.part0 = part;
         c.part1 = part + (size_t)L.cout * L.nblk;
         c.partn = part + (size_t)2 * L.cout * L.nblk;
-        c.nblk = L.nblk;
+        c.nblk = L.wino ? L.nblk : (int)conv3x3_nblk(B, L.H, L.W, L.cout);
         int pro = PRO_BNRELU;
         if (L.pooled_in) {  // block tail materialised once; the conv and its wgrad read it raw
             Scope sc(&p.prof, s, "bn_relu_pool", l);
@@ -190,9 +195,9 @@ int small_forward(const Plan& p, const float* const* P, float* const* bnstat, in
         }
         {
             Scope sc(&p.prof, s, "conv_fwd", l);
-            RC(launch_conv3x3_dma(pro, EPI_FWD, c, s));
+            RC(L.wino ? launch_conv3x3_wino(pro, EPI_FWD, c, s) : launch_conv3x3_dma(pro, EPI_FWD, c, s));
         }
-        RC(finalize(l));
+        RC(finalize(l, c.nblk));
     }
     // head: attention + mean pool on x6 = Dropout2d(ReLU(BN6(y6)))
     const int ia = 24, ip = p.cfg.use_attention ? 26 : 24;
@@ -342,7 +347,8 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
         }
         // ---- data gradient -> dz of the previous BN (through ReLU / MaxPool / Dropout2d)
         {
-            RC(launch_pack_dgrad(P[p_conv_w(l)], at<float>(ws, L.wpd), L.cout, L.cin, s));
+            if (L.wino) RC(launch_wino_pack(P[p_conv_w(l)], at<float>(ws, L.wud), L.cin, L.cout, 1, s));
+            else RC(launch_pack_dgrad(P[p_conv_w(l)], at<float>(ws, L.wud), L.cout, L.cin, s));
             float* dzp = at<float>(ws, Lp.dz);
             if (L.pooled_in && ((L.srcH & 1) || (L.srcW & 1)))
                 RC(hip_status_ok(hipMemsetAsync(dzp, 0, (size_t)B * Lp.cout * L.srcH * L.srcW * 4, s),
@@ -354,20 +360,20 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
             c.cf_in = at<float4>(ws, L.cfb);
             c.src = at<float>(ws, p.dyb);  // dy = BN backward of (dz, y), materialised by the weight gradient
             c.srcH = L.H; c.srcW = L.W;
-            c.wpack = at<float>(ws, L.wpd);
+            c.wpack = at<float>(ws, L.wud);
             c.out = dzp;
             c.yprev = at<float>(ws, Lp.y);
             c.cf_out = at<float4>(ws, Lp.cf);
             c.drop_out = L.pooled_in ? dmask[L.drop_idx] : nullptr;
             c.Hs = L.srcH; c.Ws = L.srcW;
-            const int nblk = (int)conv3x3_nblk(B, L.H, L.W, L.cin);
+            const int nblk = L.wino ? L.nblk : (int)conv3x3_nblk(B, L.H, L.W, L.cin);
             c.part0 = part;
             c.part1 = part + (size_t)L.cin * nblk;
             c.nblk = nblk;
             {
                 Scope sc(&p.prof, s, "conv_dgrad", l);
                 const int epi = L.pooled_in ? EPI_BWD_POOL : EPI_BWD_RELU;
-                RC(launch_conv3x3_dma(PRO_RAW, epi, c, s));
+                RC(L.wino ? launch_conv3x3_wino(PRO_RAW, epi, c, s) : launch_conv3x3_dma(PRO_RAW, epi, c, s));
             }
             RC(bwd_finalize(l - 1, nblk, (double)B * Lp.H * Lp.W));
         }

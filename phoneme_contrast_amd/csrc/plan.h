@@ -92,9 +92,11 @@ struct Layer {  // one 3x3 conv of the trunk (L = 1..6)
     int srcH, srcW;        // resolution of the tensor its prologue reads
     bool pooled_in;        // prologue includes MaxPool2 + Dropout2d
     int drop_idx;          // dropout layer feeding its input (pooled_in) or -1
-    size_t y, dz, cf, cfb, wp, wpd;  // workspace offsets
+    size_t y, dz, cf, cfb, wu, wud;  // workspace offsets (wu / wud: Winograd weights, forward / data gradient)
     size_t xp;             // pooled_in: materialised input drop * maxpool2(relu(bn(y_prev)))
     int nblk;              // forward statistics tiles
+    bool wino;             // Winograd conv (W >= 31); else the direct LDS-DMA conv (wu / wud then hold
+                           // the [9][cin][cout] / flipped [9][cout][cin] packings)
     WgradArgs wg;          // weight-gradient geometry
 };
 
