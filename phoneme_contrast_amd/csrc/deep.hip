@@ -11,6 +11,7 @@
 // running mean) and the block outputs are kept in the workspace; BN statistics are reduced in
 // float64 by the same finalisers as cnn_small.  Convolutions run on the general implicit-GEMM
 // MFMA kernel (convg.hip); BN / ReLU / residual / dropout are elementwise passes.
+#include <algorithm>
 #include "plan.h"
 
 namespace pcx {
@@ -119,9 +120,11 @@ int build_deep(Plan& p) {
         *w32 = route && (w >= 50 ? wgrad_s_geometry(B, h, w, ci, co, wga) : wgrad_w32_geometry(B, h, w, ci, co, wga));
         *nblk = 0;
         if (*fwd) {
-            *nblk = (int)std::max(conv3x3_nblk(B, h, w, co), conv3x3_nblk(B, h, w, ci));
+            // the Winograd conv takes the layers whose rows are >= 31 columns wide (its own tile blocks)
+            *nblk = (int)std::max({conv3x3_nblk(B, h, w, co), conv3x3_nblk(B, h, w, ci), wino_nblk(B, h, w, ci, co),
+                                   wino_nblk(B, h, w, co, ci)});
             stat = std::max(stat, (size_t)2 * std::max(ci, co) * (*nblk) + *nblk);
-            wpk = std::max(wpk, (size_t)9 * ci * co);
+            wpk = std::max(wpk, (size_t)16 * ci * co);
         }
         if (*w32) wg = std::max(wg, (size_t)wga->nslice * co * ci * 9);
     };
@@ -248,18 +251,23 @@ int conv_bn_fwd(const Ctx& c, const char* label, int layer, const float* x, int 
     f.C = cout;
     if (dma_nblk) {  // stride-1 3x3 on the LDS-DMA conv: its epilogue writes the BN partials
         float* wp = c.w<float>(c.d.wpk);
-        RC(launch_pack_fwd(wgt, wp, cout, cin, c.s));
+        const bool wino = wino_geometry(c.p.B, OH, OW, cin, cout, nullptr);
+        if (wino) RC(launch_wino_pack(wgt, wp, cout, cin, 0, c.s));
+        else RC(launch_pack_fwd(wgt, wp, cout, cin, c.s));
         ConvArgs a{};
         a.B = c.p.B; a.H = OH; a.W = OW; a.cin = cin; a.cout = cout;
         a.src = x;
         a.srcH = IH; a.srcW = IW;
         a.wpack = wp;
         a.out = y;
-        a.nblk = (int)conv3x3_nblk(c.p.B, OH, OW, cout);
+        a.nblk = wino ? (int)wino_nblk(c.p.B, OH, OW, cin, cout) : (int)conv3x3_nblk(c.p.B, OH, OW, cout);
         a.part0 = part;
         a.part1 = part + (size_t)cout * a.nblk;
         a.partn = part + (size_t)2 * cout * a.nblk;
-        { Scope sc(&c.p.prof, c.s, label, layer); RC(launch_conv3x3_dma(PRO_RAW, EPI_FWD, a, c.s)); }
+        {
+            Scope sc(&c.p.prof, c.s, label, layer);
+            RC(wino ? launch_conv3x3_wino(PRO_RAW, EPI_FWD, a, c.s) : launch_conv3x3_dma(PRO_RAW, EPI_FWD, a, c.s));
+        }
         ns = a.nblk;
         f.part0 = a.part0;
         f.part1 = a.part1;
@@ -353,7 +361,9 @@ int conv_dgrad(const Ctx& c, int layer, const float* dy, int cout, int OH, int O
                const void* dyn = nullptr) {
     if (dma) {  // stride-1 3x3: the LDS-DMA conv on flipped weights, plain store / accumulate
         float* wp = c.w<float>(c.d.wpk);
-        RC(launch_pack_dgrad(wgt, wp, cout, cin, c.s));
+        const bool wino = wino_geometry(c.p.B, IH, IW, cout, cin, nullptr);
+        if (wino) RC(launch_wino_pack(wgt, wp, cin, cout, 1, c.s));
+        else RC(launch_pack_dgrad(wgt, wp, cout, cin, c.s));
         ConvArgs a{};
         a.B = c.p.B; a.H = IH; a.W = IW; a.cin = cout; a.cout = cin;
         a.src = dy;
@@ -361,10 +371,10 @@ int conv_dgrad(const Ctx& c, int layer, const float* dy, int cout, int OH, int O
         a.wpack = wp;
         a.out = dx;
         a.accumulate = accumulate;
-        a.nblk = (int)conv3x3_nblk(c.p.B, IH, IW, cin);
+        a.nblk = wino ? (int)wino_nblk(c.p.B, IH, IW, cout, cin) : (int)conv3x3_nblk(c.p.B, IH, IW, cin);
         a.part0 = a.part1 = c.w<float>(c.d.stat);
         Scope sc(&c.p.prof, c.s, "conv_dgrad", layer);
-        return launch_conv3x3_dma(PRO_RAW, EPI_BWD_STORE, a, c.s);
+        return wino ? launch_conv3x3_wino(PRO_RAW, EPI_BWD_STORE, a, c.s) : launch_conv3x3_dma(PRO_RAW, EPI_BWD_STORE, a, c.s);
     }
     ConvGArgs a{};
     a.mode = 1;
