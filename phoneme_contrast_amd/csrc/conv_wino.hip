@@ -488,14 +488,71 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
             border = __builtin_amdgcn_readfirstlane(
                          (int)(__ballot((fr0 * fr2 * fr3 * fc0 * fc2 * fc3) == 0.f) != 0)) != 0;
         }
-        f32x4 acc[16][2];
-#pragma unroll
-        for (int x = 0; x < 16; ++x) {
-            acc[x][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-            acc[x][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
+        f32x4 acc[16][2];  // the unit's first K-step starts the sums from 0 (no zeroing pass)
         auto kloop = [&](auto btag) {
             constexpr bool BRD = decltype(btag)::value;
+            // zero-start first K-step (not on the border copy / the pooled epilogue: registers)
+            constexpr bool PEEL = !BRD && EPI != EPI_BWD_POOL;
+            // one K-step (4 input channels) on operands in LDS
+            auto kstep = [&](const float* bi, const float* bw, int s, int c0, auto ftag) {
+                constexpr bool FIRST = decltype(ftag)::value;
+                    const int cl = 4 * s + kq;
+                float d[4][4];
+                const float* pp = bi + pbase + 4 * s * WSP;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const f2 u0 = *reinterpret_cast<const f2*>(pp + r * WSW);
+                    const f2 u1 = *reinterpret_cast<const f2*>(pp + r * WSW + 2);
+                    d[r][0] = u0.x; d[r][1] = u0.y; d[r][2] = u1.x; d[r][3] = u1.y;
+                }
+                f32x4 av[2][4];
+#pragma unroll
+                for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        av[mi][q] = *reinterpret_cast<const f32x4*>(bw + (((cl * 4 + q) * 32) + 16 * mi + n) * 4);
+                if (PRO != PRO_RAW) {
+                    const f2 st = *reinterpret_cast<const f2*>(cft + 2 * (c0 + cl));
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) d[r][c] = fmaxf(fmaf(d[r][c], st.x, st.y), 0.f);
+                    if constexpr (BRD) {
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) {
+                            d[0][c] *= fr0;
+                            d[2][c] *= fr2;
+                            d[3][c] *= fr3;
+                        }
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            d[r][0] *= fc0;
+                            d[r][2] *= fc2;
+                            d[r][3] *= fc3;
+                        }
+                    }
+                }
+                // V = B^T d B (rows first, then columns): 32 additions
+                float e_[4][4], v[16];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    e_[0][c] = d[0][c] - d[2][c];
+                    e_[1][c] = d[1][c] + d[2][c];
+                    e_[2][c] = d[2][c] - d[1][c];
+                    e_[3][c] = d[1][c] - d[3][c];
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    v[4 * r + 0] = e_[r][0] - e_[r][2];
+                    v[4 * r + 1] = e_[r][1] + e_[r][2];
+                    v[4 * r + 2] = e_[r][2] - e_[r][1];
+                    v[4 * r + 3] = e_[r][1] - e_[r][3];
+                }
+#pragma unroll
+                for (int x = 0; x < 16; ++x)
+#pragma unroll
+                    for (int mi = 0; mi < 2; ++mi) acc[x][mi] = mfma16(av[mi][x >> 2][x & 3], v[x], FIRST ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[x][mi]);
+            };
             for (int k = 0; k < nchunk; ++k, ++kk) {
                 const int c0 = k * CK;
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -508,68 +565,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
                 }
                 const float* bi = smem + (kk & 1) * BUFF;
                 const float* bw = bi + INF;
+                if (PEEL && k == 0) kstep(bi, bw, 0, c0, std::true_type{});
+                else kstep(bi, bw, 0, c0, std::false_type{});
 #pragma unroll
-                for (int s = 0; s < CK / 4; ++s) {
-                    const int cl = 4 * s + kq;
-                    float d[4][4];
-                    const float* pp = bi + pbase + 4 * s * WSP;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const f2 u0 = *reinterpret_cast<const f2*>(pp + r * WSW);
-                        const f2 u1 = *reinterpret_cast<const f2*>(pp + r * WSW + 2);
-                        d[r][0] = u0.x; d[r][1] = u0.y; d[r][2] = u1.x; d[r][3] = u1.y;
-                    }
-                    f32x4 av[2][4];
-#pragma unroll
-                    for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-                        for (int q = 0; q < 4; ++q)
-                            av[mi][q] = *reinterpret_cast<const f32x4*>(bw + (((cl * 4 + q) * 32) + 16 * mi + n) * 4);
-                    if (PRO != PRO_RAW) {
-                        const f2 st = *reinterpret_cast<const f2*>(cft + 2 * (c0 + cl));
-#pragma unroll
-                        for (int r = 0; r < 4; ++r)
-#pragma unroll
-                            for (int c = 0; c < 4; ++c) d[r][c] = fmaxf(fmaf(d[r][c], st.x, st.y), 0.f);
-                        if constexpr (BRD) {
-#pragma unroll
-                            for (int c = 0; c < 4; ++c) {
-                                d[0][c] *= fr0;
-                                d[2][c] *= fr2;
-                                d[3][c] *= fr3;
-                            }
-#pragma unroll
-                            for (int r = 0; r < 4; ++r) {
-                                d[r][0] *= fc0;
-                                d[r][2] *= fc2;
-                                d[r][3] *= fc3;
-                            }
-                        }
-                    }
-                    // V = B^T d B (rows first, then columns): 32 additions
-                    float e_[4][4], v[16];
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) {
-                        e_[0][c] = d[0][c] - d[2][c];
-                        e_[1][c] = d[1][c] + d[2][c];
-                        e_[2][c] = d[2][c] - d[1][c];
-                        e_[3][c] = d[1][c] - d[3][c];
-                    }
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        v[4 * r + 0] = e_[r][0] - e_[r][2];
-                        v[4 * r + 1] = e_[r][1] + e_[r][2];
-                        v[4 * r + 2] = e_[r][2] - e_[r][1];
-                        v[4 * r + 3] = e_[r][1] - e_[r][3];
-                    }
-#pragma unroll
-                    for (int x = 0; x < 16; ++x)
-#pragma unroll
-                        for (int mi = 0; mi < 2; ++mi) acc[x][mi] = mfma16(av[mi][x >> 2][x & 3], v[x], acc[x][mi]);
-                }
+                for (int s = 1; s < CK / 4; ++s) kstep(bi, bw, s, c0, std::false_type{});
             }
         };
-        if (border) kloop(std::true_type{});
+        if (border || EPI == EPI_BWD_POOL) {
+#pragma unroll
+            for (int x = 0; x < 16; ++x) {
+                acc[x][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+                acc[x][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+            if (border) kloop(std::true_type{});
+            else kloop(std::false_type{});
+        }
         else kloop(std::false_type{});
 
         // ---- output transform Y = A^T M A: y[j][e] = output (2 tr + (e >> 1), 2 tc + (e & 1)) of

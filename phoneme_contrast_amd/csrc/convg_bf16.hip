@@ -495,7 +495,20 @@ Conv2dNhwc conv2d_nhwc(int mode, int precision, int B, int cin, int cout, int IH
     if (mode != 0) r.dyb = (pcx::nhwc_bytes(B, cout, OH, OW) + 255) / 256 * 256;
     return r;
 }
+// fp32 stride-1 3x3 forward / data gradient with rows >= 31 columns: the Winograd conv (conv_wino.hip),
+// as in the networks; workspace = transformed weights + the forward's statistics partials
+bool conv2d_wino(int mode, int precision, int B, int cin, int cout, int IH, int IW, int k, int stride, int pad) {
+    if (precision || mode == 2 || k != 3 || stride != 1 || pad != 1) return false;
+    return mode == 0 ? pcx::wino_geometry(B, IH, IW, cin, cout, nullptr) : pcx::wino_geometry(B, IH, IW, cout, cin, nullptr);
+}
+size_t conv2d_wino_bytes(int B, int cin, int cout, int H, int W) {
+    const size_t nblk = pcx::wino_nblk(B, H, W, cin, cout);
+    return ((size_t)16 * cin * cout * 4 + 255) / 256 * 256 + ((2 * (size_t)std::max(cin, cout) + 1) * nblk * 4 + 255) / 256 * 256;
+}
 size_t conv2d_base_bytes(int mode, int precision, int B, int cin, int cout, int OH, int OW, int k) {
+    if (mode != 2 && conv2d_wino(mode, precision, B, cin, cout, OH, OW, k, 1, 1))
+        return std::max(conv2d_wino_bytes(B, cin, cout, OH, OW),
+                        (pcx::convg_wpack_bytes(mode, cin, cout, k) + 255) / 256 * 256);
     if (mode != 2)
         return ((precision ? pcx::convg_bf16_wpack_bytes(mode, cin, cout, k) : pcx::convg_wpack_bytes(mode, cin, cout, k)) +
                 255) / 256 * 256;
@@ -528,6 +541,28 @@ extern "C" int pcx_conv2d(int mode, int precision, int B, int cin, int cout, int
                   "pcx_conv2d: output %dx%d inconsistent with input %dx%d, k %d, stride %d, pad %d", OH, OW, IH, IW,
                   k, stride, pad);
     PCX_CHECK_ARG(out && (mode == 2 ? (x && dy) : mode == 1 ? (w && dy) : (x && w)), "pcx_conv2d: NULL operand");
+    if (conv2d_wino(mode, precision, B, cin, cout, IH, IW, k, stride, pad)) {
+        const size_t need = conv2d_wino_bytes(B, cin, cout, IH, IW);
+        PCX_CHECK_ARG(ws && ws_bytes >= need, "pcx_conv2d: needs %zu workspace bytes, got %zu", need, ws_bytes);
+        float* u = static_cast<float*>(ws);
+        float* part = u + ((size_t)16 * cin * cout * 4 + 255) / 256 * 64;
+        ConvArgs c{};
+        c.B = B; c.H = IH; c.W = IW;
+        c.cin = mode == 0 ? cin : cout;
+        c.cout = mode == 0 ? cout : cin;
+        c.src = mode == 0 ? x : dy;
+        c.srcH = IH; c.srcW = IW;
+        c.wpack = u;
+        c.out = out;
+        c.accumulate = accumulate;
+        c.nblk = (int)wino_nblk(B, IH, IW, c.cin, c.cout);
+        c.part0 = part;
+        c.part1 = part + (size_t)c.cout * c.nblk;
+        c.partn = part + (size_t)2 * c.cout * c.nblk;
+        const int rc = launch_wino_pack(w, u, c.cout, c.cin, mode, stream);
+        if (rc != PCX_OK) return rc;
+        return launch_conv3x3_wino(PRO_RAW, mode == 0 ? EPI_FWD : EPI_BWD_STORE, c, stream);
+    }
     ConvGArgs a{};
     a.mode = mode;
     a.B = B; a.cin = cin; a.cout = cout;

@@ -1,5 +1,6 @@
-"""Kernel-level parity of the cnn_deep convolution engine (pcx_conv2d, convg.hip / convg_bf16.hip)
-against float64 torch: forward, data gradient (incl. the stride-2 parity classes) and weight
+"""Kernel-level parity of the convolution engines behind pcx_conv2d (convg.hip / convg_bf16.hip /
+convn.hip, and for fp32 stride-1 3x3 forward / data gradient with rows >= 31 columns the Winograd
+F(2x2,3x3) conv of conv_wino.hip, which the networks run) against float64 torch: forward, data gradient (incl. the stride-2 parity classes) and weight
 gradient at the layer shapes of PhonemeNetDeep (reference src/models/phoneme_cnn.py:146-304) and at
 ragged ones.  precision 1 (bf16) is compared with the float64 result on operands rounded to bf16
 first: products of bf16 values are exact in float32, so both precisions are held to the same
@@ -25,6 +26,11 @@ SHAPES = [  # B, cin, cout, IH, IW, k, stride, pad
     (2, 128, 256, 10, 50, 3, 2, 1),
     (2, 256, 256, 5, 25, 3, 1, 1),
     (2, 256, 512, 5, 25, 1, 2, 0),
+    # Winograd conv (fp32): cnn_small layer shapes, odd width (T = 201), ragged odd height / width
+    (3, 32, 32, 40, 201, 3, 1, 1),
+    (2, 64, 32, 20, 100, 3, 1, 1),
+    (2, 32, 128, 10, 50, 3, 1, 1),
+    (5, 128, 64, 9, 33, 3, 1, 1),
 ]
 
 
