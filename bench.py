@@ -355,6 +355,10 @@ def main():
         roof["algorithmic_flops_per_launch"] = fl
         roof["algorithmic_bytes_per_launch"] = by
         roof["avg_launch_ms"] = round(avg_s * 1000.0, 4)
+    if roof is not None and dom.startswith(("conv_fwd_L", "conv_dgrad_L")) and not deep:
+        # cnn_small's 3x3 convs run Winograd F(2x2,3x3): 4/9 of the direct multiplies are executed
+        roof["executed_flops_per_launch"] = fl * 4 // 9
+        roof["executed_frac"] = round(roof["frac"] * 4 / 9, 4)
     sf, sb = deep_step_cost(B, F, T, D) if deep else step_cost(B, F, T, D)
     step_roof = {"flops_per_step": sf, "bytes_per_step": sb,
                  "mfma_fraction": round(sf / (el / args.steps) / (peak * 1e12), 4),
@@ -398,6 +402,10 @@ def main():
                    "embedding_dim": D, "parallelism": f"dp{world}",
                    "allreduce": None if world == 1 else f"{len(bucketer.buckets(next(iter(model._plans.values()))))} "
                                                         "RCCL buckets behind the backward"},
+        "conv_algorithms": None if deep else {
+            "conv_fwd / conv_dgrad L2-L6": "Winograd F(2x2,3x3) on fp32 MFMA (16 multiplies per 2x2 outputs: "
+                                           "4/9 of the direct conv's; exact fp32 arithmetic)",
+            "wgrad L2-L6": "direct implicit GEMM on fp32 MFMA (pixel streams)"},
         "roofline": roof,
         "step_roofline": step_roof,
         "cpu_baseline": cpu,

@@ -17,6 +17,7 @@ FWD = [f"conv_fwd_L{l}" for l in range(2, 7)]
 DGRAD = [f"conv_dgrad_L{l}" for l in range(6, 1, -1)]
 # kernel family (name up to '<' / '(') -> layer labels in per-step dispatch order
 ORDER = {
+    "conv_wino_kernel": FWD + DGRAD,  # Winograd conv (every cnn_small layer at W >= 31)
     "conv3x3_dma_kernel": FWD + DGRAD,
     "wgrad_s_kernel": [f"wgrad_L{l}" for l in range(6, 1, -1)],
     "bn_relu_pool_kernel": ["bn_relu_pool_L3", "bn_relu_pool_L5"],
