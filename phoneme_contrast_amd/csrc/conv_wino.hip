@@ -41,6 +41,15 @@ typedef __attribute__((address_space(3))) void lds_void;
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 
+// n / d for 0 <= n < 2^22 with inv = 1 / d (float): one correction step makes it exact
+__device__ __forceinline__ int wdiv(int n, int d, float inv) {
+    int q = (int)((float)n * inv);
+    const int r = n - q * d;
+    q += r >= d ? 1 : 0;
+    q -= r < 0 ? 1 : 0;
+    return q;
+}
+
 __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -187,10 +196,11 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
                 const float nw = red[384 + w];
                 if (nw > 0.f) {
                     const float* d = red + (w * 32 + tid) * 3;
-                    const float mw = d[2] + d[0] / nw, m2w = fmaxf(d[1] - d[0] * d[0] / nw, 0.f);
-                    const float nt = nn + nw, delta = mw - mean;
-                    mean += delta * nw / nt;
-                    m2 += m2w + delta * delta * nn * nw / nt;
+                    const float rw = __builtin_amdgcn_rcpf(nw);  // 1-ulp reciprocals (statistics)
+                    const float mw = d[2] + d[0] * rw, m2w = fmaxf(d[1] - d[0] * d[0] * rw, 0.f);
+                    const float nt = nn + nw, delta = mw - mean, f = nw * __builtin_amdgcn_rcpf(nt);
+                    mean += delta * f;
+                    m2 += m2w + delta * delta * nn * f;
                     nn = nt;
                 }
             }
@@ -409,13 +419,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     const int slot = (G & 7) ? (int)blockIdx.x : (int)(blockIdx.x & 7) * (G >> 3) + (int)(blockIdx.x >> 3);
 
     struct Unit { int b, tb, cg, tw, tr_a, tc_a; };
+    // (wave-uniform divisions by float reciprocals: a few VALU instead of ~30 per integer division)
     auto unit_of = [&](int u) {
         Unit x;
-        x.tb = u / g.ncg;
+        x.tb = wdiv(u, g.ncg, g.inv_ncg);
         x.cg = u - x.tb * g.ncg;
-        x.b = x.tb / g.BPS;
+        x.b = wdiv(x.tb, g.BPS, g.inv_BPS);
         x.tw = (x.tb - x.b * g.BPS) * 64 + wave * 16;  // the wave's first tile (within its sample)
-        x.tr_a = x.tw / g.TC;
+        x.tr_a = wdiv(x.tw, g.TC, g.inv_TC);
         x.tc_a = x.tw - x.tr_a * g.TC;
         return x;
     };
@@ -553,7 +564,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
 #pragma unroll
                     for (int mi = 0; mi < 2; ++mi) acc[x][mi] = mfma16(av[mi][x >> 2][x & 3], v[x], FIRST ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[x][mi]);
             };
-            for (int k = 0; k < nchunk; ++k, ++kk) {
+            auto chunk = [&](int k, auto ftag) {
                 const int c0 = k * CK;
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();  // chunk kk visible; chunk kk-1 fully consumed
@@ -565,10 +576,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
                 }
                 const float* bi = smem + (kk & 1) * BUFF;
                 const float* bw = bi + INF;
-                if (PEEL && k == 0) kstep(bi, bw, 0, c0, std::true_type{});
-                else kstep(bi, bw, 0, c0, std::false_type{});
+                kstep(bi, bw, 0, c0, ftag);
 #pragma unroll
                 for (int s = 1; s < CK / 4; ++s) kstep(bi, bw, s, c0, std::false_type{});
+                ++kk;
+            };
+            // chunk 0 peeled: its first K-step starts the sums from 0 (PEEL), so no copies of the
+            // accumulators are needed between a zeroing and a summing loop entry
+            if constexpr (PEEL) {
+                chunk(0, std::true_type{});
+                for (int k = 1; k < nchunk; ++k) chunk(k, std::false_type{});
+            } else {
+                for (int k = 0; k < nchunk; ++k) chunk(k, std::false_type{});
             }
         };
         if (border || EPI == EPI_BWD_POOL) {
@@ -658,7 +677,10 @@ bool wino_geometry(int B, int H, int W, int cin, int cout, WinoGeo* g) {
     r.NTS = r.TR * r.TC;
     r.BPS = ceil_div(r.NTS, 64);
     r.ncg = cout / 32;
-    if ((int64_t)B * r.BPS * r.ncg >= ((int64_t)1 << 31)) return false;
+    r.inv_ncg = 1.f / r.ncg;
+    r.inv_BPS = 1.f / r.BPS;
+    r.inv_TC = 1.f / r.TC;
+    if ((int64_t)B * r.BPS * r.ncg >= ((int64_t)1 << 22)) return false;  // unit indices (float division)
     if ((int64_t)cin * H * W >= ((int64_t)1 << 30)) return false;
     if ((int64_t)wino_ck(cin) * H * W + 4 * W + 64 >= ((int64_t)1 << 24)) return false;  // packed copy offsets
     if (g) *g = r;

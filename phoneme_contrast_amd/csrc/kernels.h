@@ -56,6 +56,7 @@ int launch_conv3x3_dma(int pro, int epi, ConvArgs a, hipStream_t s);
 struct WinoGeo {
     int TR, TC, NTS, BPS;  // tile rows / columns per sample, tiles per sample, 64-tile blocks per sample
     int ncg;               // output-channel groups of 32
+    float inv_ncg, inv_BPS, inv_TC;  // reciprocals for the kernel's unit decode
 };
 bool wino_geometry(int B, int H, int W, int cin, int cout, WinoGeo* g);
 size_t wino_nblk(int B, int H, int W, int cin, int cout);
