@@ -286,18 +286,19 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
             }
         } else {  // EPI_BWD_POOL: the conv runs at the pooled resolution; dz lives at Hs x Ws
             const int HWs = a.Hs * a.Ws;
+            constexpr int PB = V4 ? 1 : 2;  // channels per batch of window loads (registers)
             const int soff0 = tvalid ? (2 * h0) * a.Ws + 2 * w0 : 0;  // loads clamped in bounds
             const float* yb = a.yprev + ((int64_t)b * a.cout + n0) * HWs + soff0;
             float* ob = a.out + ((int64_t)b * a.cout + n0) * HWs + (2 * h0) * a.Ws + 2 * w0;
 #pragma unroll
-            for (int half = 0; half < 4; ++half) {
-                // two channels' windows loaded together (one round trip per pair; registers)
-                float win[2][4][4];
-                float4 cf[2];
-                float dv[2];
+            for (int half = 0; half < 8 / PB; ++half) {
+                // PB channels' windows loaded together (one round trip per batch; registers)
+                float win[PB][4][4];
+                float4 cf[PB];
+                float dv[PB];
 #pragma unroll
-                for (int jj = 0; jj < 2; ++jj) {
-                    const int j = 2 * half + jj;
+                for (int jj = 0; jj < PB; ++jj) {
+                    const int j = PB * half + jj;
                     const int co = 16 * (j >> 2) + 4 * kq + (j & 3);
                     cf[jj] = a.cf_out[n0 + co];
                     dv[jj] = a.drop_out ? a.drop_out[(int64_t)b * a.cout + n0 + co] : 1.f;
@@ -322,8 +323,8 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
                     }
                 }
 #pragma unroll
-                for (int jj = 0; jj < 2; ++jj) {
-                    const int j = 2 * half + jj;
+                for (int jj = 0; jj < PB; ++jj) {
+                    const int j = PB * half + jj;
                     const int co = 16 * (j >> 2) + 4 * kq + (j & 3);
                     float* op = ob + (int64_t)co * HWs;
                     float dzw[4][4];
@@ -448,14 +449,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
             voff[p] = ok ? 4u * (unsigned)(grow * a.W + gcol) : 0x80000000u;
         }
     };
-    auto issue = [&](const Unit& x, int c0, int buf) {
+    // part p of NP: channel planes [p CK / NP, (p + 1) CK / NP) and the matching share of the weight
+    // copies (the copies of a chunk are spread over its K-steps: the TA takes a dword copy's 64
+    // addresses at a few per clock, and a burst of them stalls the issuing wave in order)
+    auto issue = [&](const Unit& x, int c0, int buf, int part, int np) {
 #if defined(WINO_KO) && (WINO_KO & 1)  // analysis builds only (tools/wino_ko.sh): no operand copies
         return;
 #endif
         const float* sb = a.src + ((int64_t)x.b * a.cin + c0) * HW;
         const unsigned sl = lds0 + 4u * (unsigned)(buf * BUFF + wave * WSLOT);
+        const int cpp = CK / np;
 #pragma unroll
-        for (int cl = 0; cl < CK; ++cl) {
+        for (int ci = 0; ci < cpp; ++ci) {
+            const int cl = part * cpp + ci;
             const __amdgpu_buffer_rsrc_t r = wrsrc(sb + (int64_t)cl * HW, 4 * HW);
             bdma<false>(r, voff[0], sl + 4u * (unsigned)(cl * WSP));
             bdma<false>(r, voff[1], sl + 4u * (unsigned)(cl * WSP + 64));
@@ -463,8 +469,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
         }
         const float* sw = wuniform(a.wpack + ((int64_t)x.cg * a.cin + c0) * 512);
         const unsigned wl = lds0 + 4u * (unsigned)(buf * BUFF + INF);
+        const int wpp = (CK / 2) / np;
 #pragma unroll
-        for (int j = 0; j < CK / 2; ++j) wdma<4>(sw, 4u * (unsigned)(j * 1024 + tid * 4), wl + 4u * (unsigned)(j * 1024 + wave * 256));
+        for (int jj = 0; jj < wpp; ++jj) {
+            const int j = part * wpp + jj;
+            wdma<4>(sw, 4u * (unsigned)(j * 1024 + tid * 4), wl + 4u * (unsigned)(j * 1024 + wave * 256));
+        }
     };
 
     const int nchunk = a.cin / CK;
@@ -472,7 +482,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     Unit cur = unit_of(u < nunits ? u : 0);
     if (u < nunits) {
         plan_copies(cur);
-        issue(cur, 0, 0);
+        issue(cur, 0, 0, 0, 1);
     }
     int kk = 0;  // chunks issued so far (buffer = kk & 1)
     while (u < nunits) {
@@ -566,19 +576,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
             };
             auto chunk = [&](int k, auto ftag) {
                 const int c0 = k * CK;
+#if !(defined(WINO_KO) && (WINO_KO & 4))  // analysis builds only: no chunk synchronisation
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();  // chunk kk visible; chunk kk-1 fully consumed
-                if (k + 1 < nchunk) {
-                    issue(cur, c0 + CK, (kk + 1) & 1);
-                } else if (un < nunits) {
-                    plan_copies(nxt);
-                    issue(nxt, 0, (kk + 1) & 1);
-                }
+#endif
+                // the next chunk (of this unit, or the next unit's first), copied part by part
+                // ahead of this chunk's K-steps
+                const bool more = k + 1 < nchunk;
+                const bool pre = more || un < nunits;
+                if (!more && pre) plan_copies(nxt);
+                const Unit& tgt = more ? cur : nxt;
+                const int tc0 = more ? c0 + CK : 0, tbuf = (kk + 1) & 1;
                 const float* bi = smem + (kk & 1) * BUFF;
                 const float* bw = bi + INF;
+                if (pre) issue(tgt, tc0, tbuf, 0, CK / 4);
                 kstep(bi, bw, 0, c0, ftag);
 #pragma unroll
-                for (int s = 1; s < CK / 4; ++s) kstep(bi, bw, s, c0, std::false_type{});
+                for (int s = 1; s < CK / 4; ++s) {
+                    if (pre) issue(tgt, tc0, tbuf, s, CK / 4);
+                    kstep(bi, bw, s, c0, std::false_type{});
+                }
                 ++kk;
             };
             // chunk 0 peeled: its first K-step starts the sums from 0 (PEEL), so no copies of the

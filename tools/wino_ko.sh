@@ -4,7 +4,7 @@
 # On the GPU box: LD_LIBRARY_PATH=tools/ko<k> tools/wino_bench ...
 set -e
 cd "$(dirname "$0")/.."
-for k in 1 2 3; do
+for k in ${KOS:-1 2 3}; do
   mkdir -p tools/ko$k
   /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Iinclude -munsafe-fp-atomics -DWINO_KO=$k \
       -fno-slp-vectorize -c phoneme_contrast_amd/csrc/conv_wino.hip -o tools/ko$k/conv_wino.o
