@@ -76,17 +76,10 @@ __device__ __forceinline__ const float* wuniform(const float* p) {
 constexpr int WSW = 36, WSP = 160;
 
 // LDS DMA of one dword per lane from a buffer resource (out-of-range offsets write 0);
-// LDS destination = M0 + 4 * lane.  HALF: only lanes 0..15 take part (exec set inside the asm).
-template <bool HALF>
+// LDS destination = M0 + 4 * lane.
 __device__ __forceinline__ void bdma(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned lds_byte_addr) {
     const unsigned m0 = __builtin_amdgcn_readfirstlane(lds_byte_addr);
-    if constexpr (HALF) {
-        unsigned long long save;
-        asm volatile("s_mov_b64 %0, exec\n\ts_mov_b64 exec, 0xffff\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds\n\ts_mov_b64 exec, %0"
-                     : "=&s"(save) : "v"(voff), "s"(r), "{m0}"(m0) : "memory");
-    } else {
-        asm volatile("s_nop 0\n\tbuffer_load_dword %0, %1, 0 offen lds" :: "v"(voff), "s"(r), "{m0}"(m0) : "memory");
-    }
+    asm volatile("s_nop 0\n\tbuffer_load_dword %0, %1, 0 offen lds" :: "v"(voff), "s"(r), "{m0}"(m0) : "memory");
 }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t wrsrc(const float* base, int bytes) {
@@ -398,7 +391,7 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
 // last chunk of the current one is multiplied and during its epilogue.
 template <int PRO, int EPI, int CK, bool V4>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv_wino_kernel(ConvArgs a, WinoGeo g) {
-    constexpr int WSLOT = CK * WSP;           // floats of one wave's slot
+    constexpr int WSLOT = CK * WSP + 32;      // floats of one wave's slot (+ the last plane's overflow)
     constexpr int INF = 4 * WSLOT;            // input floats per buffer
     constexpr int BUFF = INF + CK * 512;      // + transformed weights of the chunk
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -431,9 +424,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
         x.tc_a = x.tw - x.tr_a * g.TC;
         return x;
     };
-    // Copies: per channel plane three 64-lane dword copies cover slot positions 0..143 (4 rows x WSW
-    // columns; the third uses lanes 0..15).  Lane offsets depend on the unit only (the channel is
-    // the buffer base); out-of-image positions get an out-of-range offset, which copies a 0.
+    // Copies: per channel plane three 64-lane dword copies cover slot positions 0..191: 0..143 are
+    // the 4 rows x WSW columns, 144..191 (out-of-range offsets: zeros) run into the next plane's
+    // first 32 positions, which that plane's copies, issued later by the same wave, overwrite (a
+    // wave's loads land in issue order); the last plane runs into the slot's 32-float tail.  Lane
+    // offsets depend on the unit only (the channel is the buffer base); out-of-image positions get
+    // an out-of-range offset, which copies a 0.  (No exec masking next to in-flight MFMAs.)
     unsigned voff[3];
     auto plan_copies = [&](const Unit& x) {
         const int segw = 2 * min(16, g.TC - x.tc_a) + 2;
@@ -446,7 +442,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
             const bool s1 = cc >= segw;
             const int grow = r + (s1 ? rb1 : rb0), gcol = cc + (s1 ? cb1 : cb0);
             const bool ok = (unsigned)grow < (unsigned)a.H && (unsigned)gcol < (unsigned)a.W;
-            voff[p] = ok ? 4u * (unsigned)(grow * a.W + gcol) : 0x80000000u;
+            voff[p] = (pos < 4 * WSW && ok) ? 4u * (unsigned)(grow * a.W + gcol) : 0x80000000u;
         }
     };
     // part p of NP: channel planes [p CK / NP, (p + 1) CK / NP) and the matching share of the weight
@@ -463,9 +459,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
         for (int ci = 0; ci < cpp; ++ci) {
             const int cl = part * cpp + ci;
             const __amdgpu_buffer_rsrc_t r = wrsrc(sb + (int64_t)cl * HW, 4 * HW);
-            bdma<false>(r, voff[0], sl + 4u * (unsigned)(cl * WSP));
-            bdma<false>(r, voff[1], sl + 4u * (unsigned)(cl * WSP + 64));
-            bdma<true>(r, voff[2], sl + 4u * (unsigned)(cl * WSP + 128));
+            bdma(r, voff[0], sl + 4u * (unsigned)(cl * WSP));
+            bdma(r, voff[1], sl + 4u * (unsigned)(cl * WSP + 64));
+            bdma(r, voff[2], sl + 4u * (unsigned)(cl * WSP + 128));
         }
         const float* sw = wuniform(a.wpack + ((int64_t)x.cg * a.cin + c0) * 512);
         const unsigned wl = lds0 + 4u * (unsigned)(buf * BUFF + INF);
@@ -729,7 +725,7 @@ int launch_conv3x3_wino(int pro, int epi, ConvArgs a, hipStream_t s) {
         PCX_CHECK_ARG(a.Hs >= 2 * a.H && a.Ws >= 2 * a.W, "conv3x3_wino: pooled source %dx%d for %dx%d", a.Hs, a.Ws,
                       a.H, a.W);
     const int ck = wino_ck(a.cin);
-    const size_t buff = (size_t)4 * ck * WSP + (size_t)ck * 512;
+    const size_t buff = (size_t)4 * (ck * WSP + 32) + (size_t)ck * 512;
     const size_t smem = (2 * buff + 2 * (size_t)a.cin + 512) * 4;
     PCX_CHECK_ARG(smem <= 160 * 1024, "conv3x3_wino: %zu B of LDS", smem);
     // persistent workgroups: two per CU (a multiple of 8, one XCD-contiguous run of units each round)
