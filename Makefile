@@ -8,7 +8,14 @@ OBJ = $(patsubst phoneme_contrast_amd/csrc/%.hip,build/%.o,$(SRC))
 HDR = $(wildcard phoneme_contrast_amd/csrc/*.h) include/pcx.h
 LIB = phoneme_contrast_amd/libpcx.so
 
-all: $(LIB)
+TOOLS = tools/wino_bench
+
+all: $(LIB) $(TOOLS)
+
+# engine cross-check / micro-benchmark (tests/test_wino_engine_gpu.py runs it)
+tools/wino_bench: tools/wino_bench.cpp $(LIB) $(HDR)
+	$(HIPCC) -O2 -std=c++17 --offload-arch=$(ARCH) -Iinclude $< -Lphoneme_contrast_amd -lpcx \
+	    -Wl,-rpath,'$$ORIGIN/../phoneme_contrast_amd' -o $@
 
 build/%.o: phoneme_contrast_amd/csrc/%.hip $(HDR)
 	@mkdir -p build
@@ -21,6 +28,6 @@ $(LIB): $(OBJ)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJ)
 
 clean:
-	rm -rf build $(LIB)
+	rm -rf build $(LIB) $(TOOLS)
 
 .PHONY: all clean

@@ -80,5 +80,7 @@ int main(int argc, char** argv) {
     double fl = 2.0 * B * H * W * cin * cout * 9;
     printf("H%d W%d %d->%d epi%d pro%d: direct %.3f ms (%.2f of fp32 roof)  wino %.3f ms (%.2f alg.)  |d out| %.2e of %.2e  |d sum0| %.2e of %.2e\n",
            H, W, cin, cout, epi, pro, msd, fl / msd / 1e9 / 157.3, msw, fl / msw / 1e9 / 157.3, emax, gmax, smax, sref);
-    return emax > 1e-3 * gmax + 1e-5 ? 2 : 0;
+    // exit status: 2 when the outputs or the summed statistics partials disagree beyond fp32 noise
+    const bool bad = emax > 1e-5 * gmax + 1e-6 || smax > 1e-4 * sref + 1e-3;
+    return bad ? 2 : 0;
 }
