@@ -246,12 +246,14 @@ def main():
     ap.add_argument("--cpu-full", action="store_true", help="also time the CPU baseline at B=4096 (minutes)")
     ap.add_argument("--bucket-mb", type=float, default=None,
                     help="N > 1: gradient all-reduce bucket size (default 0.5 MB cnn_small, 4 MB cnn_deep)")
+    ap.add_argument("--global-supcon", action="store_true",
+                    help="N > 1: SupCon over the global batch (embedding all-gather, sharded anchor rows)")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-peaks", action="store_true", help="skip the measured-peak probes")
     args = ap.parse_args()
 
     from phoneme_contrast_amd import distributed as ddp
-    from phoneme_contrast_amd.losses import SupervisedContrastiveLoss
+    from phoneme_contrast_amd.losses import GlobalSupervisedContrastiveLoss, SupervisedContrastiveLoss
     from phoneme_contrast_amd.models import model_registry
     from phoneme_contrast_amd.optim import FusedAdam
 
@@ -280,7 +282,8 @@ def main():
     if world > 1:  # buckets all-reduced on a side stream behind the native backward
         mb = args.bucket_mb if args.bucket_mb is not None else (4.0 if deep else 0.5)
         bucketer = ddp.GradBucketer(model, bucket_bytes=int(mb * (1 << 20)))
-    loss_fn = SupervisedContrastiveLoss(temperature=0.15)
+    loss_fn = (GlobalSupervisedContrastiveLoss if args.global_supcon else SupervisedContrastiveLoss)(temperature=0.15)
+    gscale = 1.0 if args.global_supcon else 1.0 / world
     g = torch.Generator().manual_seed(1234 + rank)
     x = torch.randn(B, 1, F, T, generator=g).to(dev)
     labels = (torch.arange(B // 4).repeat_interleave(4) + rank * (B // 4)).to(dev)
@@ -291,7 +294,7 @@ def main():
         opt.zero_grad(set_to_none=True)
         loss.backward()
         if world > 1:
-            opt.step(flat_grads=bucketer.finish(), grad_scale=1.0 / world)
+            opt.step(flat_grads=bucketer.finish(), grad_scale=gscale)
         else:
             opt.step()
         return loss
@@ -401,7 +404,9 @@ def main():
                    "per_gpu_batch": B, "global_batch": B * world, "n_mfcc": F, "T": T,
                    "embedding_dim": D, "parallelism": f"dp{world}",
                    "allreduce": None if world == 1 else f"{len(bucketer.buckets(next(iter(model._plans.values()))))} "
-                                                        "RCCL buckets behind the backward"},
+                                                        "RCCL buckets behind the backward",
+                   "supcon": "global batch (embedding + coefficient all-gathers, anchor rows per rank)"
+                             if args.global_supcon and world > 1 else "per rank (DDP-equivalent)"},
         "conv_algorithms": None if deep else {
             "conv_fwd / conv_dgrad L2-L6": "Winograd F(2x2,3x3) on fp32 MFMA (16 multiplies per 2x2 outputs: "
                                            "4/9 of the direct conv's; exact fp32 arithmetic)",

@@ -61,6 +61,28 @@ int pcx_supcon_backward(const float* features, const int64_t* labels, const floa
                         float* dfeatures, void* workspace, size_t workspace_bytes,
                         hipStream_t stream);
 
+/* Anchor-row ranges (the global-batch mode): rows [row0, row0+nrows) of a batch of B
+ * features act as anchors against all B columns.  A partition of [0, B) over ranks reproduces the
+ * single-batch loss: forward_rows writes rowstats [nrows*4] and loss_out ([1]: the range's share
+ * of the batch mean or sum; [nrows] for none).  coef_rows turns the range's rowstats + grad_out
+ * ([1] or [nrows]) into coef [nrows*4]; backward_rows takes coef for ALL B rows (the ranges'
+ * coefficients gathered) and writes dfeatures [nrows,D] = the full d loss / dF of its rows (the
+ * anchor-side and column-side terms both: no reduction of dF across ranges is needed).  The
+ * single-range calls above are row0 = 0, nrows = B.  Replaces nothing in the reference (which is
+ * single-device, src/training/losses.py:41-86); the semantics are that of the reference loss on
+ * the concatenated batch. */
+size_t pcx_supcon_rows_workspace_bytes(int64_t B, int64_t D, int64_t nrows);
+int pcx_supcon_forward_rows(const float* features, const int64_t* labels, const float* mask,
+                            int64_t B, int64_t D, int64_t row0, int64_t nrows, float temperature,
+                            float base_temperature, int reduction, float* loss_out, float* rowstats,
+                            void* workspace, size_t workspace_bytes, hipStream_t stream);
+int pcx_supcon_coef_rows(const float* rowstats, const float* grad_out, int64_t B, int64_t nrows,
+                         float base_temperature, int reduction, float* coef, hipStream_t stream);
+int pcx_supcon_backward_rows(const float* features, const int64_t* labels, const float* mask,
+                             int64_t B, int64_t D, int64_t row0, int64_t nrows, float temperature,
+                             float base_temperature, const float* coef, float* dfeatures,
+                             void* workspace, size_t workspace_bytes, hipStream_t stream);
+
 /* ------------------------------------------------------------------ Adam (flat buffers)
  * p, g, m, v: n fp32 each.  Coupled L2 (g += wd*p), bias correction with 1-based `step`.
  * grad_scale multiplies g first (1/world_size after an all-reduce SUM). */

@@ -235,6 +235,62 @@ def supcon_fwd_bwd(f, labels=None, mask=None, temperature=0.07, base_temperature
     return loss, df
 
 
+def _pos_mask(bsz, labels, mask):
+    if mask is None:
+        lab = np.asarray(labels).reshape(-1, 1)
+        return (lab == lab.T).astype(np.float64) * (1.0 - np.eye(bsz))
+    return np.asarray(mask, dtype=np.float64) * (1.0 - np.eye(bsz))
+
+
+def supcon_rows_fwd(f, labels, mask, row0, nrows, temperature=0.07, base_temperature=0.07,
+                    reduction="mean"):
+    """Anchor rows [row0, row0+nrows) of SupCon over the batch f [B, D] (the global-batch mode's
+    per-rank forward, include/pcx.h pcx_supcon_forward_rows).  Returns (loss share, rowstats
+    [nrows, 4] = (m_i, den_i, msum_i, loss_i)); the shares of a partition of [0, B) sum to the
+    reference loss (losses.py:41-86) of the whole batch."""
+    f = np.asarray(f, dtype=np.float64)
+    bsz = f.shape[0]
+    rows = np.arange(row0, row0 + nrows)
+    m = _pos_mask(bsz, labels, mask)[rows]
+    lm = np.ones((nrows, bsz))
+    lm[np.arange(nrows), rows] = 0.0
+    logits = f[rows] @ f.T / temperature
+    mx = logits.max(axis=1)
+    e = np.exp(logits - mx[:, None]) * lm
+    den = e.sum(axis=1) + 1e-6
+    msum = m.sum(axis=1)
+    p = np.where(msum == 0, 1.0, msum)
+    mlpp = (m * (logits - mx[:, None] - np.log(den)[:, None])).sum(axis=1) / p
+    per = -(temperature / base_temperature) * mlpp
+    share = {"mean": per.sum() / bsz, "sum": per.sum()}.get(reduction, per)
+    return share, np.stack([mx, den, msum, per], axis=1)
+
+
+def supcon_coef_rows(rowstats, grad_out, bsz, base_temperature=0.07, reduction="mean"):
+    """Per-anchor gradient coefficients (a_i, b_i, m_i) of pcx_supcon_coef_rows:
+    dLoss_i/dS_ij = a_i M_ij - b_i exp(S_ij/T - m_i) (j != i) with a_i = -w_i / (bT P_i),
+    b_i = a_i msum_i / den_i and w_i the anchor's weight in the reduction."""
+    mx, den, msum = rowstats[:, 0], rowstats[:, 1], rowstats[:, 2]
+    g = np.asarray(grad_out, dtype=np.float64).reshape(-1)
+    w = g if reduction == "none" else np.full(len(mx), g[0] / bsz if reduction == "mean" else g[0])
+    a = -w / base_temperature / np.where(msum == 0, 1.0, msum)
+    return np.stack([a, a * msum / den, mx], axis=1)
+
+
+def supcon_rows_bwd(f, labels, mask, row0, nrows, coef_all, temperature=0.07):
+    """dLoss/dF of rows [row0, row0+nrows) given every anchor's coefficients (pcx_supcon_backward_rows):
+    dF_i = sum_j (H_ij + H_ji) F_j, H_ij = a_i M_ij - b_i exp(S_ij/T - m_i), j != i -- the
+    anchor-side and column-side terms, so the ranges' results need no reduction."""
+    f = np.asarray(f, dtype=np.float64)
+    bsz = f.shape[0]
+    m = _pos_mask(bsz, labels, mask)
+    z = f @ f.T / temperature
+    a, b, mx = coef_all[:, 0], coef_all[:, 1], coef_all[:, 2]
+    h = a[:, None] * m - b[:, None] * np.exp(z - mx[:, None]) * (1.0 - np.eye(bsz))
+    rows = slice(row0, row0 + nrows)
+    return (h + h.T)[rows] @ f
+
+
 def ntxent_fwd_bwd(f, labels, temperature=0.07, reduction="mean"):
     """NTXentLoss labelled branch (losses.py:101-151) == SupCon with base_temperature=T."""
     if labels is None:

@@ -52,6 +52,12 @@ SIGNATURES = {
                                    c_int, c_void_p, c_void_p, c_void_p, c_size, c_void_p]),
     "pcx_supcon_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_i64, c_i64, c_float, c_float,
                                     c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_size, c_void_p]),
+    "pcx_supcon_rows_workspace_bytes": (c_size, [c_i64, c_i64, c_i64]),
+    "pcx_supcon_forward_rows": (c_int, [c_void_p, c_void_p, c_void_p, c_i64, c_i64, c_i64, c_i64, c_float,
+                                        c_float, c_int, c_void_p, c_void_p, c_void_p, c_size, c_void_p]),
+    "pcx_supcon_coef_rows": (c_int, [c_void_p, c_void_p, c_i64, c_i64, c_float, c_int, c_void_p, c_void_p]),
+    "pcx_supcon_backward_rows": (c_int, [c_void_p, c_void_p, c_void_p, c_i64, c_i64, c_i64, c_i64, c_float,
+                                         c_float, c_void_p, c_void_p, c_void_p, c_size, c_void_p]),
     "pcx_adam_step": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_i64, c_float,
                               c_float, c_float, c_float, c_float, c_float, c_void_p]),
     "pcx_net_create": (c_void_p, [ctypes.POINTER(NetConfig), c_i64, c_i64, c_i64]),

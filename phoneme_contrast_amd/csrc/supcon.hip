@@ -69,18 +69,20 @@ __device__ __forceinline__ float pos_weight(const int64_t* __restrict__ labels,
 template <int D>
 __global__ __launch_bounds__(256) void supcon_rows_partial(
     const float* __restrict__ F, const int64_t* __restrict__ labels, const float* __restrict__ mask,
-    int64_t B, float inv_t, int jblk_per_split, RowPart* __restrict__ part) {
+    int64_t B, int64_t row0, int64_t nrows, float inv_t, int jblk_per_split, RowPart* __restrict__ part) {
     const int lane = lane_id(), wave = threadIdx.x >> 6, h = lane >> 5;
-    const int64_t i = (int64_t)blockIdx.x * TILE + (lane & 31);
+    const int64_t il = (int64_t)blockIdx.x * TILE + (lane & 31);  // anchor row within the range
+    const bool ivalid = il < nrows;
+    const int64_t i = row0 + il;                                    // its column index in F
     const int64_t nj = (B + TILE - 1) / TILE;
-    const int64_t li = (labels && i < B) ? labels[i] : 0;
+    const int64_t li = (labels && ivalid) ? labels[i] : 0;
 
     RowPart p = {-INFINITY, 0.f, 0.f, 0.f};
     const int64_t jb0 = (int64_t)blockIdx.y * jblk_per_split;
     const int64_t jb1 = min(nj, jb0 + jblk_per_split);
     for (int64_t jb = jb0 + wave; jb < jb1; jb += WAVES) {
         f32x16 acc = tile_s<D>(F, jb * TILE + (lane & 31), i, B, h);
-        if (i < B) {
+        if (ivalid) {
             float mb = -INFINITY;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
@@ -119,21 +121,24 @@ __global__ __launch_bounds__(256) void supcon_rows_partial(
 #pragma unroll
         for (int w = 1; w < WAVES; ++w) q = merge(q, red[w][threadIdx.x]);
         int64_t row = (int64_t)blockIdx.x * TILE + threadIdx.x;
-        if (row < B) part[(int64_t)blockIdx.y * B + row] = q;
+        if (row < nrows) part[(int64_t)blockIdx.y * nrows + row] = q;
     }
 }
 
 // ---------------------------------------------------------------- forward: finalize
-// rowstats[i] = {m_i, den_i, msum_i, loss_i}; loss_out reduced per `reduction`.
+// rowstats[i] = {m_i, den_i, msum_i, loss_i} for the nrows anchors of the range; loss_out reduced
+// per `reduction` over the range, the mean taken over all B anchors of the batch (a range's value
+// is its share of the batch mean; the shares of a partition sum to the mean).
 __global__ __launch_bounds__(256) void supcon_rows_finalize(const RowPart* __restrict__ part,
-                                                             int nsplit, int64_t B, float t_over_bt,
-                                                             int reduction, float4* __restrict__ rowstats,
+                                                             int nsplit, int64_t B, int64_t nrows,
+                                                             float t_over_bt, int reduction,
+                                                             float4* __restrict__ rowstats,
                                                              float* __restrict__ loss_out) {
     __shared__ float red[256];
     float acc = 0.f;
-    for (int64_t i = threadIdx.x; i < B; i += blockDim.x) {
+    for (int64_t i = threadIdx.x; i < nrows; i += blockDim.x) {
         RowPart q = part[i];
-        for (int sp = 1; sp < nsplit; ++sp) q = merge(q, part[(int64_t)sp * B + i]);
+        for (int sp = 1; sp < nsplit; ++sp) q = merge(q, part[(int64_t)sp * nrows + i]);
         float den = q.s + 1e-6f;
         float P = (q.msum == 0.f) ? 1.f : q.msum;
         float mlpp = (q.pos - q.msum * q.m - q.msum * logf(den)) / P;
@@ -154,10 +159,12 @@ __global__ __launch_bounds__(256) void supcon_rows_finalize(const RowPart* __res
 
 // ---------------------------------------------------------------- backward: row coefficients
 // G_ij = a_i M_ij - b_i exp(S_ij/T - m_i), a_i = -w_i/(base_T P_i), b_i = a_i msum_i / den_i
+// (rows of one range; the mean's 1/B is over the whole batch as in the forward)
 __global__ void supcon_coef(const float4* __restrict__ rowstats, const float* __restrict__ grad_out,
-                            int64_t B, float inv_bt, int reduction, float4* __restrict__ coef) {
+                            int64_t B, int64_t nrows, float inv_bt, int reduction,
+                            float4* __restrict__ coef) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= B) return;
+    if (i >= nrows) return;
     float4 st = rowstats[i];
     float w = (reduction == PCX_REDUCTION_NONE) ? grad_out[i]
               : (reduction == PCX_REDUCTION_MEAN ? grad_out[0] / (float)B : grad_out[0]);
@@ -170,13 +177,14 @@ __global__ void supcon_coef(const float4* __restrict__ rowstats, const float* __
 template <int D>
 __global__ __launch_bounds__(256) void supcon_grad_partial(
     const float* __restrict__ F, const int64_t* __restrict__ labels, const float* __restrict__ mask,
-    const float4* __restrict__ coef, int64_t B, float inv_t, int jblk_per_split,
-    float* __restrict__ part) {
+    const float4* __restrict__ coef, int64_t B, int64_t row0, int64_t nrows, float inv_t,
+    int jblk_per_split, float* __restrict__ part) {
     constexpr int NQ = D / 32;  // 32-wide feature sub-tiles of dF
     const int lane = lane_id(), wave = threadIdx.x >> 6, h = lane >> 5;
-    const int64_t i = (int64_t)blockIdx.x * TILE + (lane & 31);
+    const int64_t il = (int64_t)blockIdx.x * TILE + (lane & 31);
+    const int64_t i = row0 + il;
     const int64_t nj = (B + TILE - 1) / TILE;
-    const bool ivalid = i < B;
+    const bool ivalid = il < nrows;
     const int64_t li = (labels && ivalid) ? labels[i] : 0;
     const float4 ci = ivalid ? coef[i] : make_float4(0.f, 0.f, 0.f, 0.f);
 
@@ -232,7 +240,7 @@ __global__ __launch_bounds__(256) void supcon_grad_partial(
     for (int e = threadIdx.x; e < TILE * D; e += blockDim.x) {
         int rr = e / D, cc = e % D;
         int64_t row = (int64_t)blockIdx.x * TILE + rr;
-        if (row < B) part[((int64_t)blockIdx.y * B + row) * D + cc] = red[rr][cc];
+        if (row < nrows) part[((int64_t)blockIdx.y * nrows + row) * D + cc] = red[rr][cc];
     }
 }
 
@@ -249,10 +257,11 @@ struct Geo {
     int nib, nsplit, per;
 };
 
-Geo geometry(int64_t B) {
+// anchor-row blocks over the range x column splits over the whole batch
+Geo geometry(int64_t B, int64_t nrows) {
     Geo g;
-    g.nib = ceil_div(B, TILE);
-    int64_t nj = g.nib;
+    g.nib = ceil_div(nrows, TILE);
+    int64_t nj = ceil_div(B, TILE);
     int64_t want = nj / (WAVES * 4);  // aim for >= 4 j-blocks per wave
     g.nsplit = (int)(want < 1 ? 1 : (want > 16 ? 16 : want));
     g.per = ceil_div(nj, g.nsplit);
@@ -273,6 +282,47 @@ int check_common(const float* F, const int64_t* labels, const float* mask, int64
     return PCX_OK;
 }
 
+int check_range(int64_t B, int64_t row0, int64_t nrows) {
+    PCX_CHECK_ARG(row0 >= 0 && nrows >= 1 && row0 + nrows <= B,
+                  "supcon: anchor rows [%lld, %lld) outside the batch of %lld", (long long)row0,
+                  (long long)(row0 + nrows), (long long)B);
+    return PCX_OK;
+}
+
+size_t ws_bytes_rows(int64_t B, int64_t D, int64_t nrows, bool with_coef) {
+    Geo g = geometry(B, nrows);
+    size_t fwd = (size_t)g.nsplit * nrows * sizeof(RowPart);
+    size_t bwd = (size_t)g.nsplit * nrows * D * sizeof(float) + (with_coef ? (size_t)B * sizeof(float4) : 0);
+    size_t n = fwd > bwd ? fwd : bwd;
+    return (n + 255) / 256 * 256;
+}
+
+void launch_rows_partial(const float* F, const int64_t* labels, const float* mask, int64_t B, int64_t D,
+                         int64_t row0, int64_t nrows, float temperature, RowPart* part, const Geo& g,
+                         hipStream_t stream) {
+    dim3 grid(g.nib, g.nsplit);
+    float inv_t = 1.0f / temperature;
+    if (D == 64)
+        supcon_rows_partial<64><<<grid, 256, 0, stream>>>(F, labels, mask, B, row0, nrows, inv_t, g.per, part);
+    else if (D == 128)
+        supcon_rows_partial<128><<<grid, 256, 0, stream>>>(F, labels, mask, B, row0, nrows, inv_t, g.per, part);
+    else
+        supcon_rows_partial<256><<<grid, 256, 0, stream>>>(F, labels, mask, B, row0, nrows, inv_t, g.per, part);
+}
+
+void launch_grad(const float* F, const int64_t* labels, const float* mask, int64_t B, int64_t D,
+                 int64_t row0, int64_t nrows, float temperature, const float4* coef, float* part,
+                 float* dF, const Geo& g, hipStream_t stream) {
+    dim3 grid(g.nib, g.nsplit);
+    float inv_t = 1.0f / temperature;
+    if (D == 64)
+        supcon_grad_partial<64><<<grid, 256, 0, stream>>>(F, labels, mask, coef, B, row0, nrows, inv_t, g.per, part);
+    else if (D == 128)
+        supcon_grad_partial<128><<<grid, 256, 0, stream>>>(F, labels, mask, coef, B, row0, nrows, inv_t, g.per, part);
+    else
+        supcon_grad_partial<256><<<grid, 256, 0, stream>>>(F, labels, mask, coef, B, row0, nrows, inv_t, g.per, part);
+}
+
 }  // namespace
 }  // namespace pcx
 
@@ -280,39 +330,79 @@ using namespace pcx;
 
 extern "C" size_t pcx_supcon_workspace_bytes(int64_t B, int64_t D) {
     if (B < 2) return 0;
-    Geo g = geometry(B);
-    size_t fwd = (size_t)g.nsplit * B * sizeof(RowPart);
-    size_t bwd = (size_t)g.nsplit * B * D * sizeof(float) + (size_t)B * sizeof(float4);
-    size_t n = fwd > bwd ? fwd : bwd;
-    return (n + 255) / 256 * 256;
+    return ws_bytes_rows(B, D, B, true);
+}
+
+extern "C" size_t pcx_supcon_rows_workspace_bytes(int64_t B, int64_t D, int64_t nrows) {
+    if (B < 2 || nrows < 1) return 0;
+    return ws_bytes_rows(B, D, nrows, false);
+}
+
+extern "C" int pcx_supcon_forward_rows(const float* F, const int64_t* labels, const float* mask,
+                                       int64_t B, int64_t D, int64_t row0, int64_t nrows,
+                                       float temperature, float base_temperature, int reduction,
+                                       float* loss_out, float* rowstats, void* ws, size_t ws_bytes,
+                                       hipStream_t stream) {
+    int rc = check_common(F, labels, mask, B, D, temperature, base_temperature, reduction);
+    if (rc) return rc;
+    if ((rc = check_range(B, row0, nrows))) return rc;
+    PCX_CHECK_ARG(loss_out && rowstats, "supcon: NULL output");
+    if (ws_bytes < ws_bytes_rows(B, D, nrows, false)) {
+        set_error("supcon: workspace too small");
+        return PCX_EWORKSPACE;
+    }
+    Geo g = geometry(B, nrows);
+    RowPart* part = static_cast<RowPart*>(ws);
+    launch_rows_partial(F, labels, mask, B, D, row0, nrows, temperature, part, g, stream);
+    PCX_LAUNCH_CHECK("supcon_rows_partial");
+    supcon_rows_finalize<<<1, 256, 0, stream>>>(part, g.nsplit, B, nrows, temperature / base_temperature,
+                                                 reduction, reinterpret_cast<float4*>(rowstats), loss_out);
+    PCX_LAUNCH_CHECK("supcon_rows_finalize");
+    return PCX_OK;
 }
 
 extern "C" int pcx_supcon_forward(const float* F, const int64_t* labels, const float* mask, int64_t B,
                                   int64_t D, float temperature, float base_temperature, int reduction,
                                   float* loss_out, float* rowstats, void* ws, size_t ws_bytes,
                                   hipStream_t stream) {
-    int rc = check_common(F, labels, mask, B, D, temperature, base_temperature, reduction);
+    return pcx_supcon_forward_rows(F, labels, mask, B, D, 0, B, temperature, base_temperature, reduction,
+                                   loss_out, rowstats, ws, ws_bytes, stream);
+}
+
+extern "C" int pcx_supcon_coef_rows(const float* rowstats, const float* grad_out, int64_t B, int64_t nrows,
+                                    float base_temperature, int reduction, float* coef, hipStream_t stream) {
+    PCX_CHECK_ARG(rowstats && grad_out && coef, "supcon: NULL argument");
+    PCX_CHECK_ARG(nrows >= 1 && nrows <= B, "supcon: bad row count %lld of %lld", (long long)nrows,
+                  (long long)B);
+    PCX_CHECK_ARG(base_temperature > 0.f, "supcon: temperatures must be > 0");
+    PCX_CHECK_ARG(reduction >= 0 && reduction <= 2, "supcon: bad reduction %d", reduction);
+    supcon_coef<<<ceil_div(nrows, 256), 256, 0, stream>>>(reinterpret_cast<const float4*>(rowstats), grad_out,
+                                                           B, nrows, 1.0f / base_temperature, reduction,
+                                                           reinterpret_cast<float4*>(coef));
+    PCX_LAUNCH_CHECK("supcon_coef");
+    return PCX_OK;
+}
+
+extern "C" int pcx_supcon_backward_rows(const float* F, const int64_t* labels, const float* mask,
+                                        int64_t B, int64_t D, int64_t row0, int64_t nrows,
+                                        float temperature, float base_temperature, const float* coef,
+                                        float* dF, void* ws, size_t ws_bytes, hipStream_t stream) {
+    int rc = check_common(F, labels, mask, B, D, temperature, base_temperature, 0);
     if (rc) return rc;
-    PCX_CHECK_ARG(loss_out && rowstats, "supcon: NULL output");
-    if (ws_bytes < pcx_supcon_workspace_bytes(B, D)) {
+    if ((rc = check_range(B, row0, nrows))) return rc;
+    PCX_CHECK_ARG(coef && dF, "supcon: NULL argument");
+    if (ws_bytes < ws_bytes_rows(B, D, nrows, false)) {
         set_error("supcon: workspace too small");
         return PCX_EWORKSPACE;
     }
-    Geo g = geometry(B);
-    RowPart* part = static_cast<RowPart*>(ws);
-    dim3 grid(g.nib, g.nsplit);
-    float inv_t = 1.0f / temperature;
-    if (D == 64)
-        supcon_rows_partial<64><<<grid, 256, 0, stream>>>(F, labels, mask, B, inv_t, g.per, part);
-    else if (D == 128)
-        supcon_rows_partial<128><<<grid, 256, 0, stream>>>(F, labels, mask, B, inv_t, g.per, part);
-    else
-        supcon_rows_partial<256><<<grid, 256, 0, stream>>>(F, labels, mask, B, inv_t, g.per, part);
-    PCX_LAUNCH_CHECK("supcon_rows_partial");
-    supcon_rows_finalize<<<1, 256, 0, stream>>>(part, g.nsplit, B, temperature / base_temperature,
-                                                 reduction, reinterpret_cast<float4*>(rowstats),
-                                                 loss_out);
-    PCX_LAUNCH_CHECK("supcon_rows_finalize");
+    Geo g = geometry(B, nrows);
+    float* part = static_cast<float*>(ws);
+    launch_grad(F, labels, mask, B, D, row0, nrows, temperature, reinterpret_cast<const float4*>(coef), part,
+                dF, g, stream);
+    PCX_LAUNCH_CHECK("supcon_grad_partial");
+    int64_t n = nrows * D;
+    sum_splits<<<ceil_div(n, 256), 256, 0, stream>>>(part, g.nsplit, n, dF);
+    PCX_LAUNCH_CHECK("sum_splits");
     return PCX_OK;
 }
 
@@ -327,21 +417,13 @@ extern "C" int pcx_supcon_backward(const float* F, const int64_t* labels, const 
         set_error("supcon: workspace too small");
         return PCX_EWORKSPACE;
     }
-    Geo g = geometry(B);
+    Geo g = geometry(B, B);
     float* part = static_cast<float*>(ws);
-    float4* coef = reinterpret_cast<float4*>(part + (size_t)g.nsplit * B * D);
-    supcon_coef<<<ceil_div(B, 256), 256, 0, stream>>>(reinterpret_cast<const float4*>(rowstats),
-                                                       grad_out, B, 1.0f / base_temperature,
-                                                       reduction, coef);
-    PCX_LAUNCH_CHECK("supcon_coef");
-    dim3 grid(g.nib, g.nsplit);
-    float inv_t = 1.0f / temperature;
-    if (D == 64)
-        supcon_grad_partial<64><<<grid, 256, 0, stream>>>(F, labels, mask, coef, B, inv_t, g.per, part);
-    else if (D == 128)
-        supcon_grad_partial<128><<<grid, 256, 0, stream>>>(F, labels, mask, coef, B, inv_t, g.per, part);
-    else
-        supcon_grad_partial<256><<<grid, 256, 0, stream>>>(F, labels, mask, coef, B, inv_t, g.per, part);
+    float* coef = part + (size_t)g.nsplit * B * D;
+    if ((rc = pcx_supcon_coef_rows(rowstats, grad_out, B, B, base_temperature, reduction, coef, stream)))
+        return rc;
+    launch_grad(F, labels, mask, B, D, 0, B, temperature, reinterpret_cast<const float4*>(coef), part, dF, g,
+                stream);
     PCX_LAUNCH_CHECK("supcon_grad_partial");
     int64_t n = B * D;
     sum_splits<<<ceil_div(n, 256), 256, 0, stream>>>(part, g.nsplit, n, dF);

@@ -109,6 +109,11 @@ class ContrastiveTrainer:
                 pbar.set_postfix({"loss": loss.item()})
         return {"loss": total_loss / max(num_batches, 1), "lr": self.optimizer.param_groups[0]["lr"]}
 
+    def _grad_scale(self) -> float:
+        """1/world for the per-rank (DDP-equivalent) loss; 1 for a global-batch loss
+        (GlobalSupervisedContrastiveLoss), whose ranks' gradients are shares of one gradient."""
+        return 1.0 if getattr(self.loss_fn, "global_batch", False) else 1.0 / self.world_size
+
     def _reduce_clip_step(self):
         """(all-reduce) -> (clip) -> optimizer step, in the reference's order (trainer.py:143-152).
 
@@ -130,7 +135,7 @@ class ContrastiveTrainer:
                     flats = opt.flat_grad_views()
                     for f in flats:
                         ddp.allreduce_flat(f)
-                scale = 1.0 / self.world_size
+                scale = self._grad_scale()
             if clip:
                 if flats is None:
                     flats = opt.flat_grad_views()
@@ -141,7 +146,7 @@ class ContrastiveTrainer:
             grads = [p.grad for p in self.model.parameters() if p.grad is not None]
             flat = torch.cat([g.reshape(-1) for g in grads])
             ddp.allreduce_flat(flat)
-            flat /= self.world_size
+            flat *= self._grad_scale()
             off = 0
             for g in grads:
                 g.copy_(flat[off:off + g.numel()].view_as(g))

@@ -30,7 +30,7 @@ from phoneme_contrast_amd import distributed as ddp  # noqa: E402
 from phoneme_contrast_amd.data import (GpuContrastiveBatches, GpuEvalBatches, ShardedBatchSampler,  # noqa: E402
                                        WaveformStore, parse_dataset)
 from phoneme_contrast_amd.features import GpuViewBuilder, build_feature_extractor  # noqa: E402
-from phoneme_contrast_amd.losses import get_loss_fn  # noqa: E402
+from phoneme_contrast_amd.losses import GlobalSupervisedContrastiveLoss, get_loss_fn  # noqa: E402
 from phoneme_contrast_amd.models import model_registry  # noqa: E402
 from phoneme_contrast_amd.optim import FusedAdam  # noqa: E402
 from phoneme_contrast_amd.samplers import ContrastiveBatchSampler  # noqa: E402
@@ -104,7 +104,13 @@ def setup_model(cfg, device, world=1):
         scheduler = torch.optim.lr_scheduler.CosineAnnealingLR(
             optimizer, T_max=cfg.training.epochs, eta_min=cfg.training.get("min_lr", 1e-6))
     loss_cfg = dict(cfg.training.loss)
-    loss_fn = get_loss_fn(loss_cfg.pop("type"), **loss_cfg)
+    loss_type = loss_cfg.pop("type")
+    if cfg.accel.get("global_supcon", False) and world > 1:
+        if loss_type != "supervised_contrastive":
+            raise ValueError(f"accel.global_supcon needs the supervised_contrastive loss, not {loss_type}")
+        loss_fn = GlobalSupervisedContrastiveLoss(**loss_cfg)
+    else:
+        loss_fn = get_loss_fn(loss_type, **loss_cfg)
     return model, optimizer, scheduler, loss_fn
 
 

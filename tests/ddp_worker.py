@@ -82,6 +82,51 @@ def run(name, case, cfg, bucketed, clip, rank, world, out):
         bucketer.detach()
 
 
+def run_global(rank, world, out):
+    """Global-batch SupCon (GlobalSupervisedContrastiveLoss): (a) the loss alone on this rank's rows
+    of a seeded global embedding batch, reductions mean / none; (b) a cnn_small trainer step on the
+    golden case's shard, whose gradients the trainer SUMS (grad_scale 1)."""
+    from golden_util import model_case
+    from phoneme_contrast_amd import distributed as ddp
+    from phoneme_contrast_amd.losses import GlobalSupervisedContrastiveLoss
+    from phoneme_contrast_amd.models import model_registry
+    from phoneme_contrast_amd.optim import FusedAdam
+    from phoneme_contrast_amd.trainer import ContrastiveTrainer
+
+    g = torch.Generator().manual_seed(77)
+    fg = torch.nn.functional.normalize(torch.randn(2 * 384, 128, generator=g), dim=1)
+    lab = torch.randint(0, 40, (2 * 384,), generator=g)
+    lo, hi = ddp.shard(fg.shape[0], rank, world)
+    for red in ("mean", "none"):
+        f = fg[lo:hi].clone().cuda().requires_grad_(True)
+        loss = GlobalSupervisedContrastiveLoss(temperature=0.1, reduction=red)(f, lab[lo:hi].cuda())
+        (loss.sum() if loss.dim() else loss).backward()
+        out[f"gloss_{red}/loss"] = np.atleast_1d(loss.detach().cpu().numpy())
+        out[f"gloss_{red}/grad"] = f.grad.cpu().numpy()
+
+    c = model_case("cnn_small_T201")
+    m = model_registry.create("phoneme_cnn", {"embedding_dim": 128, "use_attention": True, "dropout_rate": 0.1})
+    m.load_state_dict({k: torch.tensor(v) for k, v in c["state0"].items()})
+    m = m.cuda().train()
+    opt = FusedAdam(m.parameters(), lr=c["lr"], weight_decay=c["weight_decay"])
+    loss_fn = GlobalSupervisedContrastiveLoss(temperature=c["temperature"])
+    tmp = tempfile.mkdtemp(prefix=f"ddp_global_{rank}_")
+    trainer = ContrastiveTrainer(model=m, train_loader=[], val_loader=None, loss_fn=loss_fn, optimizer=opt,
+                                 scheduler=None, device=torch.device("cuda"), config={}, output_dir=tmp,
+                                 logger=logging.getLogger("ddp_worker"))
+    B = c["x"].shape[0]
+    lo, hi = ddp.shard(B, rank, world)
+    m.set_dropout_masks([torch.tensor(k[lo:hi]) for k in c["steps"][0]["masks"]])
+    loss = loss_fn(m(torch.tensor(c["x"][lo:hi]).cuda()), torch.tensor(c["labels"][lo:hi]).cuda())
+    opt.zero_grad()
+    loss.backward()
+    out["small_global/local"] = opt.flat_grad_views()[0].cpu().numpy().copy()
+    trainer._reduce_clip_step()
+    torch.cuda.synchronize()
+    out["small_global/loss"] = np.array([loss.item()])
+    out["small_global/m"] = opt._flat[0]["m"].cpu().numpy()
+
+
 def main():
     out_dir = sys.argv[1]
     from phoneme_contrast_amd import distributed as ddp
@@ -90,6 +135,7 @@ def main():
     out = {}
     for sc in SCENARIOS:
         run(*sc, rank, world, out)
+    run_global(rank, world, out)
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **out)
     torch.distributed.barrier()
     torch.distributed.destroy_process_group()

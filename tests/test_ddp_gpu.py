@@ -179,3 +179,64 @@ def test_fused_adam_second_group_unaligned_grads_match_torch():
         fa.step()
         ta.step()
     assert torch.allclose(b_f, b_t, rtol=1e-6, atol=1e-7) and torch.allclose(a_f, a_t, rtol=1e-6, atol=1e-7)
+
+
+def test_global_supcon_loss_is_the_single_batch_loss(ranks):
+    """GlobalSupervisedContrastiveLoss over 2 ranks == the reference loss on the concatenated batch
+    (float64 oracle), every rank returning the batch value and the FULL gradient of its rows."""
+    from oracle import np_ops as op
+    g = torch.Generator().manual_seed(77)
+    fg = torch.nn.functional.normalize(torch.randn(2 * 384, 128, generator=g), dim=1)
+    lab = torch.randint(0, 40, (2 * 384,), generator=g)
+    for red in ("mean", "none"):
+        ref_l, ref_g = op.supcon_fwd_bwd(fg.double().numpy(), lab.numpy(), None, 0.1, 0.07, red)
+        if red == "mean":
+            for r in ranks:
+                assert abs(r[f"gloss_{red}/loss"][0] - ref_l) < 1e-4
+        else:
+            got = np.concatenate([r[f"gloss_{red}/loss"] for r in ranks])
+            assert np.abs(got - ref_l).max() < 1e-4 * max(1.0, np.abs(ref_l).max())
+        got_g = np.concatenate([r[f"gloss_{red}/grad"] for r in ranks])
+        assert np.abs(got_g - ref_g).max() <= 1e-4 * np.abs(ref_g).max()
+
+
+def test_global_supcon_trainer_sums_rank_gradients(ranks):
+    """cnn_small with the global loss: per-rank BatchNorm, SupCon over both shards' embeddings.  The
+    trainer sums the ranks' gradients (grad_scale 1): m = (1 - b1)(g0 + g1 + wd p0) exactly, and
+    g0 + g1 matches the float64 oracle (per-shard forward, SupCon on the concatenated embeddings,
+    per-shard backward) within the 5e-3 relative tolerance of the DDP tests."""
+    from oracle import np_models as nm
+    from oracle import np_ops as op
+    r0, r1 = ranks
+    case, cfg = "cnn_small_T201", {"embedding_dim": 128, "use_attention": True, "dropout_rate": 0.1}
+    c = model_case(case)
+    assert r0["small_global/loss"][0] == r1["small_global/loss"][0]
+    assert np.array_equal(r0["small_global/m"], r1["small_global/m"])
+    names = _names_offsets(case, cfg)
+    p0_all = np.concatenate([c["state0"][k].reshape(-1) for k in names]).astype(np.float32)
+    gsum = (r0["small_global/local"] + r1["small_global/local"]).astype(np.float32)
+    m_ref = np.float32(1 - B1) * (gsum + np.float32(c["weight_decay"]) * p0_all)
+    assert np.allclose(r0["small_global/m"], m_ref, rtol=1e-5, atol=1e-12)
+    B = c["x"].shape[0]
+    embs, tapes = [], []
+    for r in range(2):
+        lo, hi = r * B // 2, (r + 1) * B // 2
+        e, t = nm.forward(c["state0"], c["x"][lo:hi], True, [k[lo:hi] for k in c["steps"][0]["masks"]])
+        embs.append(e)
+        tapes.append(t)
+    loss, de = op.supcon_fwd_bwd(np.concatenate(embs), c["labels"], None, c["temperature"], 0.07)
+    assert abs(r0["small_global/loss"][0] - loss) < 1e-3 * max(1.0, abs(loss))
+    gref = None
+    for r in range(2):
+        gr = nm.backward(c["state0"], tapes[r], de[r * B // 2:(r + 1) * B // 2])
+        gref = gr if gref is None else {k: gref[k] + gr[k] for k in gref}
+    bad = {}
+    for k, (off, n, shape) in names.items():
+        got, ref = gsum[off:off + n].astype(np.float64), gref[k].reshape(-1)
+        if bn_fed_bias(k, None):
+            err, tol = np.abs(got - ref).max(), 1e-4
+        else:
+            err, tol = np.abs(got - ref).max() / max(np.abs(ref).max(), 1e-30), 5e-3
+        if err > tol:
+            bad[k] = err
+    assert not bad, bad

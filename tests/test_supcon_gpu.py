@@ -54,6 +54,81 @@ def test_supcon_large_vs_oracle(B, D, T):
     assert err < 1e-4
 
 
+@pytest.mark.parametrize("B,D,cuts,red,use_mask", [(1000, 128, (0, 333, 1000), "mean", False),
+                                                   (4096, 128, (0, 512, 4096), "sum", False),
+                                                   (200, 64, (0, 7, 120, 200), "none", True),
+                                                   (130, 256, (0, 65, 130), "mean", True)])
+def test_supcon_row_ranges_match_oracle(B, D, cuts, red, use_mask):
+    """The global-batch mode's C-ABI (pcx_supcon_forward_rows / _coef_rows / _backward_rows) on a
+    partition of the anchors, in one process: each range's rowstats and loss share, its gradient
+    coefficients and -- given all ranges' coefficients -- the full gradient of its rows, vs the
+    float64 restatement (oracle/np_ops.py supcon_rows_*), and the assembled ranges vs the
+    single-batch reference loss."""
+    from phoneme_contrast_amd import _lib
+    lib = _lib.lib()
+    g = torch.Generator().manual_seed(B + D)
+    f = torch.nn.functional.normalize(torch.randn(B, D, generator=g), dim=1)
+    lab = torch.randint(0, max(2, B // 5), (B,), generator=g)
+    mask = (torch.rand(B, B, generator=g) < 0.05).float() if use_mask else None
+    T, bT = 0.12, 0.07
+    red_i = _lib.REDUCTIONS[red]
+    fd = f.cuda()
+    labd = None if use_mask else lab.cuda()
+    maskd = mask.cuda() if use_mask else None
+    stream = _lib.stream_of(fd)
+    ranges = list(zip(cuts[:-1], cuts[1:]))
+    shares, coefs, stats = [], [], []
+    for lo, hi in ranges:
+        n = hi - lo
+        loss = torch.empty(n if red == "none" else 1, device="cuda")
+        st = torch.empty(n, 4, device="cuda")
+        nws = lib.pcx_supcon_rows_workspace_bytes(B, D, n)
+        ws = _lib.workspace(nws, fd.device)
+        _lib.check(lib.pcx_supcon_forward_rows(_lib.ptr(fd), _lib.ptr(labd), _lib.ptr(maskd), B, D, lo, n, T, bT,
+                                               red_i, _lib.ptr(loss), _lib.ptr(st), _lib.ptr(ws), nws, stream), "fwd")
+        gout = torch.ones(n if red == "none" else 1, device="cuda")
+        cf = torch.empty(n, 4, device="cuda")
+        _lib.check(lib.pcx_supcon_coef_rows(_lib.ptr(st), _lib.ptr(gout), B, n, bT, red_i, _lib.ptr(cf), stream),
+                   "coef")
+        shares.append(loss.cpu().double().numpy())
+        stats.append(st.cpu().double().numpy())
+        coefs.append(cf)
+    coef_all = torch.cat(coefs)
+    fn, mn, ln = f.double().numpy(), (mask.double().numpy() if use_mask else None), lab.numpy()
+    ref_l, ref_g = op.supcon_fwd_bwd(fn, None if use_mask else ln, mn, T, bT, red)
+    cref = []
+    for (lo, hi), share, st in zip(ranges, shares, stats):
+        s_ref, st_ref = op.supcon_rows_fwd(fn, None if use_mask else ln, mn, lo, hi - lo, T, bT, red)
+        assert np.abs(share - s_ref).max() <= 1e-4 * max(1.0, np.abs(s_ref).max())
+        assert np.abs(st[:, 3] - st_ref[:, 3]).max() <= 1e-4 * max(1.0, np.abs(st_ref[:, 3]).max())
+        cref.append(op.supcon_coef_rows(st_ref, np.ones(hi - lo if red == "none" else 1), B, bT, red))
+    got_l = np.concatenate(shares) if red == "none" else sum(s[0] for s in shares)
+    assert np.abs(got_l - ref_l).max() <= 1e-4 * max(1.0, np.abs(ref_l).max())
+    np.testing.assert_allclose(coef_all.cpu().double().numpy(), np.concatenate(cref), rtol=1e-4, atol=1e-9)
+    parts = []
+    for lo, hi in ranges:
+        n = hi - lo
+        df = torch.empty(n, D, device="cuda")
+        nws = lib.pcx_supcon_rows_workspace_bytes(B, D, n)
+        ws = _lib.workspace(nws, fd.device)
+        _lib.check(lib.pcx_supcon_backward_rows(_lib.ptr(fd), _lib.ptr(labd), _lib.ptr(maskd), B, D, lo, n, T, bT,
+                                                _lib.ptr(coef_all), _lib.ptr(df), _lib.ptr(ws), nws, stream), "bwd")
+        parts.append(df.cpu().double().numpy())
+    got_g = np.concatenate(parts)
+    assert np.abs(got_g - ref_g).max() <= 1e-4 * np.abs(ref_g).max() + 1e-7
+
+
+def test_supcon_row_range_errors():
+    from phoneme_contrast_amd import _lib
+    lib = _lib.lib()
+    f = torch.zeros(16, 128, device="cuda")
+    lab = torch.zeros(16, dtype=torch.int64, device="cuda")
+    out = torch.empty(4, device="cuda")
+    rc = lib.pcx_supcon_forward_rows(_lib.ptr(f), _lib.ptr(lab), None, 16, 128, 10, 8, 0.1, 0.07, 0,
+                                     _lib.ptr(out), _lib.ptr(out), None, 0, _lib.stream_of(f))
+    assert rc != 0 and "outside the batch" in _lib.last_error()
+
+
 def test_supcon_errors_match_reference():
     from phoneme_contrast_amd.losses import NTXentLoss, SupervisedContrastiveLoss
     f = torch.nn.functional.normalize(torch.randn(1, 128, device="cuda"), dim=1)
