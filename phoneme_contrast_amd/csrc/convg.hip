@@ -721,6 +721,56 @@ __global__ __launch_bounds__(256) void maxpool3_bwd_prep_kernel(const uint8_t* _
     }
 }
 
+// Class-planar stride-2 data gradient -> dx (the parity classes' dense planes written by the
+// channel-last engine, ConvGArgs::par_out).  VW = 4 (W % 4 == 0): a thread writes 4 consecutive
+// elements of a dx row (one 16-byte store) from two 8-byte loads of its row parity's two column
+// classes; VW = 2 (W even): 2 elements (8-byte store) from one element of each; VW = 1: one element.
+template <int VW>
+__global__ __launch_bounds__(256) void par_interleave_kernel(const float* __restrict__ src, float* __restrict__ dx,
+                                                             unsigned total, int IH, int IW, int acc, int64_t o1,
+                                                             int64_t o2, int64_t o3) {
+    const unsigned t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= total) return;
+    const int64_t off[4] = {0, o1, o2, o3};
+    if (VW == 2) {
+        const unsigned IW2 = (unsigned)IW >> 1, per = (unsigned)IH * IW2;
+        const unsigned pl = t / per, rem = t - pl * per, ih = rem / IW2, k = rem - ih * IW2;
+        const int r = ih & 1, IWc = IW >> 1, IHc = (IH - r + 1) >> 1;
+        const int64_t so = (int64_t)pl * IHc * IWc + (int64_t)(ih >> 1) * IWc + k;
+        float2 v = make_float2(src[off[2 * r] + so], src[off[2 * r + 1] + so]);
+        float2* d = reinterpret_cast<float2*>(dx + (int64_t)pl * IH * IW + (int64_t)ih * IW + 2 * k);
+        if (acc) {
+            const float2 u = *d;
+            v.x += u.x;
+            v.y += u.y;
+        }
+        *d = v;
+    } else if (VW == 4) {
+        const unsigned IW4 = (unsigned)IW >> 2, per = (unsigned)IH * IW4;
+        const unsigned pl = t / per, rem = t - pl * per, ih = rem / IW4, k = rem - ih * IW4;
+        const int r = ih & 1, IWc = IW >> 1, IHc = (IH - r + 1) >> 1;
+        const int64_t CHW = (int64_t)IHc * IWc;
+        const int64_t so = (int64_t)pl * CHW + (int64_t)(ih >> 1) * IWc + 2 * k;
+        const float2 e = *reinterpret_cast<const float2*>(src + off[2 * r] + so);
+        const float2 o = *reinterpret_cast<const float2*>(src + off[2 * r + 1] + so);
+        float4 v = make_float4(e.x, o.x, e.y, o.y);
+        float4* d = reinterpret_cast<float4*>(dx + (int64_t)pl * IH * IW + (int64_t)ih * IW + 4 * k);
+        if (acc) {
+            const float4 u = *d;
+            v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+        }
+        *d = v;
+    } else {
+        const unsigned per = (unsigned)IH * IW;
+        const unsigned pl = t / per, rem = t - pl * per, ih = rem / IW, iw = rem - ih * IW;
+        const int q = (ih & 1) * 2 + (iw & 1);
+        const int IHc = (IH - (q >> 1) + 1) >> 1, IWc = (IW - (q & 1) + 1) >> 1;
+        const float v = src[off[q] + (int64_t)pl * IHc * IWc + (int64_t)(ih >> 1) * IWc + (iw >> 1)];
+        float* d = dx + t;
+        *d = acc ? *d + v : v;
+    }
+}
+
 __global__ void fill_cf_kernel(float4* cf, int C, float4 v) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c < C) cf[c] = v;
@@ -785,11 +835,14 @@ size_t convg_wpack_bytes(int mode, int cin, int cout, int k) {
 int launch_convg(ConvGArgs a, hipStream_t s) {
     PCX_CHECK_ARG(a.stride == 1 || a.stride == 2, "convg: stride %d unsupported", a.stride);
     PCX_CHECK_ARG(a.B > 0 && a.cin > 0 && a.cout > 0, "convg: empty tensor");
+    PCX_CHECK_ARG(!a.par_out || ((a.mode == 1 || a.mode == 3) && a.stride == 2 && a.bf16 && a.dyn),
+                  "convg: class-planar output only for the channel-last stride-2 data gradient");
     if (a.mode == 1 && a.stride == 2) {
         for (int par = 0; par < 4; ++par) {  // each parity class of dx written exactly once
             ConvGArgs c = a;
             c.mode = 3;
             c.par = par;
+            if (a.par_out) c.par_out = a.par_out + par_off(a.B, a.cin, a.IH, a.IW, par);
             const int rc = launch_convg(c, s);
             if (rc != PCX_OK) return rc;
         }
@@ -950,6 +1003,33 @@ int launch_maxpool3_bwd(const uint8_t* arg, const float* dout, float* dz, int B,
     const int64_t rows = (int64_t)B * C;
     maxpool3_bwd_kernel<<<(unsigned)rows, 256, 0, s>>>(arg, dout, dz, H, W, OH, OW);
     PCX_LAUNCH_CHECK("maxpool3_bwd_kernel");
+    return PCX_OK;
+}
+
+int64_t par_off(int B, int C, int IH, int IW, int q) {
+    int64_t off = 0;
+    for (int k = 0; k < q; ++k)
+        off += (int64_t)B * C * ((IH - (k >> 1) + 1) / 2) * ((IW - (k & 1) + 1) / 2);
+    return off;
+}
+
+int launch_par_interleave(const float* src, float* dx, int B, int C, int IH, int IW, int accumulate, hipStream_t s) {
+    const int64_t n = (int64_t)B * C * IH * IW;
+    PCX_CHECK_ARG(n > 0 && n < ((int64_t)1 << 31), "par_interleave: %lld elements unsupported", (long long)n);
+    const int64_t o1 = par_off(B, C, IH, IW, 1), o2 = par_off(B, C, IH, IW, 2), o3 = par_off(B, C, IH, IW, 3);
+    if (IW % 4 == 0) {
+        const unsigned total = (unsigned)(n / 4);
+        par_interleave_kernel<4><<<ceil_div((int64_t)total, 256), 256, 0, s>>>(src, dx, total, IH, IW, accumulate, o1,
+                                                                               o2, o3);
+    } else if (IW % 2 == 0) {
+        const unsigned total = (unsigned)(n / 2);
+        par_interleave_kernel<2><<<ceil_div((int64_t)total, 256), 256, 0, s>>>(src, dx, total, IH, IW, accumulate, o1,
+                                                                               o2, o3);
+    } else {
+        par_interleave_kernel<1><<<ceil_div(n, 256), 256, 0, s>>>(src, dx, (unsigned)n, IH, IW, accumulate, o1, o2,
+                                                                   o3);
+    }
+    PCX_LAUNCH_CHECK("par_interleave_kernel");
     return PCX_OK;
 }
 

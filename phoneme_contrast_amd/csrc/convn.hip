@@ -261,6 +261,7 @@ __global__ __launch_bounds__(256) void convn_kernel(ConvGArgs a) {
         const int64_t col = n0 + wc * 32 * WN + ni * 32 + l32;
         if (col >= N) continue;
         int64_t obase, ostride;
+        float* dst = a.out;
         if (MODE == 0) {
             const int64_t b = col / OHW;
             obase = b * a.cout * OHW + (col - b * OHW);
@@ -271,9 +272,15 @@ __global__ __launch_bounds__(256) void convn_kernel(ConvGArgs a) {
             ostride = IHW;
         } else {
             const int64_t b = col / CHW, p = col - b * CHW;
-            const int ihc = (int)(p / IWc), iwc = (int)(p - (int64_t)(p / IWc) * IWc);
-            obase = b * a.cin * IHW + (int64_t)(2 * ihc + ph) * a.IW + 2 * iwc + pw;
-            ostride = IHW;
+            if (a.par_out) {  // dense class planes (contiguous 128-byte rows)
+                dst = a.par_out;
+                obase = b * a.cin * CHW + p;
+                ostride = CHW;
+            } else {
+                const int ihc = (int)(p / IWc), iwc = (int)(p - (int64_t)(p / IWc) * IWc);
+                obase = b * a.cin * IHW + (int64_t)(2 * ihc + ph) * a.IW + 2 * iwc + pw;
+                ostride = IHW;
+            }
         }
 #pragma unroll
         for (int mi = 0; mi < WM; ++mi)
@@ -281,7 +288,7 @@ __global__ __launch_bounds__(256) void convn_kernel(ConvGArgs a) {
             for (int r = 0; r < 16; ++r) {
                 const int64_t row = m0 + wr * 32 * WM + mi * 32 + acc_row(r, h);
                 if (row < M) {
-                    float* o = a.out + obase + row * ostride;
+                    float* o = dst + obase + row * ostride;
                     if (MODE != 0 && a.accumulate) *o += acc[mi][ni][r];
                     else *o = acc[mi][ni][r];
                 }

@@ -31,6 +31,7 @@ struct DeepBlock {
     // precision "bf16" with channel counts the channel-last engine takes (convn.hip): padded NHWC
     // bf16 images of the block input (conv1, shortcut) and of d1 (conv2), kept for the backward
     bool cn;
+    bool planar;                   // stride-2 data gradient through class-planar planes (channel-last)
     size_t an, d1n;
 };
 
@@ -48,6 +49,7 @@ struct DeepPlan {
     DeepBlock blk[4];
     size_t g, dyA, dyB, dd, hdz;   // backward scratch
     size_t dyn1, dyn2;             // channel-last bf16 dy images (conv1 / conv2, shortcut)
+    size_t partmp;                 // class-planar stride-2 data gradient (ConvGArgs::par_out), or 0
     size_t stat, wgp, ident;
     int ia, ip;                    // attention / projection parameter indices
     int bn_proj;
@@ -89,7 +91,7 @@ int build_deep(Plan& p) {
     d.cf0 = p.carve("cf0", C0 * 16);
     d.cfb0 = p.carve("cfb0", C0 * 16);
     int pidx = 4, bnidx = 1, cin = C0, H = d.H1, W = d.W1;
-    size_t gmax = 0, stat = 0, wg = 0, dynmax = 0;
+    size_t gmax = 0, stat = 0, wg = 0, dynmax = 0, partmax = 0;
     auto wg_need = [&](int ci, int co, int k, int oh, int ow) {
         ConvGArgs a{};
         a.B = B; a.cin = ci; a.cout = co; a.KH = a.KW = k; a.OH = oh; a.OW = ow;
@@ -155,6 +157,8 @@ int build_deep(Plan& p) {
         wg_need(k.cout, k.cout, 3, k.Ho, k.Wo);
         if (k.sc) wg_need(k.cin, k.cout, 1, k.Ho, k.Wo);
         k.cn = d.bf16 && k.cin % 32 == 0 && k.cout % 32 == 0;
+        k.planar = k.cn && k.stride == 2 && (int64_t)planes(B, k.cin, k.Hi, k.Wi) < ((int64_t)1 << 31);
+        if (k.planar) partmax = std::max(partmax, (size_t)planes(B, k.cin, k.Hi, k.Wi) * 4);
         k.an = k.d1n = 0;
         if (k.cn) {
             k.an = p.carve("nhwc_a", nhwc_bytes(B, k.cin, k.Hi, k.Wi));
@@ -171,6 +175,7 @@ int build_deep(Plan& p) {
     d.dyA = p.carve("dyA", gmax);
     d.dyB = p.carve("dyB", gmax);
     d.dd = p.carve("dd", gmax);
+    d.partmp = partmax ? p.carve("par_planes", partmax) : 0;
     d.dyn1 = dynmax ? p.carve("nhwc_dy1", dynmax) : 0;
     d.dyn2 = dynmax ? p.carve("nhwc_dy2", dynmax) : 0;
     const int C4 = d.h[3];
@@ -358,7 +363,7 @@ int conv_wgrad(const Ctx& c, int layer, const float* x, int cin, int IH, int IW,
 
 int conv_dgrad(const Ctx& c, int layer, const float* dy, int cout, int OH, int OW, int k, int stride, int pad,
                const float* wgt, float* dx, int cin, int IH, int IW, int accumulate, bool dma = false,
-               const void* dyn = nullptr) {
+               const void* dyn = nullptr, float* par_out = nullptr) {
     if (dma) {  // stride-1 3x3: the LDS-DMA conv on flipped weights, plain store / accumulate
         float* wp = c.w<float>(c.d.wpk);
         const bool wino = wino_geometry(c.p.B, IH, IW, cout, cin, nullptr);
@@ -385,6 +390,7 @@ int conv_dgrad(const Ctx& c, int layer, const float* dy, int cout, int OH, int O
     a.bf16 = c.d.bf16;
     a.wpack = c.w<void>(c.d.wpk16);
     a.dyn = dyn;
+    a.par_out = par_out;
     Scope sc(&c.p.prof, c.s, "conv_dgrad", layer);
     return launch_convg(a, c.s);
 }
@@ -710,12 +716,20 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
                              "copy shortcut grad"));
             acc = 1;
         }
-        RC(conv_dgrad(c, L, dy1, k.cout, k.Ho, k.Wo, 3, k.stride, 1, P[q], da, k.cin, k.Hi, k.Wi, acc, k.dma1, dyn1));
+        // stride 2 on the channel-last engine: the parity classes go dense into class planes (the
+        // shortcut's class accumulates there too), then one pass interleaves them into da
+        float* ptmp = k.planar ? c.w<float>(d.partmp) : nullptr;
+        RC(conv_dgrad(c, L, dy1, k.cout, k.Ho, k.Wo, 3, k.stride, 1, P[q], da, k.cin, k.Hi, k.Wi, k.planar ? 0 : acc,
+                      k.dma1, dyn1, ptmp));
         if (k.sc) {
             RC(conv_wgrad(c, 100 + i, a_in, k.cin, k.Hi, k.Wi, 1, k.stride, 0, dysc, k.cout, k.Ho, k.Wo, G[q + 8],
                           G[q + 9], nullptr, nullptr, nullptr, nullptr, an, dyn2));
             RC(conv_dgrad(c, 100 + i, dysc, k.cout, k.Ho, k.Wo, 1, k.stride, 0, P[q + 8], da, k.cin, k.Hi, k.Wi, 1,
-                          false, dyn2));
+                          false, dyn2, ptmp));
+        }
+        if (k.planar) {
+            Scope sc(&p.prof, s, "dgrad_interleave", L);
+            RC(launch_par_interleave(ptmp, da, B, k.cin, k.Hi, k.Wi, acc, s));
         }
         dout = da;
         masked = false;

@@ -274,7 +274,15 @@ struct ConvGArgs {
     // (modes 1, 2) written by launch_to_nhwc; when set, the channel-last engine (convn.hip) runs
     const void* xn;
     const void* dyn;
+    // mode 1 stride 2 on the channel-last engine (optional): the four parity classes are written
+    // dense, class-planar, into par_out (class q at par_off(q), [B][cin][IHc][IWc] each; together the
+    // size of dx) instead of every other element of dx; launch_par_interleave then writes dx
+    float* par_out;
 };
+// offset of parity class q's dense planes inside a class-planar buffer (see ConvGArgs::par_out)
+int64_t par_off(int B, int C, int IH, int IW, int q);
+// dx[b][c][ih][iw] (=|+=) class-planar src (classes of (ih % 2, iw % 2))
+int launch_par_interleave(const float* src, float* dx, int B, int C, int IH, int IW, int accumulate, hipStream_t s);
 // NCHW float32 -> zero-padded NHWC bf16 (convn.hip), optionally through the BN backward or the
 // BN + residual + ReLU + dropout activation on the way
 enum NhwcOp {
