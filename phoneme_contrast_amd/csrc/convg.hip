@@ -316,6 +316,7 @@ __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
         if (col >= N) continue;
         int64_t obase;
         int64_t ostride;  // distance between consecutive rows (M index)
+        float* dst = a.out;
         if (MODE == 0) {
             const int64_t b = col / OHW;
             obase = b * a.cout * OHW + (col - b * OHW);
@@ -326,9 +327,15 @@ __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
             ostride = IHW;
         } else if (MODE == 3) {
             const int64_t b = col / CHW, p = col - b * CHW;
-            const int ihc = (int)(p / IWc), iwc = (int)(p - (int64_t)(p / IWc) * IWc);
-            obase = b * a.cin * IHW + (int64_t)(2 * ihc + ph) * a.IW + 2 * iwc + pw;
-            ostride = IHW;
+            if (a.par_out) {  // dense class planes
+                dst = a.par_out;
+                obase = b * a.cin * CHW + p;
+                ostride = CHW;
+            } else {
+                const int ihc = (int)(p / IWc), iwc = (int)(p - (int64_t)(p / IWc) * IWc);
+                obase = b * a.cin * IHW + (int64_t)(2 * ihc + ph) * a.IW + 2 * iwc + pw;
+                ostride = IHW;
+            }
         } else {  // column (tap, c) -> the reference weight layout [cout][cin][KH][KW]
             const int tap = (int)(col / a.cin), c = (int)(col - (int64_t)tap * a.cin);
             obase = (int64_t)slice * M * N + (int64_t)c * KK + tap;
@@ -340,7 +347,7 @@ __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
             for (int r = 0; r < 16; ++r) {
                 const int64_t row = m0 + wr * 32 * WM + mi * 32 + acc_row(r, h);
                 if (row < M) {
-                    float* o = a.out + obase + row * ostride;
+                    float* o = dst + obase + row * ostride;
                     if ((MODE == 1 || MODE == 3) && a.accumulate) *o += acc[mi][ni][r];
                     else *o = acc[mi][ni][r];
                 }
@@ -835,8 +842,8 @@ size_t convg_wpack_bytes(int mode, int cin, int cout, int k) {
 int launch_convg(ConvGArgs a, hipStream_t s) {
     PCX_CHECK_ARG(a.stride == 1 || a.stride == 2, "convg: stride %d unsupported", a.stride);
     PCX_CHECK_ARG(a.B > 0 && a.cin > 0 && a.cout > 0, "convg: empty tensor");
-    PCX_CHECK_ARG(!a.par_out || ((a.mode == 1 || a.mode == 3) && a.stride == 2 && a.bf16 && a.dyn),
-                  "convg: class-planar output only for the channel-last stride-2 data gradient");
+    PCX_CHECK_ARG(!a.par_out || ((a.mode == 1 || a.mode == 3) && a.stride == 2 && (!a.bf16 || a.dyn)),
+                  "convg: class-planar output only for the stride-2 data gradient (fp32 or channel-last)");
     if (a.mode == 1 && a.stride == 2) {
         for (int par = 0; par < 4; ++par) {  // each parity class of dx written exactly once
             ConvGArgs c = a;

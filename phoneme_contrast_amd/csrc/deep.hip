@@ -31,7 +31,7 @@ struct DeepBlock {
     // precision "bf16" with channel counts the channel-last engine takes (convn.hip): padded NHWC
     // bf16 images of the block input (conv1, shortcut) and of d1 (conv2), kept for the backward
     bool cn;
-    bool planar;                   // stride-2 data gradient through class-planar planes (channel-last)
+    bool planar;                   // stride-2 data gradient through class-planar planes
     size_t an, d1n;
 };
 
@@ -157,7 +157,7 @@ int build_deep(Plan& p) {
         wg_need(k.cout, k.cout, 3, k.Ho, k.Wo);
         if (k.sc) wg_need(k.cin, k.cout, 1, k.Ho, k.Wo);
         k.cn = d.bf16 && k.cin % 32 == 0 && k.cout % 32 == 0;
-        k.planar = k.cn && k.stride == 2 && (int64_t)planes(B, k.cin, k.Hi, k.Wi) < ((int64_t)1 << 31);
+        k.planar = (k.cn || !d.bf16) && k.stride == 2 && (int64_t)planes(B, k.cin, k.Hi, k.Wi) < ((int64_t)1 << 31);
         if (k.planar) partmax = std::max(partmax, (size_t)planes(B, k.cin, k.Hi, k.Wi) * 4);
         k.an = k.d1n = 0;
         if (k.cn) {
@@ -716,7 +716,7 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
                              "copy shortcut grad"));
             acc = 1;
         }
-        // stride 2 on the channel-last engine: the parity classes go dense into class planes (the
+        // stride 2 (fp32 / channel-last engines): the parity classes go dense into class planes (the
         // shortcut's class accumulates there too), then one pass interleaves them into da
         float* ptmp = k.planar ? c.w<float>(d.partmp) : nullptr;
         RC(conv_dgrad(c, L, dy1, k.cout, k.Ho, k.Wo, 3, k.stride, 1, P[q], da, k.cin, k.Hi, k.Wi, k.planar ? 0 : acc,

@@ -274,7 +274,7 @@ struct ConvGArgs {
     // (modes 1, 2) written by launch_to_nhwc; when set, the channel-last engine (convn.hip) runs
     const void* xn;
     const void* dyn;
-    // mode 1 stride 2 on the channel-last engine (optional): the four parity classes are written
+    // mode 1 stride 2, fp32 or the channel-last engine (optional): the four parity classes are written
     // dense, class-planar, into par_out (class q at par_off(q), [B][cin][IHc][IWc] each; together the
     // size of dx) instead of every other element of dx; launch_par_interleave then writes dx
     float* par_out;
