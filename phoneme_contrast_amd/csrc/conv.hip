@@ -355,6 +355,105 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(StemArgs a) {
     if (threadIdx.x == 0) a.partn[blockIdx.x] = n;
 }
 
+// bf16 precision, cout = 64: the 7x7 stem as a bf16 MFMA GEMM per 32-pixel tile (v_mfma_f32_32x32x16_bf16),
+// C[cout][pixel] = W[cout][tap] x im2col[tap][pixel] with fp32 accumulation.  The operands are the values
+// stem_fwd_kernel<true> multiplies (x and w rounded to bf16), so only the summation order differs.
+// K = 64 is an 8 x 8 tap grid (dh = 2s + h, dw = j for K-step s, lane half h, element j; dh or dw = 7 carry
+// zero weights), which makes every B offset lane-uniform: element j of K-step s is xs[2s RW + j] from the
+// lane's (pixel, h) base.  Per tile: 32 LDS reads, 8 MFMAs, 32 coalesced 128-byte row stores; BN partials
+// as stem_fwd_kernel's (per-block shift = the outputs of the block's first pixel, sum and M2).
+typedef __bf16 st_bf16x8 __attribute__((ext_vector_type(8)));
+
+__global__ __launch_bounds__(256) void stem_fwd_mfma_kernel(StemArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float xs[];  // (H + 7) rows: one spare zero row for dh = 7
+    __shared__ float red[2][64][2];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
+    const int mt = wave >> 1, wt = wave & 1;  // waves 2 mt, 2 mt + 1: couts 32 mt .. 32 mt + 31, alternate tiles
+    const int H = a.H, W = a.W, HW = H * W, RW = st_rw(W);
+    st_bf16x8 A[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int dh = 2 * s + h, dw = j;
+            A[s][j] = (__bf16)((dh < ST_K && dw < ST_K) ? a.w[(32 * mt + l32) * ST_T + dh * ST_K + dw] : 0.f);
+        }
+    for (int i = threadIdx.x; i < (H + 7) * RW; i += 256) xs[i] = 0.f;
+    const int ntile = (HW + 31) >> 5;
+    auto tile = [&](int tt, int& p) {
+        p = tt * 32 + l32;
+        const int pc = min(p, HW - 1);
+        const int hh = pc / W, ww = pc - hh * W;
+        const float* xb = xs + (hh + h) * RW + ww + 1;
+        f32x16 acc = {0.f};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            st_bf16x8 Bv;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) Bv[j] = (__bf16)xb[2 * s * RW + j];
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[s], Bv, acc, 0, 0, 0);
+        }
+        return acc;
+    };
+    float K[16], s1[16], s2[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s1[r] = s2[r] = 0.f;
+    int nsamp = 0;
+    for (int b = blockIdx.x; b < a.B; b += gridDim.x, ++nsamp) {
+        __syncthreads();
+        st_stage<true>(a.x + (int64_t)b * HW, H, W, xs);
+        __syncthreads();
+        if (b == (int)blockIdx.x) {  // shift: every wave evaluates the block's first pixel itself
+            int p;
+            const f32x16 acc = tile(0, p);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) K[r] = __shfl(acc[r], 32 * h, 64);
+        }
+        float* ob = a.out + ((int64_t)b * a.cout + 32 * mt) * HW;
+        for (int tt = wt; tt < ntile; tt += 2) {
+            int p;
+            const f32x16 acc = tile(tt, p);
+            if (p < HW) {
+                float* op = ob + p;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float v = acc[r];
+                    op[acc_row(r, h) * HW] = v;
+                    const float d = v - K[r];
+                    s1[r] += d;
+                    s2[r] = fmaf(d, d, s2[r]);
+                }
+            }
+        }
+    }
+    // per channel: the 32 pixel lanes of each half, then the two waves of the cout half
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        float t1 = s1[r], t2 = s2[r];
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) {
+            t1 += __shfl_xor(t1, o, 64);
+            t2 += __shfl_xor(t2, o, 64);
+        }
+        if (l32 == 0) {
+            red[wt][32 * mt + acc_row(r, h)][0] = t1;
+            red[wt][32 * mt + acc_row(r, h)][1] = t2;
+        }
+    }
+    __syncthreads();
+    const float n = (float)nsamp * (float)HW;
+    if (wt == 0 && l32 == 0) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int c = 32 * mt + acc_row(r, h);
+            const float t1 = red[0][c][0] + red[1][c][0], t2 = red[0][c][1] + red[1][c][1];
+            a.part0[(int64_t)c * a.nblk + blockIdx.x] = n * K[r] + t1;
+            a.part1[(int64_t)c * a.nblk + blockIdx.x] = n > 0.f ? fmaxf(t2 - t1 * t1 / n, 0.f) : 0.f;
+        }
+    }
+    if (threadIdx.x == 0) a.partn[blockIdx.x] = n;
+}
+
 template <bool BF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void stem_wgrad_kernel(StemArgs a) {
     extern __shared__ __attribute__((aligned(16))) float xs[];
@@ -544,6 +643,14 @@ int launch_stem_fwd(StemArgs a, int bf16, float* wround, hipStream_t s) {
         a.w = wround;
     }
     const size_t sm = stem_smem(a.H, a.W);
+    if (bf16 && a.cout == 64 && (size_t)(a.H + 7) * st_rw(a.W) * 4 <= 160 * 1024) {  // bf16 MFMA form
+        const size_t smm = (size_t)(a.H + 7) * st_rw(a.W) * 4;
+        (void)hipFuncSetAttribute((const void*)stem_fwd_mfma_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)smm);
+        stem_fwd_mfma_kernel<<<a.nblk, 256, smm, s>>>(a);
+        PCX_LAUNCH_CHECK("stem_fwd_mfma_kernel");
+        return PCX_OK;
+    }
 #define PCX_STEM_F(B_, C_)                                                                          \
     if ((bf16 != 0) == B_ && a.cout == 4 * C_) {                                                    \
         (void)hipFuncSetAttribute((const void*)stem_fwd_kernel<B_, C_>,                              \
