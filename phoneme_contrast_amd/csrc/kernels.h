@@ -127,7 +127,8 @@ struct StemArgs {
     int nblk, rows_per_blk;
 };
 int stem_nblk(int B, int H, int* rows_per_blk);
-int stem_wgrad_nslice(int B, int H, int* rows_per_slice);
+int stem_wgrad_nslice(int B, int H, int* rows_per_slice, bool mfma = false);
+bool stem_wgrad_mfma_ok(int cout, int H, int W);  // bf16: the MFMA weight-gradient form applies
 int launch_stem_fwd(StemArgs a, int bf16, float* wround, hipStream_t s);  // wround: [cout][49] scratch (bf16)
 int launch_stem_wgrad(StemArgs a, int bf16, hipStream_t s);
 
