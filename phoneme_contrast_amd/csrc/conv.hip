@@ -454,20 +454,21 @@ __global__ __launch_bounds__(256) void stem_fwd_mfma_kernel(StemArgs a) {
     if (threadIdx.x == 0) a.partn[blockIdx.x] = n;
 }
 
-// bf16 precision, cout = 64, W % 8 == 0: the stem weight gradient as a bf16 MFMA GEMM,
+// bf16 precision, cout = 64: the stem weight gradient as a bf16 MFMA GEMM,
 // dW[cout][tap] = sum over pixels dy[cout][p] x[p + tap] (K = pixels), per block a slice of samples.
 // Wave w owns couts 32 (w >> 1) .. + 31 and every other 64-pixel chunk (w & 1).  dy = bf16(a dz + b y + c)
 // (the BN backward, as stem_wgrad_kernel<true> rounds it) is loaded pixel-contiguous (16-byte loads),
 // transposed through the wave's LDS tile [32 couts][64 pixels] and read back as the MFMA A operand
 // (8 pixels per lane); B = x of the staged sample at the 8 x 8 tap grid (dh = t >> 3, dw = t & 7 for
 // tap column t; dh or dw = 7 columns are dropped), 8 consecutive pixels of one image row per lane half.
+// The pixel (K) index runs over rows padded to WV = W rounded up to 8 (padding columns carry dy = 0).
 __global__ __launch_bounds__(256) void stem_wgrad_mfma_kernel(StemArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float xs[];  // (H + 7) rows of the sample
+    extern __shared__ __attribute__((aligned(16))) float xs[];  // (H + 8) rows of the sample
     __shared__ __attribute__((aligned(16))) __bf16 dyt[4][32][64 + 8];  // per wave (row pad: 16 bytes)
     __shared__ float red[2][32][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
     const int mt = wave >> 1, wt = wave & 1;
-    const int H = a.H, W = a.W, HW = H * W, RW = st_rw(W);
+    const int H = a.H, W = a.W, HW = H * W, RW = st_rw(W), WV = (W + 7) & ~7, HWV = H * WV;
     const int slice = blockIdx.x;
     const int b0 = slice * a.rows_per_blk, b1 = min(a.B, b0 + a.rows_per_blk);
     // BN-backward coefficients of the 4 couts this lane loads per row group (lane = 16 pixel quads x 4 couts)
@@ -488,8 +489,8 @@ __global__ __launch_bounds__(256) void stem_wgrad_mfma_kernel(StemArgs a) {
         boff[nt] = dh * RW + dw;
     }
     f32x16 acc[2] = {f32x16{0.f}, f32x16{0.f}};
-    for (int i = threadIdx.x; i < (H + 7) * RW; i += 256) xs[i] = 0.f;
-    const int nchunk = (HW + 63) >> 6;
+    for (int i = threadIdx.x; i < (H + 8) * RW; i += 256) xs[i] = 0.f;
+    const int nchunk = (HWV + 63) >> 6;
     for (int b = b0; b < b1; ++b) {
         __syncthreads();
         st_stage<true>(a.x + (int64_t)b * HW, H, W, xs);
@@ -497,26 +498,39 @@ __global__ __launch_bounds__(256) void stem_wgrad_mfma_kernel(StemArgs a) {
         const int64_t pb = ((int64_t)b * a.cout + 32 * mt) * HW;
         for (int ch = wt; ch < nchunk; ch += 2) {
             const int c0 = ch * 64;
-            // dy tile: lane (q, cg) loads pixels c0 + 4q .. + 3 of couts 4i + cg
+            // dy tile: lane (q, cg) loads virtual pixels c0 + 4q .. + 3 (one padded row) of couts 4i + cg
             const int pq = c0 + 4 * q;
-            const bool pv = pq < HW;  // (HW % 4 == 0: a quad is all in or all out)
+            const int qr = pq / WV, qc = pq - qr * WV;
+            const bool pv = qr < H;
+            const int nv = pv ? min(4, W - qc) : 0;  // real pixels of the quad (<= 0: padding)
+            const int64_t po = (int64_t)qr * W + qc;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
-                const int64_t o = pb + (int64_t)(4 * i + cg) * HW + (pv ? pq : 0);
-                const float4 z = ld4(a.dz + o), y = ld4(a.y + o);
-                const float zz[4] = {z.x, z.y, z.z, z.w}, yy[4] = {y.x, y.y, y.z, y.w};
+                const int64_t o = pb + (int64_t)(4 * i + cg) * HW;
+                float zz[4], yy[4];
+                if ((W & 3) == 0 && nv == 4) {
+                    const float4 z = ld4(a.dz + o + po), y = ld4(a.y + o + po);
+                    zz[0] = z.x; zz[1] = z.y; zz[2] = z.z; zz[3] = z.w;
+                    yy[0] = y.x; yy[1] = y.y; yy[2] = y.z; yy[3] = y.w;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        zz[e] = e < nv ? a.dz[o + po + e] : 0.f;
+                        yy[e] = e < nv ? a.y[o + po + e] : 0.f;
+                    }
+                }
                 __bf16* d = &dyt[wave][4 * i + cg][4 * q];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) d[e] = (__bf16)(pv ? fmaf(A1[i], zz[e], fmaf(A2[i], yy[e], A3[i])) : 0.f);
+                for (int e = 0; e < 4; ++e) d[e] = (__bf16)(e < nv ? fmaf(A1[i], zz[e], fmaf(A2[i], yy[e], A3[i])) : 0.f);
             }
             __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS writes done (wave-private tile)
             __builtin_amdgcn_wave_barrier();
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 const st_bf16x8 Av = *reinterpret_cast<const st_bf16x8*>(&dyt[wave][l32][16 * s + 8 * h]);
-                // this lane half's 8 pixels (one image row: W % 8 == 0)
-                const int p = min(c0 + 16 * s + 8 * h, HW - 8);
-                const int hh = p / W, ww = p - hh * W;
+                // this lane half's 8 virtual pixels (one padded row; past the image: dy = 0 there)
+                const int p = min(c0 + 16 * s + 8 * h, HWV - 8);
+                const int hh = p / WV, ww = p - hh * WV;
                 const float* xb = xs + hh * RW + ww + 1;
 #pragma unroll
                 for (int nt = 0; nt < 2; ++nt) {
@@ -764,14 +778,14 @@ int launch_stem_fwd(StemArgs a, int bf16, float* wround, hipStream_t s) {
 }
 
 bool stem_wgrad_mfma_ok(int cout, int H, int W) {
-    return cout == 64 && W % 8 == 0 && (H * W) % 8 == 0 && (size_t)(H + 7) * st_rw(W) * 4 + 48 * 1024 <= 160 * 1024;
+    return cout == 64 && (size_t)(H + 8) * st_rw(W) * 4 + 48 * 1024 <= 160 * 1024;
 }
 
 int launch_stem_wgrad(StemArgs a, int bf16, hipStream_t s) {
     PCX_CHECK_ARG(a.cout % ST_WCPW == 0, "stem: cout %d must be even", a.cout);
     PCX_CHECK_ARG(stem_smem(a.H, a.W) <= 160 * 1024, "stem: %dx%d input too large", a.H, a.W);
     if (bf16 && stem_wgrad_mfma_ok(a.cout, a.H, a.W)) {  // bf16 MFMA form: one block per slice
-        const size_t smm = (size_t)(a.H + 7) * st_rw(a.W) * 4;
+        const size_t smm = (size_t)(a.H + 8) * st_rw(a.W) * 4;
         (void)hipFuncSetAttribute((const void*)stem_wgrad_mfma_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)smm);
         stem_wgrad_mfma_kernel<<<(unsigned)a.nblk, 256, smm, s>>>(a);
