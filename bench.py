@@ -279,7 +279,7 @@ def main():
     ddp.broadcast_module(model)
     opt = FusedAdam(model.parameters(), lr=3e-4, weight_decay=1e-4)
     bucketer = None
-    if world > 1:  # buckets all-reduced on a side stream behind the native backward
+    if ddp.is_distributed():  # buckets all-reduced on a side stream behind the native backward
         mb = args.bucket_mb if args.bucket_mb is not None else (4.0 if deep else 0.5)
         bucketer = ddp.GradBucketer(model, bucket_bytes=int(mb * (1 << 20)))
     loss_fn = (GlobalSupervisedContrastiveLoss if args.global_supcon else SupervisedContrastiveLoss)(temperature=0.15)
@@ -293,7 +293,7 @@ def main():
         loss = loss_fn(e, labels)
         opt.zero_grad(set_to_none=True)
         loss.backward()
-        if world > 1:
+        if bucketer is not None:
             opt.step(flat_grads=bucketer.finish(), grad_scale=gscale)
         else:
             opt.step()
@@ -307,17 +307,17 @@ def main():
     timing = not args.no_kernel_timing
     if timing:
         model.kernel_profile(True)
-    if world > 1:
+    if ddp.is_distributed():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
     torch.cuda.synchronize()
-    if world > 1:
+    if ddp.is_distributed():
         torch.distributed.barrier()
     el = time.perf_counter() - t0
-    if world > 1:
+    if ddp.is_distributed():
         t = torch.tensor([el], device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         el = t.item()
@@ -326,11 +326,15 @@ def main():
     final_loss = loss.item()
 
     if rank != 0:
-        if world > 1:
+        if ddp.is_distributed():
             torch.distributed.destroy_process_group()
         return
 
     ms_step = 1000.0 * el / args.steps
+    nbuckets = len(bucketer.buckets(next(iter(model._plans.values())))) if bucketer is not None else 0
+    backend = torch.distributed.get_backend() if ddp.is_distributed() else None
+    if backend == "nccl":
+        backend = "rccl"  # torch's "nccl" backend is RCCL on ROCm
     value = world * B * args.steps / el
     costs = deep_kernel_costs(B, F, T) if deep else kernel_costs(B, F, T, D)
     bf16 = deep and args.precision == "bf16"
@@ -403,13 +407,15 @@ def main():
                                "grad all-reduce + Adam(lr 3e-4, wd 1e-4)",
                    "per_gpu_batch": B, "global_batch": B * world, "n_mfcc": F, "T": T,
                    "embedding_dim": D, "parallelism": f"dp{world}",
-                   "allreduce": None if world == 1 else f"{len(bucketer.buckets(next(iter(model._plans.values()))))} "
-                                                        "RCCL buckets behind the backward",
+                   "allreduce": None if bucketer is None else f"{nbuckets} {backend} buckets behind the backward",
+                   "allreduce_buckets": nbuckets,
+                   "dist_backend": backend,
                    "supcon": "global batch (embedding + coefficient all-gathers, anchor rows per rank)"
                              if args.global_supcon and world > 1 else "per rank (DDP-equivalent)"},
         "conv_algorithms": None if deep else {
             "conv_fwd / conv_dgrad L2-L6": "Winograd F(2x2,3x3) on fp32 MFMA (16 multiplies per 2x2 outputs: "
-                                           "4/9 of the direct conv's; exact fp32 arithmetic)",
+                                           "4/9 of the direct conv's; fp32 arithmetic, rounding differs from the direct "
+                                           "conv by 2-6e-6 of max|y|)",
             "wgrad L2-L6": "direct implicit GEMM on fp32 MFMA (pixel streams)"},
         "roofline": roof,
         "step_roofline": step_roof,
@@ -419,7 +425,7 @@ def main():
         "final_loss": round(final_loss, 5),
     }
     print(json.dumps(out), flush=True)
-    if world > 1:
+    if ddp.is_distributed():
         torch.distributed.destroy_process_group()
 
 

@@ -105,8 +105,8 @@ def forward(sd, x, train=True, masks=None, keep=None):
 def supcon(f, labels, temperature=0.07, base_temperature=0.07):
     """SupervisedContrastiveLoss, reduction='mean' (reference losses.py:41-86)."""
     b = f.shape[0]
-    m = (labels.view(-1, 1) == labels.view(1, -1)).float()
-    lm = 1.0 - torch.eye(b, dtype=f.dtype)
+    m = (labels.view(-1, 1) == labels.view(1, -1)).to(f.dtype)
+    lm = 1.0 - torch.eye(b, dtype=f.dtype, device=f.device)
     m = m * lm
     logits = f @ f.T / temperature
     logits = logits - logits.max(dim=1, keepdim=True)[0].detach()

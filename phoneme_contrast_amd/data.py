@@ -82,6 +82,15 @@ def parse_dataset(data_dir: Path, logger: Optional[logging.Logger] = None
     label_map = {lab: i for i, lab in enumerate(uniq)}
     log(f"Successfully parsed {len(paths)} files")
     log(f"Found {len(uniq)} unique phonemes: {uniq}")
+    count = lambda key, val: sum(1 for m in metas if m[key] == val)  # noqa: E731
+    log(f"Structure: CV={count('structure', 'CV')}, VCV={count('structure', 'VCV')}")
+    log(f"Gender: Male={count('gender', 'male')}, Female={count('gender', 'female')}")
+    vowels = {}
+    for m in metas:
+        if m["structure"] == "CV" and m["vowel_context"] != "unknown":
+            vowels[m["vowel_context"]] = vowels.get(m["vowel_context"], 0) + 1
+    if vowels:
+        log(f"CV vowel contexts: {vowels}")
     return paths, [label_map[lab] for lab in labels], label_map, metas
 
 
@@ -111,50 +120,125 @@ def read_wav(path: Path) -> Tuple[np.ndarray, int]:
         return (x[None] if x.ndim == 1 else x.T).copy(), sr
 
 
-def pad_or_trim(w: np.ndarray, max_samples: int, mode: str) -> np.ndarray:
+def pad_or_trim(w: np.ndarray, max_samples: int, mode: str, rng: Optional[random.Random] = None) -> np.ndarray:
     """Random crop / random left pad for training, centred for validation (dataset.py:174-203;
-    the reference draws from Python's global `random`)."""
+    the reference draws from Python's global `random`, here from `rng` when given)."""
+    rnd = rng if rng is not None else random
     length = w.shape[-1]
     if length > max_samples:
-        start = random.randint(0, length - max_samples) if mode == "train" else (length - max_samples) // 2
+        start = rnd.randint(0, length - max_samples) if mode == "train" else (length - max_samples) // 2
         return w[..., start:start + max_samples]
     if length < max_samples:
         pad = max_samples - length
-        left = random.randint(0, pad) if mode == "train" else pad // 2
+        left = rnd.randint(0, pad) if mode == "train" else pad // 2
         return np.pad(w, [(0, 0)] * (w.ndim - 1) + [(left, pad - left)])
     return w
 
 
-class WaveformStore:
-    """Fixed-length mono clips [N, S] resident on one device, with their integer labels."""
+def _mix64(x: np.ndarray) -> np.ndarray:
+    """splitmix64 finaliser (uint64 -> uint64), vectorised."""
+    x = x.astype(np.uint64)
+    with np.errstate(over="ignore"):
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return x ^ (x >> np.uint64(31))
 
-    def __init__(self, waves: torch.Tensor, labels: Sequence[int], metadata: Optional[List[Dict]] = None):
-        if waves.dim() != 2:
-            raise ValueError(f"waveforms must be [N, samples], got {tuple(waves.shape)}")
-        self.waves = waves.contiguous().float()
+
+def crop_shifts(lengths: np.ndarray, max_samples: int, seed: int, epoch: int, indices: np.ndarray) -> np.ndarray:
+    """Per-clip source shift of the train-mode random crop / left pad: output sample j of clip i
+    reads source sample j + shift_i (crop: shift = start in [0, len - max]; pad: shift = -left with
+    left in [0, max - len]), each drawn uniformly from a counter hash of (seed, epoch, clip index),
+    so every rank and every run draws the same crops."""
+    lengths = np.asarray(lengths, np.int64)
+    span = np.abs(lengths - max_samples)
+    key = _mix64(np.uint64((int(seed) * 0x9E3779B97F4A7C15 + int(epoch)) & ((1 << 64) - 1)))
+    h = _mix64(key ^ (np.asarray(indices, np.uint64) * np.uint64(0xD1B54A32D192ED03)))
+    draw = (h % (span.astype(np.uint64) + np.uint64(1))).astype(np.int64)
+    return np.where(lengths > max_samples, draw, -draw)
+
+
+class WaveformStore:
+    """Mono clips resident on one device, with their integer labels.
+
+    Either fixed-length clips `waves` [N, S] (synthetic stores, validation, small train sets), or
+    for a train set of >= 500 files the uncropped clips `raw` [N, L_max] with their `lengths`: the
+    reference reloads and re-crops such a set on every __getitem__ (dataset.py:57-59,113-145), so
+    `clips(indices, epoch)` draws a fresh crop / left pad per clip and epoch on the device
+    (crop_shifts).  Below 500 files the reference caches the first crop, and so does this store
+    (drawn once, at load)."""
+
+    def __init__(self, waves: Optional[torch.Tensor], labels: Sequence[int], metadata: Optional[List[Dict]] = None,
+                 raw: Optional[torch.Tensor] = None, lengths: Optional[Sequence[int]] = None,
+                 max_samples: Optional[int] = None, seed: int = 0):
+        if raw is None:
+            if waves is None or waves.dim() != 2:
+                raise ValueError(f"waveforms must be [N, samples], got {None if waves is None else tuple(waves.shape)}")
+            self.waves = waves.contiguous().float()
+            self.max_samples = self.waves.shape[1]
+        else:
+            self.waves = None
+            self.raw = raw.contiguous().float()
+            self.lengths = np.asarray(lengths, np.int64)
+            self.max_samples = int(max_samples)
+            self.seed = int(seed)
         self.labels = [int(v) for v in labels]
         self.metadata = metadata or [{} for _ in self.labels]
 
     def __len__(self):
         return len(self.labels)
 
-    @classmethod
-    def from_files(cls, file_paths, labels, metadata, target_sr, max_samples, mode, device):
-        """Load + mono + pad/trim once (dataset.py:113-145).  Resampling to target_sr uses
+    @property
+    def recrops(self) -> bool:
+        return self.waves is None
+
+    def clips(self, indices: torch.Tensor, epoch: int = 0) -> torch.Tensor:
+        """[n, max_samples] clips of `indices` (a device LongTensor) for this epoch."""
+        if self.waves is not None:
+            return self.waves.index_select(0, indices)
+        idx_np = indices.cpu().numpy()
+        shift = torch.as_tensor(crop_shifts(self.lengths[idx_np], self.max_samples, self.seed, epoch, idx_np),
+                                device=self.raw.device)
+        ln = torch.as_tensor(self.lengths[idx_np], device=self.raw.device)
+        src = torch.arange(self.max_samples, device=self.raw.device)[None, :] + shift[:, None]
+        valid = (src >= 0) & (src < ln[:, None])
+        rows = self.raw.index_select(0, indices)
+        out = rows.gather(1, src.clamp(0, self.raw.shape[1] - 1))
+        return out * valid
+
+    @staticmethod
+    def _load_mono(path, target_sr) -> np.ndarray:
+        """Load + resample + mono (dataset.py:126-136) -> float32 [samples].  Resampling uses
         scipy's polyphase filter (torchaudio's sinc resampler is not in this image: values of a
         resampled clip are not bit-exact with the reference's)."""
-        out = np.zeros((len(file_paths), max_samples), np.float32)
-        for i, f in enumerate(file_paths):
-            x, sr = read_wav(f)
-            if sr != target_sr:
-                from math import gcd
+        x, sr = read_wav(path)
+        if sr != target_sr:
+            from math import gcd
 
-                from scipy.signal import resample_poly
-                g = gcd(int(sr), int(target_sr))
-                x = resample_poly(x, target_sr // g, sr // g, axis=-1).astype(np.float32)
-            if x.shape[0] > 1:
-                x = x.mean(axis=0, keepdims=True)
-            out[i] = pad_or_trim(x, max_samples, mode)[0]
+            from scipy.signal import resample_poly
+            g = gcd(int(sr), int(target_sr))
+            x = resample_poly(x, target_sr // g, sr // g, axis=-1).astype(np.float32)
+        if x.shape[0] > 1:
+            x = x.mean(axis=0, keepdims=True)
+        return x[0]
+
+    @classmethod
+    def from_files(cls, file_paths, labels, metadata, target_sr, max_samples, mode, device, seed=0):
+        """Load every clip of the split once (dataset.py:113-145).  Validation: centred crop / pad
+        (deterministic).  Train with < 500 files: one seeded random crop / pad per clip, kept (the
+        reference's cached path).  Train with >= 500 files: the uncropped clips stay in HBM and
+        every epoch draws new crops (`clips`)."""
+        mono = [cls._load_mono(f, target_sr) for f in file_paths]
+        if mode == "train" and len(mono) >= 500:
+            lmax = max(max_samples, max((len(m) for m in mono), default=0))
+            raw = np.zeros((len(mono), lmax), np.float32)
+            for i, m in enumerate(mono):
+                raw[i, :len(m)] = m
+            return cls(None, labels, metadata, raw=torch.from_numpy(raw).to(device),
+                       lengths=[len(m) for m in mono], max_samples=max_samples, seed=seed)
+        rng = random.Random(int(seed))
+        out = np.zeros((len(mono), max_samples), np.float32)
+        for i, m in enumerate(mono):
+            out[i] = pad_or_trim(m[None], max_samples, mode, rng)[0]
         return cls(torch.from_numpy(out).to(device), labels, metadata)
 
     @classmethod
@@ -181,9 +265,15 @@ class WaveformStore:
         return cls(waves, labels.tolist())
 
     def subset(self, indices: Sequence[int]) -> "WaveformStore":
-        idx = torch.as_tensor(list(indices), dtype=torch.long, device=self.waves.device)
-        return WaveformStore(self.waves.index_select(0, idx), [self.labels[i] for i in indices],
-                             [self.metadata[i] for i in indices])
+        indices = list(indices)
+        labels, meta = [self.labels[i] for i in indices], [self.metadata[i] for i in indices]
+        if self.waves is not None:
+            idx = torch.as_tensor(indices, dtype=torch.long, device=self.waves.device)
+            return WaveformStore(self.waves.index_select(0, idx), labels, meta)
+        idx = torch.as_tensor(indices, dtype=torch.long, device=self.raw.device)
+        return WaveformStore(None, labels, meta, raw=self.raw.index_select(0, idx),
+                             lengths=self.lengths[np.asarray(indices, np.int64)], max_samples=self.max_samples,
+                             seed=self.seed)
 
 
 # ----------------------------------------------------------------------------- batching
@@ -225,15 +315,19 @@ class GpuContrastiveBatches:
     def __init__(self, store: WaveformStore, batch_sampler, builder: GpuViewBuilder):
         self.store, self.batch_sampler, self.builder = store, batch_sampler, builder
         self.dataset = _Sized(len(store), store.labels)
+        self.epoch = 0  # counts passes: the re-cropping store draws new crops per pass
 
     def __len__(self):
         return len(self.batch_sampler)
 
     def __iter__(self):
-        dev = self.store.waves.device
+        store = self.store
+        dev = (store.waves if store.waves is not None else store.raw).device
+        epoch = self.epoch
+        self.epoch += 1
         for idx in self.batch_sampler:
             ix = torch.as_tensor([int(i) for i in idx], dtype=torch.long, device=dev)
-            views = self.builder(self.store.waves.index_select(0, ix), [int(i) for i in idx])
+            views = self.builder(store.clips(ix, epoch), [int(i) for i in idx])
             labels = torch.as_tensor([self.store.labels[int(i)] for i in idx], dtype=torch.long)
             yield {"views": views, "label": labels, "index": ix}
 
@@ -249,8 +343,10 @@ class GpuEvalBatches:
         return (len(self.store) + self.batch_size - 1) // self.batch_size
 
     def __iter__(self):
-        for s in range(0, len(self.store), self.batch_size):
-            idx = list(range(s, min(len(self.store), s + self.batch_size)))
-            views = self.builder(self.store.waves[s:idx[-1] + 1], idx)
+        store = self.store
+        dev = (store.waves if store.waves is not None else store.raw).device
+        for s in range(0, len(store), self.batch_size):
+            idx = list(range(s, min(len(store), s + self.batch_size)))
+            views = self.builder(store.clips(torch.as_tensor(idx, dtype=torch.long, device=dev), 0), idx)
             labels = torch.as_tensor(self.store.labels[s:idx[-1] + 1], dtype=torch.long)
             yield {"views": views, "label": labels, "index": torch.as_tensor(idx)}

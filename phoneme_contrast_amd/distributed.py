@@ -12,6 +12,7 @@ RCCL on ROCm; "gloo" serves the CPU tests and the N-ranks-on-one-GPU rehearsal.
 """
 import ctypes
 import os
+import weakref
 
 import torch
 import torch.distributed as dist
@@ -25,10 +26,12 @@ def world():
 
 def init_from_env(backend=None):
     """Initialise the process group from torchrun's env (RANK, WORLD_SIZE, LOCAL_RANK,
-    MASTER_ADDR/PORT).  Returns (rank, world_size, local_rank); no-op for a single process."""
+    MASTER_ADDR/PORT).  Returns (rank, world_size, local_rank); no-op for a single process unless
+    PCX_DIST_FORCE_INIT=1 (a world-1 group: runs the RCCL bucket path on a one-GPU box, where two
+    RCCL ranks cannot share the device)."""
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     lr = int(os.environ.get("LOCAL_RANK", "0"))
-    if ws <= 1:
+    if ws <= 1 and os.environ.get("PCX_DIST_FORCE_INIT") != "1":
         return 0, 1, lr
     if backend is None:  # PCX_DIST_BACKEND=gloo rehearses N ranks on one GPU (tests only)
         backend = os.environ.get("PCX_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
@@ -58,6 +61,11 @@ def broadcast_module(module: torch.nn.Module, src: int = 0):
         return
     for t in list(module.parameters()) + list(module.buffers()):
         dist.broadcast(t.data, src)
+
+
+def is_distributed() -> bool:
+    """A process group is up (any world size, including a forced world-1 group)."""
+    return dist.is_available() and dist.is_initialized()
 
 
 def allreduce_flat(flat: torch.Tensor):
@@ -112,7 +120,7 @@ class GradBucketer:
         self.offsets = [0]
         for n in self.sizes:
             self.offsets.append(self.offsets[-1] + n)
-        self._plans = {}
+        self._plans = weakref.WeakKeyDictionary()  # plan -> bucket first-parameter indices
         self._works = []
         self._flat = None
         self._stream = None
@@ -124,7 +132,7 @@ class GradBucketer:
 
     def _configure(self, plan):
         from . import _lib
-        key = id(plan)
+        key = plan
         firsts = self._plans.get(key)
         if firsts is not None:
             return firsts
@@ -160,7 +168,7 @@ class GradBucketer:
 
     def launch(self, plan, flat: torch.Tensor):
         from . import _lib
-        if world()[1] == 1:
+        if not is_distributed():
             return
         if self._stream is None or self._stream.device != flat.device:
             self._stream = torch.cuda.Stream(device=flat.device)
@@ -176,8 +184,12 @@ class GradBucketer:
     def pending(self) -> bool:
         return self._flat is not None
 
-    def finish(self):
-        """Wait (on the current stream) for every bucket of the last backward; returns [flat]."""
+    def finish(self, group_sizes=None):
+        """Wait (on the current stream) for every bucket of the last backward.  Returns the summed
+        gradient as one tensor per optimizer parameter group: `group_sizes` (element counts of the
+        groups, in parameter order; default one group) cuts the flat buffer into consecutive
+        slices, and a slice that does not start 16-byte aligned (pcx_adam_step's vector loads) is
+        returned as an aligned copy."""
         flat = self._flat
         if flat is None:
             return None
@@ -185,4 +197,13 @@ class GradBucketer:
             w.wait()
         torch.cuda.current_stream(flat.device).wait_stream(self._stream)
         self._works, self._flat = [], None
-        return [flat]
+        if group_sizes is None:
+            return [flat]
+        if sum(group_sizes) != flat.numel():
+            raise ValueError(f"parameter groups hold {sum(group_sizes)} elements, the gradient {flat.numel()}")
+        out, off = [], 0
+        for n in group_sizes:
+            g = flat[off:off + n]
+            out.append(g if g.data_ptr() % 16 == 0 else g.clone())
+            off += n
+        return out

@@ -181,6 +181,7 @@ class GlobalSupervisedContrastiveLoss(SupervisedContrastiveLoss):
                  reduction: str = "mean", group=None):
         super().__init__(temperature, base_temperature, reduction)
         self.group = group
+        self._checked_sizes = set()
 
     def forward(self, features: torch.Tensor, labels: torch.Tensor,
                 mask: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -201,10 +202,12 @@ class GlobalSupervisedContrastiveLoss(SupervisedContrastiveLoss):
             if labels.shape[0] != features.shape[0]:
                 raise ValueError("Num of labels does not match num of features")
         n = features.shape[0]
-        ext = torch.tensor([n, -n], device=features.device)  # (max, -min) in one collective
-        dist.all_reduce(ext, op=dist.ReduceOp.MAX, group=self.group)
-        if ext[0].item() != -ext[1].item():
-            raise ValueError("global mode: every rank must pass the same local batch size")
+        if n not in self._checked_sizes:  # once per local batch size: no per-step host sync
+            ext = torch.tensor([n, -n], device=features.device)  # (max, -min) in one collective
+            dist.all_reduce(ext, op=dist.ReduceOp.MAX, group=self.group)
+            if ext[0].item() != -ext[1].item():
+                raise ValueError("global mode: every rank must pass the same local batch size")
+            self._checked_sizes.add(n)
         return _GlobalSupConFn.apply(features, labels, mask, self.temperature, self.base_temperature,
                                      self.reduction, self.group)
 
@@ -220,6 +223,13 @@ class NTXentLoss(nn.Module):
 
     def forward(self, features: torch.Tensor, labels: torch.Tensor = None) -> torch.Tensor:
         if labels is not None:
+            if features.dim() == 2 and features.shape[0] == 1:
+                # the reference's labelled branch has no batch-size check (losses.py:114-151): a
+                # lone anchor has no positive and no other column, so its loss is -0/1 = -0.0 with
+                # a zero gradient (the SupCon kernels need B >= 2)
+                _lib.require_gpu(features, labels, what="NTXentLoss")
+                per = -(features * 0.0).sum(dim=1)
+                return per.mean() if self.reduction == "mean" else per.sum() if self.reduction == "sum" else per
             return supcon(features, labels, None, self.temperature, self.temperature,
                           self.reduction)
         if features.shape[0] % 2 != 0:

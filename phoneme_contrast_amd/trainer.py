@@ -126,15 +126,17 @@ class ContrastiveTrainer:
         from .optim import FusedAdam
         clip = self.config.get("gradient_clip_val")
         opt = self.optimizer
+        bucketer = getattr(self.model, "_grad_bucketer", None)
+        pending = bucketer is not None and bucketer.pending()
         if isinstance(opt, FusedAdam) and ddp.covers(opt, self.model):
             flats, scale = None, 1.0
+            if pending:  # buckets already summed behind the backward
+                flats = bucketer.finish([sum(p.numel() for p in g["params"]) for g in opt.param_groups])
+            elif self.world_size > 1:
+                flats = opt.flat_grad_views()
+                for f in flats:
+                    ddp.allreduce_flat(f)
             if self.world_size > 1:
-                bucketer = getattr(self.model, "_grad_bucketer", None)
-                flats = bucketer.finish() if bucketer is not None and bucketer.pending() else None
-                if flats is None:
-                    flats = opt.flat_grad_views()
-                    for f in flats:
-                        ddp.allreduce_flat(f)
                 scale = self._grad_scale()
             if clip:
                 if flats is None:
@@ -142,11 +144,15 @@ class ContrastiveTrainer:
                 ddp.clip_flat_(flats, float(clip), scale)
             opt.step(flat_grads=flats, grad_scale=scale)
             return
-        if self.world_size > 1:  # generic path: leave the AVERAGED gradient in p.grad
-            grads = [p.grad for p in self.model.parameters() if p.grad is not None]
-            flat = torch.cat([g.reshape(-1) for g in grads])
-            ddp.allreduce_flat(flat)
-            flat *= self._grad_scale()
+        grads = [p.grad for p in self.model.parameters() if p.grad is not None]
+        if pending or self.world_size > 1:  # generic path: leave the AVERAGED gradient in p.grad
+            if pending:  # the bucketer already summed the backward's flat buffer: no second reduce
+                flat = bucketer.finish()[0]
+            else:
+                flat = torch.cat([g.reshape(-1) for g in grads])
+                ddp.allreduce_flat(flat)
+            if self.world_size > 1:
+                flat = flat * self._grad_scale()
             off = 0
             for g in grads:
                 g.copy_(flat[off:off + g.numel()].view_as(g))

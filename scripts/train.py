@@ -53,7 +53,7 @@ def setup_data(cfg, logger, rank, world, device):
         store = WaveformStore.synthetic(s.num_classes, s.samples_per_class, s.get("clip_samples", max_samples),
                                         cfg.experiment.seed, device, target_sr)
         labels, n_classes = store.labels, s.num_classes
-        logger.info(f"Synthetic data: {len(store)} clips of {store.waves.shape[1]} samples, {n_classes} classes")
+        logger.info(f"Synthetic data: {len(store)} clips of {store.max_samples} samples, {n_classes} classes")
     else:
         file_paths, labels, label_map, metadata = parse_dataset(Path(cfg.data.data_path), logger)
         store, n_classes = None, len(label_map)
@@ -65,11 +65,13 @@ def setup_data(cfg, logger, rank, world, device):
         train_store, val_store = store.subset(train_idx), store.subset(val_idx)
         del store
     else:
+        seed = cfg.experiment.seed  # crops drawn from (seed, epoch, clip): identical on every rank
         train_store = WaveformStore.from_files([file_paths[i] for i in train_idx], [labels[i] for i in train_idx],
                                                [metadata[i] for i in train_idx], target_sr, max_samples, "train",
-                                               device)
+                                               device, seed=seed)
         val_store = WaveformStore.from_files([file_paths[i] for i in val_idx], [labels[i] for i in val_idx],
-                                             [metadata[i] for i in val_idx], target_sr, max_samples, "val", device)
+                                             [metadata[i] for i in val_idx], target_sr, max_samples, "val", device,
+                                             seed=seed)
     c = cfg.data.contrastive
     sampler = ContrastiveBatchSampler(labels=train_store.labels, classes_per_batch=c.classes_per_batch,
                                       samples_per_class=c.samples_per_class, views_per_sample=c.views_per_sample,
@@ -92,13 +94,15 @@ def setup_data(cfg, logger, rank, world, device):
 def setup_model(cfg, device, world=1):
     model = model_registry.create(cfg.model.type, dict(cfg.model)).to(device)
     ddp.broadcast_module(model)
-    if world > 1:  # gradient all-reduce in buckets behind the native backward
-        ddp.GradBucketer(model, bucket_bytes=int(cfg.accel.get("bucket_mb", 4) * (1 << 20)))
     wd = cfg.training.get("weight_decay", 0)
     if cfg.accel.get("fused_adam", True):
         optimizer = FusedAdam(model.parameters(), lr=cfg.training.learning_rate, weight_decay=wd)
     else:
         optimizer = torch.optim.Adam(model.parameters(), lr=cfg.training.learning_rate, weight_decay=wd)
+    if ddp.is_distributed() and isinstance(optimizer, FusedAdam) and ddp.covers(optimizer, model):
+        # gradient all-reduce in buckets behind the native backward, handed to the fused step;
+        # torch.optim.Adam takes the trainer's flat all-reduce into p.grad instead
+        ddp.GradBucketer(model, bucket_bytes=int(cfg.accel.get("bucket_mb", 4) * (1 << 20)))
     scheduler = None
     if cfg.training.get("use_scheduler", False):
         scheduler = torch.optim.lr_scheduler.CosineAnnealingLR(

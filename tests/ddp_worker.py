@@ -82,6 +82,48 @@ def run(name, case, cfg, bucketed, clip, rank, world, out):
         bucketer.detach()
 
 
+def run_groups(rank, world, out):
+    """FusedAdam with two parameter groups (different weight decay) behind the trainer: bucketed
+    (GradBucketer.finish cuts the summed buffer per group; group 1 starts at an unaligned offset)
+    and flat all-reduce must give bit-identical updates (finish() used to return one
+    buffer for every group)."""
+    from golden_util import model_case
+    from phoneme_contrast_amd import distributed as ddp
+    from phoneme_contrast_amd.losses import SupervisedContrastiveLoss
+    from phoneme_contrast_amd.models import model_registry
+    from phoneme_contrast_amd.optim import FusedAdam
+    from phoneme_contrast_amd.trainer import ContrastiveTrainer
+
+    c = model_case("cnn_small_T201")
+    for name, bucketed in (("groups_flat", False), ("groups_bucket", True)):
+        m = model_registry.create("phoneme_cnn", {"embedding_dim": 128, "use_attention": True, "dropout_rate": 0.1})
+        m.load_state_dict({k: torch.tensor(v) for k, v in c["state0"].items()})
+        m = m.cuda().train()
+        ps = list(m.parameters())
+        opt = FusedAdam([{"params": ps[:26]}, {"params": ps[26:], "weight_decay": 1e-3}], lr=c["lr"],
+                        weight_decay=c["weight_decay"])
+        loss_fn = SupervisedContrastiveLoss(temperature=c["temperature"])
+        trainer = ContrastiveTrainer(model=m, train_loader=[], val_loader=None, loss_fn=loss_fn, optimizer=opt,
+                                     scheduler=None, device=torch.device("cuda"), config={},
+                                     output_dir=tempfile.mkdtemp(prefix=f"ddp_{name}_{rank}_"),
+                                     logger=logging.getLogger("ddp_worker"))
+        bucketer = ddp.GradBucketer(m, bucket_bytes=1024) if bucketed else None
+        B = c["x"].shape[0]
+        lo, hi = ddp.shard(B, rank, world)
+        m.set_dropout_masks([torch.tensor(k[lo:hi]) for k in c["steps"][0]["masks"]])
+        loss = loss_fn(m(torch.tensor(c["x"][lo:hi]).cuda()), torch.tensor(c["labels"][lo:hi]).cuda())
+        opt.zero_grad()
+        loss.backward()
+        trainer._reduce_clip_step()
+        torch.cuda.synchronize()
+        for gi in range(2):
+            st = opt._flat[gi]
+            for key in ("flat", "m", "v"):
+                out[f"{name}/{gi}/{key}"] = st[key].cpu().numpy()
+        if bucketer:
+            bucketer.detach()
+
+
 def run_global(rank, world, out):
     """Global-batch SupCon (GlobalSupervisedContrastiveLoss): (a) the loss alone on this rank's rows
     of a seeded global embedding batch, reductions mean / none; (b) a cnn_small trainer step on the
@@ -135,6 +177,7 @@ def main():
     out = {}
     for sc in SCENARIOS:
         run(*sc, rank, world, out)
+    run_groups(rank, world, out)
     run_global(rank, world, out)
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **out)
     torch.distributed.barrier()

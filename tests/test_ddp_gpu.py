@@ -141,6 +141,15 @@ def test_ddp_deep_matches_oracle_and_bucketing_is_exact(ranks):
         assert np.array_equal(ranks[0][f"deep_flat/{key}"], ranks[0][f"deep_bucket/{key}"]), key
 
 
+def test_ddp_two_param_groups_bucketed_equals_flat(ranks):
+    for gi in range(2):
+        for key in ("flat", "m", "v"):
+            a = ranks[0][f"groups_bucket/{gi}/{key}"]
+            assert np.array_equal(a, ranks[0][f"groups_flat/{gi}/{key}"]), (gi, key)
+            assert np.array_equal(a, ranks[1][f"groups_bucket/{gi}/{key}"]), (gi, key)
+    assert ranks[0]["groups_flat/1/flat"].size > 1000  # projection (after the 1-element attention bias)
+
+
 def test_adam_grad_scale_matches_torch():
     """pcx_adam_step with grad_scale != 1 (the 1/world average) against torch.optim.Adam on the
     pre-scaled gradient."""

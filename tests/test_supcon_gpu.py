@@ -140,6 +140,25 @@ def test_supcon_errors_match_reference():
         NTXentLoss(0.5)(torch.randn(8, 128, device="cuda"))
 
 
+def test_ntxent_labelled_single_sample_is_zero_like_reference():
+    """The reference's labelled NT-Xent has no batch-size check (losses.py:114-151): at B = 1 the
+    anchor has no positive, so every reduction gives 0 (-0.0) and the gradient is zero."""
+    from phoneme_contrast_amd.losses import NTXentLoss
+    for red, shape in (("mean", ()), ("sum", ()), ("none", (1,))):
+        f = torch.nn.functional.normalize(torch.randn(1, 128, device="cuda"), dim=1).requires_grad_(True)
+        loss = NTXentLoss(0.5, reduction=red)(f, torch.tensor([3], device="cuda"))
+        assert tuple(loss.shape) == shape and float(loss.sum()) == 0.0
+        loss.sum().backward()
+        assert f.grad is not None and not f.grad.any()
+    # and B = 2 still runs the kernel (matches SupCon at base_T = T)
+    f = torch.nn.functional.normalize(torch.randn(2, 64, device="cuda"), dim=1)
+    lab = torch.tensor([1, 1], device="cuda")
+    s = float(NTXentLoss(0.5)(f, lab))
+    ref = -(float((f[0] * f[1]).sum()) / 0.5 - np.log(np.exp(float((f[0] * f[1]).sum()) / 0.5
+                                                                - 1.0 / 0.5) + 1e-6) - 1.0 / 0.5)
+    assert abs(s - ref) < 1e-4
+
+
 def test_adam_kernel_matches_torch():
     from phoneme_contrast_amd import _lib
     n = 304225
