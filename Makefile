@@ -8,12 +8,17 @@ OBJ = $(patsubst phoneme_contrast_amd/csrc/%.hip,build/%.o,$(SRC))
 HDR = $(wildcard phoneme_contrast_amd/csrc/*.h) include/pcx.h
 LIB = phoneme_contrast_amd/libpcx.so
 
-TOOLS = tools/wino_bench
+TOOLS = tools/wino_bench tools/ww_bench
 
 all: $(LIB) $(TOOLS)
 
 # engine cross-check / micro-benchmark (tests/test_wino_engine_gpu.py runs it)
 tools/wino_bench: tools/wino_bench.cpp $(LIB) $(HDR)
+	$(HIPCC) -O2 -std=c++17 --offload-arch=$(ARCH) -Iinclude $< -Lphoneme_contrast_amd -lpcx \
+	    -Wl,-rpath,'$$ORIGIN/../phoneme_contrast_amd' -o $@
+
+# Winograd weight gradient vs the pixel-stream kernel (tests/test_wino_engine_gpu.py runs it)
+tools/ww_bench: tools/ww_bench.cpp $(LIB) $(HDR)
 	$(HIPCC) -O2 -std=c++17 --offload-arch=$(ARCH) -Iinclude $< -Lphoneme_contrast_amd -lpcx \
 	    -Wl,-rpath,'$$ORIGIN/../phoneme_contrast_amd' -o $@
 

@@ -110,6 +110,26 @@ int launch_wgrad_w32(int pro, WgradArgs a, hipStream_t s);
 bool wgrad_s_geometry(int B, int H, int W, int cin, int cout, WgradArgs* a, int force_cw = 0);
 int launch_wgrad_s(int pro, WgradArgs a, hipStream_t s);
 
+// Winograd F(2x2,3x3) weight gradient of the stride-1 3x3 convs (wgrad_wino.hip): 32 x 32 channel
+// blocks, column strips of <= 50 tiles, W a multiple of 2; false if it does not apply
+struct WinoWgradArgs {
+    int B, H, W, cin, cout;
+    const float* dz;
+    const float* y;
+    const float4* cf_dy;  // {a, mb, mgi, mean}: dy = BN backward of (dz, y)
+    const float* src;     // x (raw, or the producer's y under PRO_BNRELU)
+    const float4* cf_x;
+    float* part;          // [nslice][cout][cin][16] Winograd-domain partials
+    float* dy_out;        // optional: dy written here by the cin-group-0 blocks
+    int S, nseg, V, XCS, DCS, nd, nx, Ksteps;  // strip tiles, strips per row, vector width, LDS strides, items
+    size_t lds;
+    int ntask, per_slice, nslice;
+};
+bool wgrad_wino_geometry(int B, int H, int W, int cin, int cout, WinoWgradArgs* a);
+int launch_wgrad_wino(int pro, WinoWgradArgs a, hipStream_t s);
+// dW [cout][cin][3][3] = G^T (sum of the slices) G, float64, fixed order
+int launch_wgrad_wino_reduce(const float* part, int nslice, int cout, int cin, float* dw, hipStream_t s);
+
 // PhonemeNetDeep 7x7 stem (Cin = 1, pad 3): direct forward + BN partials, weight gradient with the
 // BN backward of (dz, y) in its loads (conv.hip)
 struct StemArgs {

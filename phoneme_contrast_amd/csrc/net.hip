@@ -65,9 +65,14 @@ int build_small(Plan& p) {
             // the data gradient's tile blocks are the forward's (same H x W), so one nblk serves both
             L.nblk = L.wino ? (int)wino_nblk(B, L.H, L.W, L.cin, L.cout)
                             : (int)std::max(conv3x3_nblk(B, L.H, L.W, L.cout), conv3x3_nblk(B, L.H, L.W, L.cin));
-            PCX_CHECK_ARG(wgrad_s_geometry(B, L.H, L.W, L.cin, L.cout, &L.wg),
-                          "PhonemeNet: no weight-gradient geometry for layer %d (%dx%d)", l, L.H, L.W);
-            wg = std::max(wg, (size_t)L.wg.nslice * L.cout * L.cin * 9);
+            L.wgw = wgrad_wino_geometry(B, L.H, L.W, L.cin, L.cout, &L.ww);
+            if (L.wgw) {
+                wg = std::max(wg, (size_t)L.ww.nslice * L.cout * L.cin * 16);
+            } else {
+                PCX_CHECK_ARG(wgrad_s_geometry(B, L.H, L.W, L.cin, L.cout, &L.wg),
+                              "PhonemeNet: no weight-gradient geometry for layer %d (%dx%d)", l, L.H, L.W);
+                wg = std::max(wg, (size_t)L.wg.nslice * L.cout * L.cin * 9);
+            }
         } else {
             L.nblk = conv1_nblk(B, L.H, &p.conv1_rows);
             p.conv1_nblk = L.nblk;
@@ -320,7 +325,26 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
         // conv bias feeding a train-mode BN: exact gradient is zero (sum_b,h,w of BN-backward)
         RC(hip_status_ok(hipMemsetAsync(G[p_conv_b(l)], 0, L.cout * 4, s), "memset bias grad"));
         // ---- weight gradient
-        {
+        if (L.wgw) {
+            WinoWgradArgs w = L.ww;
+            w.B = B; w.H = L.H; w.W = L.W; w.cin = L.cin; w.cout = L.cout;
+            w.dz = at<float>(ws, L.dz);
+            w.y = at<float>(ws, L.y);
+            w.cf_dy = at<float4>(ws, L.cfb);
+            w.src = L.pooled_in ? at<float>(ws, L.xp) : at<float>(ws, Lp.y);
+            w.cf_x = at<float4>(ws, Lp.cf);
+            w.part = wgp;
+            w.dy_out = at<float>(ws, p.dyb);
+            {
+                Scope sc(&p.prof, s, "wgrad", l);
+                RC(launch_wgrad_wino(L.pooled_in ? PRO_RAW : PRO_BNRELU, w, s));
+            }
+            {
+                Scope sc(&p.prof, s, "wgrad_reduce", l);
+                RC(launch_wgrad_wino_reduce(wgp, w.nslice, L.cout, L.cin, G[p_conv_w(l)], s));
+            }
+            p.buckets.mark(p_conv_w(l), s);
+        } else {
             WgradArgs w = L.wg;
             w.B = B; w.H = L.H; w.W = L.W; w.cin = L.cin; w.cout = L.cout;
             w.dz = at<float>(ws, L.dz);

@@ -97,7 +97,9 @@ struct Layer {  // one 3x3 conv of the trunk (L = 1..6)
     int nblk;              // forward statistics tiles
     bool wino;             // Winograd conv (W >= 31); else the direct LDS-DMA conv (wu / wud then hold
                            // the [9][cin][cout] / flipped [9][cout][cin] packings)
-    WgradArgs wg;          // weight-gradient geometry
+    WgradArgs wg;          // weight-gradient geometry (pixel-stream kernel)
+    bool wgw;              // weight gradient on the Winograd kernel (wgrad_wino.hip) instead
+    WinoWgradArgs ww;
 };
 
 struct DeepPlan;  // deep.hip

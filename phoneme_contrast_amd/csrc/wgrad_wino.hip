@@ -1,0 +1,420 @@
+// Weight gradient of the stride-1 3x3 convs as Winograd F(2x2, 3x3) on v_mfma_f32_32x32x2_f32.
+//
+//   dW[n][c] = sum over 2x2 output tiles of the adjoint of Y = A^T [(G g G^T) (.) V] A:
+//   dW = G^T dU G,   dU_xi[n][c] = sum_tiles Yh_xi[n][tile] V_xi[c][tile]
+//   Yh = A dY A^T (4x4 from the tile's 2x2 output gradient dy),  V = B^T d B (4x4 input patch)
+//
+// (reference: autograd of the 3x3 convs of phoneme_cnn.py:35-65).  Per Winograd element xi the
+// tile sum is a GEMM over K = tiles with M = output channels (dy) and N = input channels (x): 16
+// multiplies per tile and channel pair instead of the direct form's 36, all in float32 (the
+// transforms are additions; dW = G^T dU G is evaluated in float64 from the summed partials).
+// Checked in float64 (tests/test_winograd_host.py); the signs of row / column 3 of A are folded
+// into the final transform (Yh' = Yh with row 3 and column 3 negated).
+//
+// Shape (MI355X):
+//  * block = 32 output x 32 input channels, 4 waves; wave q owns the 4 Winograd elements of row q
+//    of the 4x4 domain (xi = 4 q + e): 4 accumulator tiles of 32x32 (64 VGPRs), so the block's
+//    waves never duplicate an MFMA, and each wave needs only the two input rows (and the one or two
+//    dy rows) its row q combines: per K-step (2 tiles) 4 MFMAs against 4 + 2 ds_read_b64 and ~12 VALU.
+//  * K = tiles: lane l of a K-step takes tile 2 s + (l >> 5) of the current tile row strip, channel
+//    l & 31 on both operands (A = Yh (cout x tiles), B = V (tiles x cin)).
+//  * a block walks (sample, column strip) tasks tile row by tile row: dy rows 2 tr, 2 tr + 1 and x
+//    rows 2 tr - 1 .. 2 tr + 2 live in LDS (x in a 4-row ring: two rows carried to the next tile
+//    row), the next tile row's 2 + 2 rows are loaded into registers under the current row's MFMAs
+//    and stored after a barrier, the BN backward dy = A1 dz + A2 y + A3 and the producer's BN + ReLU
+//    applied between load and store; the cin-group-0 blocks also write dy to HBM for the data
+//    gradient.  Out-of-image items carry an out-of-range buffer offset (the hardware returns 0) and
+//    a zero additive term, so they stage exact zeros; padded tiles of a K-step read zeros.
+//  * x rows sit in LDS shifted by one column (position p <-> image column 2 t0 - 1 + p), so a patch
+//    is two aligned ds_read_b64 per row; channel strides are 2 * odd (the 32 lanes of a read group
+//    cover the 64 banks once).  Strips of <= 50 tiles keep the block at <= 80 KB: two blocks per CU.
+//  * per-slice partials [slice][cout][cin][16], summed in a fixed order by wgrad_wino_reduce
+//    (float64): deterministic.
+#include "kernels.h"
+
+namespace pcx {
+namespace {
+
+template <int V>
+using vecf = float __attribute__((ext_vector_type(V)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BUF_FLAGS = 0x00020000;  // raw buffer, 32-bit data
+constexpr int OOB = 0x7fff0000;        // beyond every num_records: loads 0, stores dropped
+constexpr int NIT = 7;                 // staged items (vectors) per thread and tile row, for dy and for x
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* base, int64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, (int)bytes, BUF_FLAGS);
+}
+
+template <int V>
+__device__ __forceinline__ vecf<V> bload(__amdgpu_buffer_rsrc_t r, int voff) {
+    if constexpr (V == 4)
+        return __builtin_bit_cast(vecf<4>, __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0));
+    else
+        return __builtin_bit_cast(vecf<2>, __builtin_amdgcn_raw_buffer_load_b64(r, voff, 0, 0));
+}
+
+template <int V>
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int voff, vecf<V> v) {
+    if constexpr (V == 4)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, voff, 0, 0);
+    else
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, voff, 0, 0);
+}
+
+// single v_fma_f32 (no SLP packing next to the stores of the same registers: see wgrad_s.hip)
+__device__ __forceinline__ float fma1(float a, float b, float c) {
+    float r;
+    asm("v_fma_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+__device__ __forceinline__ f2 ld2(const float* p) { return *reinterpret_cast<const f2*>(p); }
+
+// one wave's work: Winograd row Q = wave (elements 4 Q .. 4 Q + 3) of the 32 x 32 channel block
+template <int PRO, int V>
+__device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int co0, int ci0, int slice) {
+    const int tid = threadIdx.x, lane = tid & 63, c32 = lane & 31, g = lane >> 5;
+    const int Q = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int XCS = a.XCS, DCS = a.DCS;
+    float* const xl = smem + 4;                   // [4 ring slots][32][XCS]
+    float* const dyl = xl + 4 * 32 * XCS;         // [2 rows][32][DCS]
+    const int H = a.H, W = a.W, HW = H * W;
+    const int nd = a.nd, nx = a.nx;
+
+    // staging items: thread -> channel ch = tid >> 3 of the block (dy: cout co0 + ch, x: cin ci0 + ch)
+    // and the items q = (tid & 7) + 8 m (m < NIT) of that channel's two rows (q < nd: row 0)
+    const int ch = tid >> 3, j0 = tid & 7;
+    int dg[NIT], dls[NIT], xg[NIT], xls[NIT];
+    unsigned dr1 = 0, xr1 = 0, dex = 0, xex = 0;  // row-1 items, existing items (bit masks)
+#pragma unroll
+    for (int m = 0; m < NIT; ++m) {
+        const int q = j0 + 8 * m;
+        const int dr = q >= nd ? 1 : 0, dk = q - dr * nd;
+        dg[m] = ch * HW + dr * W + V * dk;
+        dls[m] = dr * 32 * DCS + ch * DCS + V * dk;
+        dr1 |= (unsigned)dr << m;
+        dex |= (unsigned)(q < 2 * nd) << m;
+        const int xr = q >= nx ? 1 : 0, xk = q - xr * nx;
+        xg[m] = ch * HW + xr * W + V * xk - V;   // item columns 2 t0 - V + V xk ...
+        xls[m] = ch * XCS + V * xk - (V - 1);    // ... at slot positions V xk - V + 1 ...
+        xr1 |= (unsigned)xr << m;
+        xex |= (unsigned)(q < 2 * nx) << m;
+    }
+    // BN backward coefficients of this thread's dy channel, BN + ReLU of its x channel
+    const float4 kd = a.cf_dy[co0 + ch];  // {a, mb, mgi, mean}: dy = a (dz - mb - (y - mean) mgi)
+    const float A1 = kd.x, A2 = -kd.x * kd.z, A3 = kd.x * (kd.w * kd.z - kd.y);
+    float xs = 1.f, xt = 0.f;
+    if (PRO == PRO_BNRELU) {
+        const float4 k = a.cf_x[ci0 + ch];
+        xs = k.x;
+        xt = k.y;
+    }
+
+    f32x16 acc[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[e] = 0.f;
+
+    const bool write_dy = a.dy_out != nullptr && ci0 == 0;
+    const int TR = (H + 1) >> 1;
+    const int t0s = slice * a.per_slice, t1s = min(a.ntask, t0s + a.per_slice);
+    vecf<V> dzv[NIT], yv[NIT], xv[NIT];
+
+    for (int task = t0s; task < t1s; ++task) {
+        const int b = task / a.nseg;
+        const int t0 = (task - b * a.nseg) * a.S;
+        const int c0 = 2 * t0;
+        const __amdgpu_buffer_rsrc_t rdz = rsrc(a.dz + ((int64_t)b * a.cout + co0) * HW, (int64_t)32 * HW * 4);
+        const __amdgpu_buffer_rsrc_t ry = rsrc(a.y + ((int64_t)b * a.cout + co0) * HW, (int64_t)32 * HW * 4);
+        const __amdgpu_buffer_rsrc_t rdo =
+            rsrc(write_dy ? a.dy_out + ((int64_t)b * a.cout + co0) * HW : a.dz, write_dy ? (int64_t)32 * HW * 4 : 0);
+        const __amdgpu_buffer_rsrc_t rx = rsrc(a.src + ((int64_t)b * a.cin + ci0) * HW, (int64_t)32 * HW * 4);
+        // per-task column validity of the items (whole vectors: V divides W and 2 t0)
+        unsigned dcol = 0, xcol = 0;
+#pragma unroll
+        for (int m = 0; m < NIT; ++m) {
+            const int dcl = dls[m] - ch * DCS - ((dr1 >> m) & 1) * 32 * DCS;   // V dk
+            const int xcl = xls[m] - ch * XCS + (V - 1) - V;                    // V xk - V
+            dcol |= (unsigned)(c0 + dcl < W) << m;
+            xcol |= (unsigned)((unsigned)(c0 + xcl) < (unsigned)W) << m;
+        }
+        dcol &= dex;
+        xcol &= xex;
+
+        // stage st (= -1 .. TR - 1): dy rows 2 st, 2 st + 1 and x rows 2 st + 1, 2 st + 2
+        auto masks = [&](int st, unsigned& dm, unsigned& xm) {
+            const bool d0 = 2 * st >= 0, d1 = 2 * st + 1 >= 0 && 2 * st + 1 < H;
+            const bool x0 = 2 * st + 1 >= 0 && 2 * st + 1 < H, x1 = 2 * st + 2 < H;
+            dm = dcol & ((d0 ? ~dr1 : 0u) | (d1 ? dr1 : 0u));
+            xm = xcol & ((x0 ? ~xr1 : 0u) | (x1 ? xr1 : 0u));
+        };
+        auto load_dy = [&](int st) {
+            unsigned dm, xm;
+            masks(st, dm, xm);
+            const int db = 2 * st * W + c0;
+#pragma unroll
+            for (int m = 0; m < NIT; ++m) {
+                const int o = (dm >> m) & 1 ? 4 * (dg[m] + db) : OOB;
+                dzv[m] = bload<V>(rdz, o);
+                yv[m] = bload<V>(ry, o);
+            }
+        };
+        // dy = A1 dz + A2 y + A3 (exact 0 outside the image) into dzv
+        auto form_dy = [&](int st) {
+            unsigned dm, xm;
+            masks(st, dm, xm);
+#pragma unroll
+            for (int m = 0; m < NIT; ++m) {
+                const float a3 = (dm >> m) & 1 ? A3 : 0.f;
+#pragma unroll
+                for (int e = 0; e < V; ++e) dzv[m][e] = fma1(A1, dzv[m][e], fma1(A2, yv[m][e], a3));
+            }
+        };
+        auto load_x = [&](int st) {
+            unsigned dm, xm;
+            masks(st, dm, xm);
+            const int xb = (2 * st + 1) * W + c0;
+#pragma unroll
+            for (int m = 0; m < NIT; ++m) xv[m] = bload<V>(rx, (xm >> m) & 1 ? 4 * (xg[m] + xb) : OOB);
+        };
+        auto store = [&](int st) {
+            unsigned dm, xm;
+            masks(st, dm, xm);
+            const int db = 2 * st * W + c0;
+#pragma unroll
+            for (int m = 0; m < NIT; ++m) {
+                if (!((dex >> m) & 1)) continue;
+                const bool ok = (dm >> m) & 1;
+                const vecf<V> v = dzv[m];
+                float* d = dyl + dls[m];
+                *reinterpret_cast<f2*>(d) = f2{v[0], v[1]};
+                if constexpr (V == 4) *reinterpret_cast<f2*>(d + 2) = f2{v[2], v[3]};
+                if (write_dy) bstore<V>(rdo, ok ? 4 * (dg[m] + db) : OOB, v);
+            }
+            // x rows 2 st + 1, 2 st + 2 -> ring slots (2 st + 2) & 3, (2 st + 3) & 3
+            const int sl0 = ((2 * st + 2) & 3) * 32 * XCS, sl1 = ((2 * st + 3) & 3) * 32 * XCS;
+#pragma unroll
+            for (int m = 0; m < NIT; ++m) {
+                if (!((xex >> m) & 1)) continue;
+                vecf<V> v = xv[m];
+                if (PRO == PRO_BNRELU) {
+                    const float tt = (xm >> m) & 1 ? xt : 0.f;
+#pragma unroll
+                    for (int e = 0; e < V; ++e) v[e] = fmaxf(fmaf(v[e], xs, tt), 0.f);
+                }
+                float* d = xl + ((xr1 >> m) & 1 ? sl1 : sl0) + xls[m];
+                if constexpr (V == 4) {
+                    d[0] = v[0];
+                    *reinterpret_cast<f2*>(d + 1) = f2{v[1], v[2]};
+                    d[3] = v[3];
+                } else {
+                    d[0] = v[0];
+                    d[1] = v[1];
+                }
+            }
+        };
+
+        // task prologue: stages -1 and 0 (x rows -1 .. 2, dy rows 0, 1)
+        for (int st = -1; st <= 0; ++st) {
+            load_dy(st);
+            load_x(st);
+            form_dy(st);
+            store(st);
+        }
+        __syncthreads();
+        // wave constants of row Q: e = w + sx u from x rows (w, u) of the tile row's four; the dy row
+        // combination pr = r0 + sy r1 (Q 0: r0, 1: r0 + r1, 2: r0 - r1, 3: r1 via r0 := row 1, sy = 0)
+        const int IW = Q == 0 ? 0 : Q == 2 ? 2 : 1, IU = Q == 0 ? 2 : Q == 2 ? 1 : Q == 1 ? 2 : 3;
+        const float sx = Q == 1 ? 1.f : -1.f;
+        const float sy = Q == 1 ? 1.f : Q == 2 ? -1.f : 0.f;
+        const float* const dr0 = dyl + (Q == 3 ? 32 * DCS : 0) + c32 * DCS + 2 * g;
+        const float* const dr1 = dyl + 32 * DCS + c32 * DCS + 2 * g;
+        auto ksteps = [&](const float* xw, const float* xu, int s0, int s1) {
+            for (int s = s0; s < s1; ++s) {
+                const int p = 4 * s;  // 2 * (2 s + g), the lane's 2 g folded into the row bases
+                const f2 w0 = ld2(xw + p), w1 = ld2(xw + p + 2), u0 = ld2(xu + p), u1 = ld2(xu + p + 2);
+                const f2 r0 = ld2(dr0 + p), r1 = ld2(dr1 + p);
+                const float e0 = fmaf(sx, u0.x, w0.x), e1 = fmaf(sx, u0.y, w0.y);
+                const float e2 = fmaf(sx, u1.x, w1.x), e3 = fmaf(sx, u1.y, w1.y);
+                const float v0 = e0 - e2, v1 = e1 + e2, v2 = e2 - e1, v3 = e1 - e3;
+                const float px = fmaf(sy, r1.x, r0.x), py = fmaf(sy, r1.y, r0.y);
+                acc[0] = mfma32(px, v0, acc[0]);
+                acc[1] = mfma32(px + py, v1, acc[1]);
+                acc[2] = mfma32(px - py, v2, acc[2]);
+                acc[3] = mfma32(py, v3, acc[3]);
+            }
+        };
+        const int Ks = a.Ksteps, Kh = Ks >> 1;
+        for (int tr = 0; tr < TR; ++tr) {
+            const bool pre = tr + 1 < TR;
+            // the next tile row's dz / y now, its x rows half way (registers: dy is formed from dz, y
+            // before the x loads are issued)
+            if (pre) load_dy(tr + 1);
+            // x rows 2 tr - 1 + i of this tile row live in ring slot (2 tr + i) & 3
+            const float* xw = xl + ((2 * tr + IW) & 3) * 32 * XCS + c32 * XCS + 2 * g;
+            const float* xu = xl + ((2 * tr + IU) & 3) * 32 * XCS + c32 * XCS + 2 * g;
+            ksteps(xw, xu, 0, Kh);
+            if (pre) {
+                form_dy(tr + 1);
+                load_x(tr + 1);
+            }
+            ksteps(xw, xu, Kh, Ks);
+            __syncthreads();  // the dy rows and the two oldest x rows are free
+            if (pre) store(tr + 1);
+            __syncthreads();
+        }
+    }
+    // partials: C register r of lane l = (cout row (r & 3) + 8 (r >> 2) + 4 g, cin c32); xi = 4 Q + e
+    float* out = a.part + (int64_t)slice * a.cout * a.cin * 16;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int co = co0 + (r & 3) + 8 * (r >> 2) + 4 * g;
+        *reinterpret_cast<float4*>(out + ((int64_t)co * a.cin + ci0 + c32) * 16 + 4 * Q) =
+            make_float4(acc[0][r], acc[1][r], acc[2][r], acc[3][r]);
+    }
+}
+
+template <int PRO, int V>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void wgrad_wino_kernel(WinoWgradArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int tid = threadIdx.x;
+    const int ncgi = a.cin / 32, ngroups = (a.cout / 32) * ncgi;
+    const int f = blockIdx.x, kk = f >> 3;
+    const int group = kk % ngroups;
+    const int slice = (kk / ngroups) * 8 + (f & 7);  // XCD-aware: a slice's groups share an XCD
+    if (slice >= a.nslice) return;
+    const int co0 = (group / ncgi) * 32, ci0 = (group % ncgi) * 32;
+    // zero the staging image (padding positions and padded tiles read zeros)
+    const int nz = 4 + 4 * 32 * a.XCS + 2 * 32 * a.DCS;
+    for (int i = tid; i < nz; i += 256) smem[i] = 0.f;
+    __syncthreads();
+    ww_body<PRO, V>(a, smem, co0, ci0, slice);
+}
+
+// dW[n][c] = G^T dU G per (n, c) from the slices' sum (float64, fixed order); the partials carry
+// row / column 3 of the Winograd domain negated (Yh' of the kernel).
+__global__ void wgrad_wino_reduce_kernel(const float* __restrict__ part, int nslice, int npair, float* __restrict__ dw) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= npair) return;
+    double u[16];
+#pragma unroll
+    for (int x = 0; x < 16; ++x) u[x] = 0.0;
+    for (int s = 0; s < nslice; ++s) {
+        const float4* p = reinterpret_cast<const float4*>(part + ((int64_t)s * npair + i) * 16);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float4 v = p[q];
+            u[4 * q + 0] += v.x;
+            u[4 * q + 1] += v.y;
+            u[4 * q + 2] += v.z;
+            u[4 * q + 3] += v.w;
+        }
+    }
+    // undo the folded signs: dU[q][e] = s_q s_e dU'[q][e], s_3 = -1
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        u[4 * q + 3] = -u[4 * q + 3];
+        u[12 + q] = -u[12 + q];
+    }
+    // t = G^T dU (3 x 4), G = [[1,0,0],[1/2,1/2,1/2],[1/2,-1/2,1/2],[0,0,1]]
+    double t[3][4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const double u0 = u[e], u1 = u[4 + e], u2 = u[8 + e], u3 = u[12 + e];
+        t[0][e] = u0 + 0.5 * (u1 + u2);
+        t[1][e] = 0.5 * (u1 - u2);
+        t[2][e] = 0.5 * (u1 + u2) + u3;
+    }
+    float* o = dw + (int64_t)i * 9;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const double t0 = t[r][0], t1 = t[r][1], t2 = t[r][2], t3 = t[r][3];
+        o[3 * r + 0] = (float)(t0 + 0.5 * (t1 + t2));
+        o[3 * r + 1] = (float)(0.5 * (t1 - t2));
+        o[3 * r + 2] = (float)(0.5 * (t1 + t2) + t3);
+    }
+}
+
+int smallest_2odd(int n) {  // smallest m >= n with m = 2 * odd
+    while ((n & 3) != 2) ++n;
+    return n;
+}
+
+}  // namespace
+
+bool wgrad_wino_geometry(int B, int H, int W, int cin, int cout, WinoWgradArgs* a) {
+    if (cin % 32 || cout % 32 || H < 1 || W < 4) return false;
+    const int V = W % 4 == 0 ? 4 : W % 2 == 0 ? 2 : 0;
+    if (!V) return false;
+    const int TC = (W + 1) / 2;
+    int nseg = ceil_div(TC, 50);
+    int S = ceil_div(TC, nseg);
+    if (nseg > 1) S = (S + 1) & ~1;  // strip starts 2 t0 on a 16-byte boundary (V = 4)
+    nseg = ceil_div(TC, S);
+    const int Ksteps = (S + 1) / 2;
+    const int nd = 2 * S / V, kmax = (2 * S + 1 + V - 1) / V, nx = kmax + 1;
+    if ((2 * S) % V) return false;
+    if (2 * nd > 8 * NIT || 2 * nx > 8 * NIT) return false;  // 8 threads x NIT items per channel
+    const int XCS = smallest_2odd(std::max(std::max(V * kmax + 1, 4 * Ksteps + 2), 2 * S + 5));
+    const int DCS = smallest_2odd(4 * Ksteps);
+    const size_t lds = ((size_t)4 + 128 * XCS + 64 * DCS) * 4;
+    if (lds > 80 * 1024) return false;
+    if ((int64_t)32 * H * W * 4 >= OOB) return false;  // valid offsets stay below the out-of-range marker
+    if (a) {
+        a->S = S;
+        a->nseg = nseg;
+        a->V = V;
+        a->XCS = XCS;
+        a->DCS = DCS;
+        a->nd = nd;
+        a->nx = nx;
+        a->Ksteps = Ksteps;
+        a->lds = lds;
+        a->ntask = B * nseg;
+        const int ngroups = (cout / 32) * (cin / 32);
+        int want = std::max(8, 2 * num_cus() / ngroups);  // ~2 resident blocks per CU
+        want = std::min(want, a->ntask);
+        a->per_slice = ceil_div(a->ntask, want);
+        a->nslice = ceil_div(a->ntask, a->per_slice);
+    }
+    return true;
+}
+
+int launch_wgrad_wino(int pro, WinoWgradArgs a, hipStream_t s) {
+    WinoWgradArgs g{};
+    PCX_CHECK_ARG(wgrad_wino_geometry(a.B, a.H, a.W, a.cin, a.cout, &g), "wgrad_wino: unsupported shape %dx%d (%d, %d)",
+                  a.H, a.W, a.cin, a.cout);
+    PCX_CHECK_ARG(g.S == a.S && g.V == a.V && g.XCS == a.XCS && g.DCS == a.DCS && g.nslice == a.nslice &&
+                      g.per_slice == a.per_slice && g.ntask == a.ntask,
+                  "wgrad_wino: geometry mismatch");
+    PCX_CHECK_ARG(pro == PRO_RAW || pro == PRO_BNRELU, "wgrad_wino: prologue %d", pro);
+    const int ngroups = (a.cout / 32) * (a.cin / 32);
+    dim3 grid((unsigned)(((a.nslice + 7) / 8) * 8 * ngroups));
+#define PCX_WW(P_, V_)                                                                                   \
+    if (pro == P_ && a.V == V_) {                                                                        \
+        (void)hipFuncSetAttribute((const void*)wgrad_wino_kernel<P_, V_>,                                \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)a.lds);               \
+        wgrad_wino_kernel<P_, V_><<<grid, 256, a.lds, s>>>(a);                                           \
+        PCX_LAUNCH_CHECK("wgrad_wino_kernel");                                                           \
+        return PCX_OK;                                                                                   \
+    }
+    PCX_WW(PRO_RAW, 4)
+    PCX_WW(PRO_RAW, 2)
+    PCX_WW(PRO_BNRELU, 4)
+    PCX_WW(PRO_BNRELU, 2)
+#undef PCX_WW
+    set_error("wgrad_wino: unsupported combination (pro %d, vec %d)", pro, a.V);
+    return PCX_EINVAL;
+}
+
+int launch_wgrad_wino_reduce(const float* part, int nslice, int cout, int cin, float* dw, hipStream_t s) {
+    const int npair = cout * cin;
+    wgrad_wino_reduce_kernel<<<ceil_div(npair, 256), 256, 0, s>>>(part, nslice, npair, dw);
+    PCX_LAUNCH_CHECK("wgrad_wino_reduce_kernel");
+    return PCX_OK;
+}
+
+}  // namespace pcx

@@ -63,6 +63,15 @@ def broadcast_module(module: torch.nn.Module, src: int = 0):
         dist.broadcast(t.data, src)
 
 
+@torch.no_grad()
+def broadcast_buffers(module: torch.nn.Module, src: int = 0):
+    """Rank `src`'s buffers (BatchNorm running statistics) on every rank."""
+    if world()[1] == 1:
+        return
+    for t in module.buffers():
+        dist.broadcast(t.data, src)
+
+
 def is_distributed() -> bool:
     """A process group is up (any world size, including a forced world-1 group)."""
     return dist.is_available() and dist.is_initialized()

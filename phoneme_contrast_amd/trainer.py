@@ -107,6 +107,10 @@ class ContrastiveTrainer:
             self.global_step += 1
             if hasattr(pbar, "set_postfix"):
                 pbar.set_postfix({"loss": loss.item()})
+        if self.world_size > 1:
+            # BatchNorm running statistics are per rank during the epoch (each rank's batches);
+            # like DDP's broadcast_buffers, validation and checkpoints use rank 0's
+            ddp.broadcast_buffers(self.model)
         return {"loss": total_loss / max(num_batches, 1), "lr": self.optimizer.param_groups[0]["lr"]}
 
     def _grad_scale(self) -> float:
