@@ -20,6 +20,8 @@ ORDER = {
     "conv_wino_kernel": FWD + DGRAD,  # Winograd conv (every cnn_small layer at W >= 31)
     "conv3x3_dma_kernel": FWD + DGRAD,
     "wgrad_s_kernel": [f"wgrad_L{l}" for l in range(6, 1, -1)],
+    "wgrad_wino_kernel": [f"wgrad_L{l}" for l in range(6, 1, -1)],  # Winograd weight gradient (W even)
+    "wgrad_wino_reduce_kernel": [f"wgrad_reduce_L{l}" for l in range(6, 1, -1)],
     "bn_relu_pool_kernel": ["bn_relu_pool_L3", "bn_relu_pool_L5"],
     "conv1_fwd_kernel": ["conv1_fwd_L1"],
     "wgrad1_kernel": ["wgrad_L1"],

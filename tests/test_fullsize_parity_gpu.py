@@ -101,8 +101,8 @@ def _compare(got, ref, emb_tol, name, yardstick=None):
         if kind == "abs":
             if not err < 1e-4:
                 bad[k] = (err, 1e-4)
-        elif not (err < max(2e-3, 3.0 * ymax) and l2 < max(1e-3, 3.0 * yl2)):
-            bad[k] = (err, l2, max(2e-3, 3.0 * ymax), max(1e-3, 3.0 * yl2))
+        elif not (err < max(2e-3, 3.0 * ymax) and l2 < max(2e-3, 3.0 * yl2)):
+            bad[k] = (err, l2, max(2e-3, 3.0 * ymax), max(2e-3, 3.0 * yl2))
     assert not bad, json.dumps(bad, sort_keys=True)
     for k, r in ref["state"].items():
         assert torch.allclose(got["state"][k], r, rtol=1e-5, atol=1e-6), k
