@@ -28,6 +28,7 @@ build/%.o: phoneme_contrast_amd/csrc/%.hip $(HDR)
 
 # fp32 MFMA shares the vector pipe: packed f32 VALU (SLP) costs more issue than scalar beside it
 build/conv_wino.o: CXXFLAGS += -fno-slp-vectorize
+build/wgrad_wino.o: CXXFLAGS += -fno-slp-vectorize
 
 $(LIB): $(OBJ)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJ)

@@ -43,7 +43,8 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BUF_FLAGS = 0x00020000;  // raw buffer, 32-bit data
 constexpr int OOB = 0x7fff0000;        // beyond every num_records: loads 0, stores dropped
-constexpr int NIT = 7;                 // staged items (vectors) per thread and tile row, for dy and for x
+constexpr int NIR = 4;                 // staged vectors per thread and row (dy and x): 8 threads x 4 >= 32 per channel
+constexpr int NIT = 2 * NIR;           // per stage (two rows)
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* base, int64_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, (int)bytes, BUF_FLAGS);
@@ -74,6 +75,56 @@ __device__ __forceinline__ float fma1(float a, float b, float c) {
 
 __device__ __forceinline__ f2 ld2(const float* p) { return *reinterpret_cast<const f2*>(p); }
 
+// Operands of one K-step (2 tiles, lane tile 2 s + g): the wave's two x rows (w, u: 4 values
+// each) and the two dy rows (r0, r1: 2 values each) of the lane's channel.
+struct KOps {
+    f2 w0, w1, u0, u1, r0, r1;
+};
+
+__device__ __forceinline__ KOps kload(const float* w, const float* u, const float* q0, const float* q1, int s) {
+    const int p = 4 * s;  // 2 * (2 s + g), the lane's 2 g folded into the row bases
+    KOps o;
+    o.w0 = ld2(w + p);
+    o.w1 = ld2(w + p + 2);
+    o.u0 = ld2(u + p);
+    o.u1 = ld2(u + p + 2);
+    o.r0 = ld2(q0 + p);
+    o.r1 = ld2(q1 + p);
+    return o;
+}
+
+// V row Q = (B^T d B) row Q from e = w + sx u; Yh' row Q = (A dY A^T) row Q (row / column 3 sign-
+// folded) from pr = r0 + sy r1; four 32x32x2 MFMAs
+__device__ __forceinline__ void kmul(const KOps& o, float sx, float sy, f32x16 (&acc)[4]) {
+    const float e0 = fmaf(sx, o.u0.x, o.w0.x), e1 = fmaf(sx, o.u0.y, o.w0.y);
+    const float e2 = fmaf(sx, o.u1.x, o.w1.x), e3 = fmaf(sx, o.u1.y, o.w1.y);
+    const float px = fmaf(sy, o.r1.x, o.r0.x), py = fmaf(sy, o.r1.y, o.r0.y);
+    acc[0] = mfma32(px, e0 - e2, acc[0]);
+    acc[1] = mfma32(px + py, e1 + e2, acc[1]);
+    acc[2] = mfma32(px - py, e2 - e1, acc[2]);
+    acc[3] = mfma32(py, e1 - e3, acc[3]);
+}
+
+// K-steps s0 .. s0 + n - 1, software-pipelined: the reads of step s + 1 are in flight while step s
+// multiplies (two operand sets, alternating: no register moves)
+__device__ __forceinline__ void kloop(const float* w, const float* u, const float* q0, const float* q1, float sx,
+                                      float sy, f32x16 (&acc)[4], int n) {
+    if (n <= 0) return;
+    KOps A = kload(w, u, q0, q1, 0);
+    int s = 0;
+    for (; s + 2 <= n; s += 2) {
+        const KOps Bn = kload(w, u, q0, q1, s + 1);
+        __builtin_amdgcn_sched_barrier(0);  // reads issued ahead of the MFMAs they overlap
+        kmul(A, sx, sy, acc);
+        __builtin_amdgcn_sched_barrier(0);
+        A = kload(w, u, q0, q1, s + 2 < n ? s + 2 : s + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        kmul(Bn, sx, sy, acc);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (s < n) kmul(A, sx, sy, acc);
+}
+
 // one wave's work: Winograd row Q = wave (elements 4 Q .. 4 Q + 3) of the 32 x 32 channel block
 template <int PRO, int V>
 __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int co0, int ci0, int slice) {
@@ -86,23 +137,17 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
     const int nd = a.nd, nx = a.nx;
 
     // staging items: thread -> channel ch = tid >> 3 of the block (dy: cout co0 + ch, x: cin ci0 + ch)
-    // and the items q = (tid & 7) + 8 m (m < NIT) of that channel's two rows (q < nd: row 0)
+    // and, in each of the stage's two rows r, the vectors k = (tid & 7) + 8 m (m < NIR) of that channel:
+    // item i = NIR r + m.  Offsets are one per-thread base plus compile-time / uniform terms.
     const int ch = tid >> 3, j0 = tid & 7;
-    int dg[NIT], dls[NIT], xg[NIT], xls[NIT];
-    unsigned dr1 = 0, xr1 = 0, dex = 0, xex = 0;  // row-1 items, existing items (bit masks)
+    const int dgb = ch * HW + V * j0, dlb = ch * DCS + V * j0;
+    const int xgb = ch * HW + V * j0 - V, xlb = ch * XCS + V * j0 - (V - 1);
+    unsigned dex = 0, xex = 0;  // existing items (bit masks)
 #pragma unroll
-    for (int m = 0; m < NIT; ++m) {
-        const int q = j0 + 8 * m;
-        const int dr = q >= nd ? 1 : 0, dk = q - dr * nd;
-        dg[m] = ch * HW + dr * W + V * dk;
-        dls[m] = dr * 32 * DCS + ch * DCS + V * dk;
-        dr1 |= (unsigned)dr << m;
-        dex |= (unsigned)(q < 2 * nd) << m;
-        const int xr = q >= nx ? 1 : 0, xk = q - xr * nx;
-        xg[m] = ch * HW + xr * W + V * xk - V;   // item columns 2 t0 - V + V xk ...
-        xls[m] = ch * XCS + V * xk - (V - 1);    // ... at slot positions V xk - V + 1 ...
-        xr1 |= (unsigned)xr << m;
-        xex |= (unsigned)(q < 2 * nx) << m;
+    for (int i = 0; i < 2 * NIR; ++i) {
+        const int k = j0 + 8 * (i % NIR);
+        dex |= (unsigned)(k < nd) << i;
+        xex |= (unsigned)(k < nx) << i;
     }
     // BN backward coefficients of this thread's dy channel, BN + ReLU of its x channel
     const float4 kd = a.cf_dy[co0 + ch];  // {a, mb, mgi, mean}: dy = a (dz - mb - (y - mean) mgi)
@@ -135,29 +180,31 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
         // per-task column validity of the items (whole vectors: V divides W and 2 t0)
         unsigned dcol = 0, xcol = 0;
 #pragma unroll
-        for (int m = 0; m < NIT; ++m) {
-            const int dcl = dls[m] - ch * DCS - ((dr1 >> m) & 1) * 32 * DCS;   // V dk
-            const int xcl = xls[m] - ch * XCS + (V - 1) - V;                    // V xk - V
-            dcol |= (unsigned)(c0 + dcl < W) << m;
-            xcol |= (unsigned)((unsigned)(c0 + xcl) < (unsigned)W) << m;
+        for (int i = 0; i < NIT; ++i) {
+            const int kc = V * (j0 + 8 * (i % NIR));
+            dcol |= (unsigned)(c0 + kc < W) << i;
+            xcol |= (unsigned)((unsigned)(c0 + kc - V) < (unsigned)W) << i;
         }
         dcol &= dex;
         xcol &= xex;
 
         // stage st (= -1 .. TR - 1): dy rows 2 st, 2 st + 1 and x rows 2 st + 1, 2 st + 2
+        constexpr unsigned R1 = ((1u << NIR) - 1) << NIR;  // items of the stage's second row
         auto masks = [&](int st, unsigned& dm, unsigned& xm) {
             const bool d0 = 2 * st >= 0, d1 = 2 * st + 1 >= 0 && 2 * st + 1 < H;
             const bool x0 = 2 * st + 1 >= 0 && 2 * st + 1 < H, x1 = 2 * st + 2 < H;
-            dm = dcol & ((d0 ? ~dr1 : 0u) | (d1 ? dr1 : 0u));
-            xm = xcol & ((x0 ? ~xr1 : 0u) | (x1 ? xr1 : 0u));
+            dm = dcol & ((d0 ? ~R1 : 0u) | (d1 ? R1 : 0u));
+            xm = xcol & ((x0 ? ~R1 : 0u) | (x1 ? R1 : 0u));
         };
+        auto dgo = [&](int i) { return dgb + (i / NIR) * W + 8 * V * (i % NIR); };
+        auto xgo = [&](int i) { return xgb + (i / NIR) * W + 8 * V * (i % NIR); };
         auto load_dy = [&](int st) {
             unsigned dm, xm;
             masks(st, dm, xm);
             const int db = 2 * st * W + c0;
 #pragma unroll
             for (int m = 0; m < NIT; ++m) {
-                const int o = (dm >> m) & 1 ? 4 * (dg[m] + db) : OOB;
+                const int o = (dm >> m) & 1 ? 4 * (dgo(m) + db) : OOB;
                 dzv[m] = bload<V>(rdz, o);
                 yv[m] = bload<V>(ry, o);
             }
@@ -178,7 +225,7 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
             masks(st, dm, xm);
             const int xb = (2 * st + 1) * W + c0;
 #pragma unroll
-            for (int m = 0; m < NIT; ++m) xv[m] = bload<V>(rx, (xm >> m) & 1 ? 4 * (xg[m] + xb) : OOB);
+            for (int m = 0; m < NIT; ++m) xv[m] = bload<V>(rx, (xm >> m) & 1 ? 4 * (xgo(m) + xb) : OOB);
         };
         auto store = [&](int st) {
             unsigned dm, xm;
@@ -189,10 +236,10 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
                 if (!((dex >> m) & 1)) continue;
                 const bool ok = (dm >> m) & 1;
                 const vecf<V> v = dzv[m];
-                float* d = dyl + dls[m];
+                float* d = dyl + dlb + (m / NIR) * 32 * DCS + 8 * V * (m % NIR);
                 *reinterpret_cast<f2*>(d) = f2{v[0], v[1]};
                 if constexpr (V == 4) *reinterpret_cast<f2*>(d + 2) = f2{v[2], v[3]};
-                if (write_dy) bstore<V>(rdo, ok ? 4 * (dg[m] + db) : OOB, v);
+                if (write_dy) bstore<V>(rdo, ok ? 4 * (dgo(m) + db) : OOB, v);
             }
             // x rows 2 st + 1, 2 st + 2 -> ring slots (2 st + 2) & 3, (2 st + 3) & 3
             const int sl0 = ((2 * st + 2) & 3) * 32 * XCS, sl1 = ((2 * st + 3) & 3) * 32 * XCS;
@@ -205,7 +252,7 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
 #pragma unroll
                     for (int e = 0; e < V; ++e) v[e] = fmaxf(fmaf(v[e], xs, tt), 0.f);
                 }
-                float* d = xl + ((xr1 >> m) & 1 ? sl1 : sl0) + xls[m];
+                float* d = xl + (m / NIR ? sl1 : sl0) + xlb + 8 * V * (m % NIR);
                 if constexpr (V == 4) {
                     d[0] = v[0];
                     *reinterpret_cast<f2*>(d + 1) = f2{v[1], v[2]};
@@ -233,19 +280,12 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
         const float* const dr0 = dyl + (Q == 3 ? 32 * DCS : 0) + c32 * DCS + 2 * g;
         const float* const dr1 = dyl + 32 * DCS + c32 * DCS + 2 * g;
         auto ksteps = [&](const float* xw, const float* xu, int s0, int s1) {
-            for (int s = s0; s < s1; ++s) {
-                const int p = 4 * s;  // 2 * (2 s + g), the lane's 2 g folded into the row bases
-                const f2 w0 = ld2(xw + p), w1 = ld2(xw + p + 2), u0 = ld2(xu + p), u1 = ld2(xu + p + 2);
-                const f2 r0 = ld2(dr0 + p), r1 = ld2(dr1 + p);
-                const float e0 = fmaf(sx, u0.x, w0.x), e1 = fmaf(sx, u0.y, w0.y);
-                const float e2 = fmaf(sx, u1.x, w1.x), e3 = fmaf(sx, u1.y, w1.y);
-                const float v0 = e0 - e2, v1 = e1 + e2, v2 = e2 - e1, v3 = e1 - e3;
-                const float px = fmaf(sy, r1.x, r0.x), py = fmaf(sy, r1.y, r0.y);
-                acc[0] = mfma32(px, v0, acc[0]);
-                acc[1] = mfma32(px + py, v1, acc[1]);
-                acc[2] = mfma32(px - py, v2, acc[2]);
-                acc[3] = mfma32(py, v3, acc[3]);
-            }
+            const int n = s1 - s0;
+            const float* w = xw + 4 * s0;
+            const float* u = xu + 4 * s0;
+            const float* q0 = dr0 + 4 * s0;
+            const float* q1 = dr1 + 4 * s0;
+            kloop(w, u, q0, q1, sx, sy, acc, n);
         };
         const int Ks = a.Ksteps, Kh = Ks >> 1;
         for (int tr = 0; tr < TR; ++tr) {
