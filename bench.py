@@ -66,7 +66,28 @@ def kernel_costs(B, F, T, D=128):
         out[f"conv_dgrad_L{l}"] = (2 * macs, 2 * y_out + 2 * x_in)
         # wgrad: reads dz_l, y_l and the forward input source
         out[f"wgrad_L{l}"] = (2 * macs, 2 * y_out + x_in)
+    # elementwise / head passes (bytes: each tensor read once, each output written once)
+    H1, W1, H3, W3, H5, W5 = F, T, F // 2, T // 2, F // 4, T // 4
+    out["bn_relu_pool_L3"] = (0, 4 * B * 32 * (H1 * W1 + H3 * W3))
+    out["bn_relu_pool_L5"] = (0, 4 * B * 64 * (H3 * W3 + H5 * W5))
+    out["head_pool_fwd"] = (4 * B * 128 * H5 * W5, 4 * B * (128 * H5 * W5 + 128 + H5 * W5))
+    out["head_pool_bwd"] = (6 * B * 128 * H5 * W5, 4 * B * (2 * 128 * H5 * W5 + 128 + H5 * W5))
+    out["proj_fwd"] = (2 * B * 128 * D, 4 * B * (128 + 2 * D))
+    out["proj_bwd"] = (4 * B * 128 * D, 4 * B * (2 * 128 + 3 * D))
     return out
+
+
+def executed_fraction(label, T):
+    """Multiplies executed per algorithmic (direct-conv) multiply for cnn_small's kernels: the 3x3
+    forward / data-gradient convs run Winograd F(2x2,3x3) at W >= 31 (conv_wino.hip), the 3x3
+    weight gradients at even W (wgrad_wino.hip): 16 multiplies per 2x2 outputs instead of 36."""
+    widths = {2: T, 3: T // 2, 4: T // 2, 5: T // 4, 6: T // 4}
+    for pre in ("conv_fwd_L", "conv_dgrad_L"):
+        if label.startswith(pre):
+            return 4 / 9 if widths.get(int(label[len(pre):]), 0) >= 31 else 1.0
+    if label.startswith("wgrad_L") and label[7:].isdigit() and int(label[7:]) >= 2:
+        return 4 / 9 if widths[int(label[7:])] % 2 == 0 else 1.0
+    return 1.0
 
 
 def deep_convs(F, T, h=DEEP_DIMS):
@@ -87,7 +108,10 @@ def deep_convs(F, T, h=DEEP_DIMS):
     return out
 
 
-def deep_kernel_costs(B, F, T):
+def deep_kernel_costs(B, F, T, bf16=False, D=128):
+    """Algorithmic FLOPs and bytes of one launch of every profiled cnn_deep label (convs: both
+    operands read once, the output written once, float32; elementwise passes: each tensor read
+    once, each output written once, float32 activations, bf16 channel-last images 2 B/element)."""
     out = {}
     for fl, wl, dl, ci, co, k, s, IH, IW, OH, OW in deep_convs(F, T):
         macs = B * OH * OW * co * ci * k * k
@@ -96,6 +120,39 @@ def deep_kernel_costs(B, F, T):
         out[wl] = (2 * macs, x_b + y_b)
         if dl:
             out[dl] = (2 * macs, x_b + y_b)
+    img = 2 if bf16 else 4
+    H0, W0 = F, T
+    H1, W1 = (H0 - 1) // 2 + 1, (W0 - 1) // 2 + 1
+    C0 = DEEP_DIMS[0]
+    out["maxpool_fwd"] = (0, B * C0 * (4 * H0 * W0 + 5 * H1 * W1))            # y0 -> a0 + first-max tap
+    out["maxpool_bwd"] = (0, B * C0 * (4 * H0 * W0 * 2 + 5 * H1 * W1))        # tap, d a0, y0 -> dz0
+    out["bwd_prep_L0"] = (0, B * C0 * 4 * H0 * W0 * 3)
+    H, W, cin = H1, W1, C0
+    for i, co in enumerate(DEEP_DIMS):
+        st = 1 if i == 0 else 2
+        Ho, Wo = (H - 1) // st + 1, (W - 1) // st + 1
+        L, Pi, Po = 2 * i + 1, H * W, Ho * Wo
+        sc = st != 1 or cin != co
+        a_in, y = 4 * B * cin * Pi, 4 * B * co * Po
+        out[f"to_nhwc_L{L}"] = (0, a_in + img * B * cin * (H + 2) * (W + 2))
+        out[f"bn_act_L{L}"] = (0, y + img * B * co * Po)                         # y1 -> d1
+        out[f"bn_act_L{L + 1}"] = (0, 2 * y + y + img * B * co * Po)             # y2 + residual -> out (+ image)
+        out[f"chan_stats_L{L}"] = (0, y)
+        out[f"chan_stats_L{L + 1}"] = (0, y)
+        out[f"chan_stats_L{100 + i}"] = (0, y)
+        out[f"bwd_prep_L{L + 1}"] = (0, y * (4 if sc else 3) + y)                # d, mask, y2 (, ysc) -> g
+        out[f"bwd_prep_L{L}"] = (0, 3 * y)                                       # d, y1 -> d
+        out[f"dy_nhwc_L{L + 1}"] = (0, 2 * y + img * B * co * Po)
+        out[f"dy_nhwc_L{L}"] = (0, 2 * y + img * B * co * Po)
+        out[f"bn_bwd_apply_L{L + 1}"] = (0, 3 * y)
+        out[f"bn_bwd_apply_L{L}"] = (0, 3 * y)
+        out[f"dgrad_interleave_L{L}"] = (0, 2 * a_in)
+        H, W, cin = Ho, Wo, co
+    C4, P4 = DEEP_DIMS[-1], H * W
+    out["head_pool_fwd"] = (4 * B * C4 * P4, 4 * B * (C4 * P4 + C4 + P4))
+    out["head_pool_bwd"] = (6 * B * C4 * P4, 4 * B * (2 * C4 * P4 + C4 + P4))
+    out["proj_fwd"] = (2 * B * C4 * D, 4 * B * (C4 + 2 * D))
+    out["proj_bwd"] = (4 * B * C4 * D, 4 * B * (2 * C4 + 3 * D))
     return out
 
 
@@ -336,8 +393,8 @@ def main():
     if backend == "nccl":
         backend = "rccl"  # torch's "nccl" backend is RCCL on ROCm
     value = world * B * args.steps / el
-    costs = deep_kernel_costs(B, F, T) if deep else kernel_costs(B, F, T, D)
     bf16 = deep and args.precision == "bf16"
+    costs = deep_kernel_costs(B, F, T, bf16, D) if deep else kernel_costs(B, F, T, D)
     peak = BF16_PEAK_TFLOPS if bf16 else FP32_PEAK_TFLOPS
     roof = None
     kernels = {}
@@ -345,6 +402,9 @@ def main():
         for lab, (tot, cnt) in sorted(prof.items(), key=lambda kv: -kv[1][0]):
             kernels[lab] = {"avg_ms": round(tot / cnt, 4), "launches": cnt,
                             "share": round(tot / (1000.0 * el), 4)}
+        # the dominant kernel: the label with the largest total time (every kernel that matters has
+        # a cost model; the bookkeeping labels without one are the tiny finalisers / reductions)
+        dom_any = max(prof, key=lambda k: prof[k][0])
         dom = max((k for k in prof if k in costs), key=lambda k: prof[k][0])
         tot, cnt = prof[dom]
         avg_s = tot / cnt / 1000.0
@@ -362,10 +422,19 @@ def main():
         roof["algorithmic_flops_per_launch"] = fl
         roof["algorithmic_bytes_per_launch"] = by
         roof["avg_launch_ms"] = round(avg_s * 1000.0, 4)
-    if roof is not None and dom.startswith(("conv_fwd_L", "conv_dgrad_L")) and not deep:
-        # cnn_small's 3x3 convs run Winograd F(2x2,3x3): 4/9 of the direct multiplies are executed
-        roof["executed_flops_per_launch"] = fl * 4 // 9
-        roof["executed_frac"] = round(roof["frac"] * 4 / 9, 4)
+    if roof is not None:
+        roof["largest_label_overall"] = dom_any
+        if not deep and roof["bound"] == "mfma":
+            # cnn_small's 3x3 convs run Winograd F(2x2,3x3): 4/9 of the direct multiplies are executed
+            xf = executed_fraction(dom, T)
+            roof["executed_flops_per_launch"] = int(fl * xf)
+            roof["executed_frac"] = round(roof["frac"] * xf, 4)
+        for lab, rec in kernels.items():  # per-kernel achieved rates for every costed label
+            if lab in costs:
+                f_, b_ = costs[lab]
+                t_ = rec["avg_ms"] / 1000.0
+                rec["alg_tflops"] = round(f_ / t_ / 1e12, 2) if f_ else None
+                rec["alg_gbps"] = round(b_ / t_ / 1e9, 1)
     sf, sb = deep_step_cost(B, F, T, D) if deep else step_cost(B, F, T, D)
     step_roof = {"flops_per_step": sf, "bytes_per_step": sb,
                  "mfma_fraction": round(sf / (el / args.steps) / (peak * 1e12), 4),
@@ -416,7 +485,8 @@ def main():
             "conv_fwd / conv_dgrad L2-L6": "Winograd F(2x2,3x3) on fp32 MFMA (16 multiplies per 2x2 outputs: "
                                            "4/9 of the direct conv's; fp32 arithmetic, rounding differs from the direct "
                                            "conv by 2-6e-6 of max|y|)",
-            "wgrad L2-L6": "direct implicit GEMM on fp32 MFMA (pixel streams)"},
+            "wgrad L2-L6": "Winograd F(2x2,3x3) weight gradient on fp32 MFMA (even W; 4/9 of the direct "
+                           "multiplies), else the direct pixel-stream implicit GEMM"},
         "roofline": roof,
         "step_roofline": step_roof,
         "cpu_baseline": cpu,

@@ -291,7 +291,7 @@ int conv_bn_fwd(const Ctx& c, const char* label, int layer, const float* x, int 
         RC(launch_convg(a, c.s));
     }
     if (train && !dma_nblk) {
-        Scope sc(&c.p.prof, c.s, "chan_stats");
+        Scope sc(&c.p.prof, c.s, "chan_stats", strcmp(label, "shortcut_fwd") == 0 ? 100 + layer : layer);
         int bps;
         const int nsl = chan_slices(c.p.B, cout, &bps);
         f.part0 = part;
@@ -453,7 +453,7 @@ int deep_forward(const Plan& p, const float* const* P, float* const* bnstat, int
         const void* an = k.cn ? c.w<void>(k.an) : nullptr;
         const void* d1n = k.cn ? c.w<void>(k.d1n) : nullptr;
         if (k.cn && (i == 0 || !d.blk[i - 1].cn)) {  // (otherwise written by the previous block's activation)
-            Scope sc(&p.prof, s, "to_nhwc");
+            Scope sc(&p.prof, s, "to_nhwc", L);
             RC(launch_to_nhwc(nhwc_args(NHWC_COPY, B, k.cin, k.Hi, k.Wi, a, c.w<void>(k.an)), s));
         }
         RC(conv_bn_fwd(c, "conv_fwd", L, a, k.cin, k.Hi, k.Wi, 3, k.stride, 1, P[q], c.w<float>(k.y1), k.cout, k.Ho,
@@ -461,7 +461,7 @@ int deep_forward(const Plan& p, const float* const* P, float* const* bnstat, int
                        c.w<float4>(k.cf1), k.dma1 ? k.nblk1 : 0, an));
         const int64_t P2 = (int64_t)k.Ho * k.Wo;
         {
-            Scope sc(&p.prof, s, "bn_act");
+            Scope sc(&p.prof, s, "bn_act", L);
             if (k.cn) {  // d1 feeds only conv2 (forward and weight gradient): its channel-last image alone
                 NhwcArgs t = nhwc_args(NHWC_ACT, B, k.cout, k.Ho, k.Wo, c.w<float>(k.y1), c.w<void>(k.d1n));
                 t.cf = c.w<float4>(k.cf1);
@@ -487,7 +487,7 @@ int deep_forward(const Plan& p, const float* const* P, float* const* bnstat, int
             res = a;
         }
         {
-            Scope sc(&p.prof, s, "bn_act");
+            Scope sc(&p.prof, s, "bn_act", L + 1);
             if (i < 3 && d.blk[i + 1].cn) {  // the block output and the next block's channel-last input
                 NhwcArgs t = nhwc_args(NHWC_ACT, B, k.cout, k.Ho, k.Wo, c.w<float>(k.y2), c.w<void>(d.blk[i + 1].an));
                 t.cf = c.w<float4>(k.cf2);
@@ -653,7 +653,7 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
         void* dyn1 = k.cn ? c.w<void>(d.dyn1) : nullptr;
         void* dyn2 = k.cn ? c.w<void>(d.dyn2) : nullptr;
         if (k.cn) {
-            Scope sc(&p.prof, s, "dy_nhwc");
+            Scope sc(&p.prof, s, "dy_nhwc", L + 1);
             NhwcArgs t = nhwc_args(NHWC_BNBWD, B, k.cout, k.Ho, k.Wo, g, dyn1);
             t.y = c.w<float>(k.y2);
             t.cf = c.w<float4>(k.cfb2);
@@ -665,7 +665,7 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
                 RC(launch_to_nhwc(t, s));
             }
         } else {
-            Scope sc(&p.prof, s, "bn_bwd_apply");
+            Scope sc(&p.prof, s, "bn_bwd_apply", L + 1);
             // (a routed conv2's dy is produced by its weight-gradient kernel's staging)
             if (!k.w32_2) RC(launch_bn_bwd_apply(g, c.w<float>(k.y2), c.w<float4>(k.cfb2), dy2, B, k.cout, P2, s));
             if (k.sc) RC(launch_bn_bwd_apply(g, c.w<float>(k.ysc), c.w<float4>(k.cfbsc), dysc, B, k.cout, P2, s));
@@ -697,13 +697,13 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
         }
         float* dy1 = dy2;  // dy2 (and its image) are dead after conv2's gradients
         if (k.cn) {
-            Scope sc(&p.prof, s, "dy_nhwc");
+            Scope sc(&p.prof, s, "dy_nhwc", L);
             NhwcArgs t = nhwc_args(NHWC_BNBWD, B, k.cout, k.Ho, k.Wo, dd, dyn1);
             t.y = c.w<float>(k.y1);
             t.cf = c.w<float4>(k.cfb1);
             RC(launch_to_nhwc(t, s));
         } else {
-            Scope sc(&p.prof, s, "bn_bwd_apply");
+            Scope sc(&p.prof, s, "bn_bwd_apply", L);
             if (!k.w32_1) RC(launch_bn_bwd_apply(dd, c.w<float>(k.y1), c.w<float4>(k.cfb1), dy1, B, k.cout, P2, s));
         }
         // ---- conv1 (+ shortcut): gradients of the weights and of the block input
