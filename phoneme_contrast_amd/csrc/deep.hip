@@ -27,6 +27,10 @@ struct DeepBlock {
     // wgrad_w32.hip weight gradient) when their channel counts fit; conv1 of block 0 and conv2
     bool dma1, dma2, w32_1, w32_2;
     WgradArgs wg1, wg2;
+    // ... whose weight gradient runs on the Winograd kernel (wgrad_wino.hip) where it applies (even W);
+    // w32_* then stays set: the BN backward is applied in its staging and dy written by it too
+    bool ww1, ww2;
+    WinoWgradArgs wwa1, wwa2;
     int nblk1, nblk2;
     // precision "bf16" with channel counts the channel-last engine takes (convn.hip): padded NHWC
     // bf16 images of the block input (conv1, shortcut) and of d1 (conv2), kept for the backward
@@ -115,11 +119,14 @@ int build_deep(Plan& p) {
     for (int i = 0; i < 4; ++i) cmax = std::max(cmax, d.h[i]);
     const bool route = !d.bf16;  // fp32: stride-1 3x3 convs on the LDS-DMA / 32x32 engines
     // a stride-1 3x3 conv cin -> cout at HxW on the DMA conv (fwd, dgrad) and the 32x32 wgrad
-    auto plan_routed = [&](int ci, int co, int h, int w, bool* fwd, bool* w32, WgradArgs* wga, int* nblk) {
+    auto plan_routed = [&](int ci, int co, int h, int w, bool* fwd, bool* w32, WgradArgs* wga, int* nblk,
+                           bool* ww, WinoWgradArgs* wwa) {
         *fwd = route && (co == 32 || co % 64 == 0) && (ci == 32 || ci % 64 == 0) && ci % 2 == 0;
-        // the pixel-stream kernel from 50 columns up; narrower rows waste its 8-column stream granule,
-        // the 32x32 row-window kernel takes them
-        *w32 = route && (w >= 50 ? wgrad_s_geometry(B, h, w, ci, co, wga) : wgrad_w32_geometry(B, h, w, ci, co, wga));
+        // the Winograd weight gradient at even widths; else the pixel-stream kernel from 50 columns
+        // up (narrower rows waste its 8-column stream granule: the 32x32 row-window kernel takes them)
+        *ww = route && wgrad_wino_geometry(B, h, w, ci, co, wwa);
+        if (*ww) wg = std::max(wg, (size_t)wwa->nslice * co * ci * 16);
+        *w32 = *ww || (route && (w >= 50 ? wgrad_s_geometry(B, h, w, ci, co, wga) : wgrad_w32_geometry(B, h, w, ci, co, wga)));
         *nblk = 0;
         if (*fwd) {
             // the Winograd conv takes the layers whose rows are >= 31 columns wide (its own tile blocks)
@@ -128,7 +135,7 @@ int build_deep(Plan& p) {
             stat = std::max(stat, (size_t)2 * std::max(ci, co) * (*nblk) + *nblk);
             wpk = std::max(wpk, (size_t)16 * ci * co);
         }
-        if (*w32) wg = std::max(wg, (size_t)wga->nslice * co * ci * 9);
+        if (*w32 && !*ww) wg = std::max(wg, (size_t)wga->nslice * co * ci * 9);
     };
     for (int i = 0; i < 4; ++i) {
         DeepBlock& k = d.blk[i];
@@ -165,10 +172,10 @@ int build_deep(Plan& p) {
             k.d1n = p.carve("nhwc_d1", nhwc_bytes(B, k.cout, k.Ho, k.Wo));
             dynmax = std::max(dynmax, nhwc_bytes(B, k.cout, k.Ho, k.Wo));
         }
-        k.dma1 = k.w32_1 = false;
+        k.dma1 = k.w32_1 = k.ww1 = false;
         k.nblk1 = 0;
-        if (k.stride == 1) plan_routed(k.cin, k.cout, k.Ho, k.Wo, &k.dma1, &k.w32_1, &k.wg1, &k.nblk1);
-        plan_routed(k.cout, k.cout, k.Ho, k.Wo, &k.dma2, &k.w32_2, &k.wg2, &k.nblk2);
+        if (k.stride == 1) plan_routed(k.cin, k.cout, k.Ho, k.Wo, &k.dma1, &k.w32_1, &k.wg1, &k.nblk1, &k.ww1, &k.wwa1);
+        plan_routed(k.cout, k.cout, k.Ho, k.Wo, &k.dma2, &k.w32_2, &k.wg2, &k.nblk2, &k.ww2, &k.wwa2);
         cin = k.cout; H = k.Ho; W = k.Wo;
     }
     d.g = p.carve("g", gmax);
@@ -313,7 +320,22 @@ int conv_bn_fwd(const Ctx& c, const char* label, int layer, const float* x, int 
 int conv_wgrad(const Ctx& c, int layer, const float* x, int cin, int IH, int IW, int k, int stride, int pad,
                const float* dy, int cout, int OH, int OW, float* gw, float* gb, const WgradArgs* w32 = nullptr,
                const float* bn_g = nullptr, const float* bn_y = nullptr, const float4* bn_cf = nullptr,
-               const void* xn = nullptr, const void* dyn = nullptr) {
+               const void* xn = nullptr, const void* dyn = nullptr, const WinoWgradArgs* ww = nullptr) {
+    if (ww) {  // stride-1 3x3, even width: Winograd weight gradient, BN backward in its staging (dy written)
+        WinoWgradArgs w = *ww;
+        w.B = c.p.B; w.H = OH; w.W = OW; w.cin = cin; w.cout = cout;
+        w.dz = bn_g;
+        w.y = bn_y;
+        w.cf_dy = bn_cf;
+        w.dy_out = const_cast<float*>(dy);
+        w.src = x;
+        w.cf_x = nullptr;
+        float* wgp = c.w<float>(c.d.wgp);
+        w.part = wgp;
+        { Scope sc(&c.p.prof, c.s, "wgrad", layer); RC(launch_wgrad_wino(PRO_RAW, w, c.s)); }
+        RC(launch_wgrad_wino_reduce(wgp, w.nslice, cout, cin, gw, c.s));
+        return hip_status_ok(hipMemsetAsync(gb, 0, (size_t)cout * 4, c.s), "memset bias grad");
+    }
     if (w32) {  // stride-1 3x3: pixel-stream (wgrad_s.hip, MT 16) or 32x32 row-window (wgrad_w32.hip) kernel
         WgradArgs w = *w32;
         w.B = c.p.B; w.H = OH; w.W = OW; w.cin = cin; w.cout = cout;
@@ -672,7 +694,8 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
         }
         // ---- conv2
         RC(conv_wgrad(c, L + 1, c.w<float>(k.d1), k.cout, k.Ho, k.Wo, 3, 1, 1, dy2, k.cout, k.Ho, k.Wo, G[q + 4],
-                      G[q + 5], k.w32_2 ? &k.wg2 : nullptr, g, c.w<float>(k.y2), c.w<float4>(k.cfb2), d1n, dyn1));
+                      G[q + 5], k.w32_2 ? &k.wg2 : nullptr, g, c.w<float>(k.y2), c.w<float4>(k.cfb2), d1n, dyn1,
+                      k.ww2 ? &k.wwa2 : nullptr));
         float* dd = c.w<float>(d.dd);
         RC(conv_dgrad(c, L + 1, dy2, k.cout, k.Ho, k.Wo, 3, 1, 1, P[q + 4], dd, k.cout, k.Ho, k.Wo, 0, k.dma2, dyn1));
         // ---- through Dropout2d / ReLU / BN1
@@ -708,7 +731,8 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
         }
         // ---- conv1 (+ shortcut): gradients of the weights and of the block input
         RC(conv_wgrad(c, L, a_in, k.cin, k.Hi, k.Wi, 3, k.stride, 1, dy1, k.cout, k.Ho, k.Wo, G[q], G[q + 1],
-                      k.w32_1 ? &k.wg1 : nullptr, dd, c.w<float>(k.y1), c.w<float4>(k.cfb1), an, dyn1));
+                      k.w32_1 ? &k.wg1 : nullptr, dd, c.w<float>(k.y1), c.w<float4>(k.cfb1), an, dyn1,
+                      k.ww1 ? &k.wwa1 : nullptr));
         float* da = c.w<float>(k.da);
         int acc = 0;
         if (d.residual && !k.sc) {  // identity shortcut: the block input receives g directly
