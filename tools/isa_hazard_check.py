@@ -1,0 +1,89 @@
+#!/usr/bin/env python
+"""Static guard against the gfx950 store-data hazard hipcc 7.2 left unprotected (Kernels):
+a packed f32 VALU instruction (v_pk_*) issued right after a wide vector-memory store (> 64-bit data:
+dwordx3 / dwordx4 / b96 / b128) overwrote the store's data VGPRs before the store had read them,
+with no wait state between them -- every second stored float came out wrong.
+
+Scans the device code of every object under build/ (the .hip_fatbin section, unbundled for gfx950
+and disassembled with ROCm's llvm-objdump) and reports each wide store followed, within the next
+WINDOW instructions and with no s_nop between, by a v_pk_* whose destination overlaps the store's
+data registers (the hazard needs one wait state: flagged when the v_pk_* is the very next
+instruction; the store data of a 4-dword store is read a cycle after its issue).
+
+    python tools/isa_hazard_check.py [build_dir]      (exit 1 on findings)
+"""
+import glob
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+WINDOW = 1  # the hazard needs one wait state: any instruction in between provides it
+STORE = re.compile(r"^\s*(buffer|global|flat|scratch)_store_(dwordx3|dwordx4|b96|b128)\b\s+(.*)$")
+REG = re.compile(r"^v\[(\d+):(\d+)\]$|^v(\d+)$")
+
+
+def regs(tok):
+    tok = tok.strip().rstrip(",")
+    m = REG.match(tok)
+    if not m:
+        return set()
+    if m.group(3) is not None:
+        return {int(m.group(3))}
+    return set(range(int(m.group(1)), int(m.group(2)) + 1))
+
+
+def disassemble(obj, tmp):
+    fat = os.path.join(tmp, "x.fatbin")
+    co = os.path.join(tmp, "x.co")
+    subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fat}", obj], check=True,
+                   stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    subprocess.run([f"{LLVM}/clang-offload-bundler", "--type=o", f"--input={fat}",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}", "--unbundle"], check=True)
+    out = subprocess.run([f"{LLVM}/llvm-objdump", "-d", co], check=True, capture_output=True, text=True).stdout
+    return out.splitlines()
+
+
+def scan(lines):
+    found = []
+    insts = [ln.split("//")[0].rstrip() for ln in lines if ln.startswith("\t") or ln.startswith("  ")]
+    insts = [i for i in insts if i.strip()]
+    for k, ins in enumerate(insts):
+        m = STORE.match(ins)
+        if not m:
+            continue
+        ops = [o.strip() for o in m.group(3).split(",")]
+        # data operand: buffer_store vdata, vaddr, ...; global / flat / scratch_store vaddr, vdata, ...
+        data = regs(ops[0] if m.group(1) == "buffer" else ops[1] if len(ops) > 1 else "")
+        for nxt in insts[k + 1:k + 1 + WINDOW]:
+            op = nxt.split()[0]
+            if op.startswith("s_nop") or op.startswith("s_waitcnt"):
+                break
+            if op.startswith("v_pk_"):
+                dst = regs(nxt.split()[1])
+                if dst & data:
+                    found.append((ins.strip(), nxt.strip()))
+    return found
+
+
+def main():
+    bdir = sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__))), "build")
+    objs = sorted(glob.glob(os.path.join(bdir, "*.o")))
+    if not objs:
+        print(f"no objects under {bdir}")
+        return 2
+    bad = 0
+    with tempfile.TemporaryDirectory() as tmp:
+        for o in objs:
+            for st, pk in scan(disassemble(o, tmp)):
+                print(f"{os.path.basename(o)}: {st}  ->  {pk}")
+                bad += 1
+    print(f"{len(objs)} objects scanned, {bad} hazard(s)")
+    return 1 if bad else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
