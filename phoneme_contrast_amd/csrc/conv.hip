@@ -45,6 +45,27 @@ __device__ __forceinline__ void c1_window(const float* xb, int H, int W, int hh,
     }
 }
 
+// The same window with every load unconditional (row / column clamped into the sample, the value
+// zeroed afterwards): a straight-line load group the compiler can issue ahead of the previous quad's
+// stores.  W % 4 == 0.
+__device__ __forceinline__ void c1_window_ld(const float* xb, int H, int W, int hh, int w0, float (&xr)[3][6]) {
+#pragma unroll
+    for (int dh = 0; dh < 3; ++dh) {
+        const int y = hh + dh - 1;
+        const int yc = min(max(y, 0), H - 1);
+        const float* row = xb + (int64_t)yc * W;
+        const float4 v = ld4(row + w0);
+        const float l = row[max(w0 - 1, 0)], r = row[min(w0 + 4, W - 1)];
+        const bool ok = y == yc;
+        xr[dh][1] = ok ? v.x : 0.f;
+        xr[dh][2] = ok ? v.y : 0.f;
+        xr[dh][3] = ok ? v.z : 0.f;
+        xr[dh][4] = ok ? v.w : 0.f;
+        xr[dh][0] = ok && w0 > 0 ? l : 0.f;
+        xr[dh][5] = ok && w0 + 4 < W ? r : 0.f;
+    }
+}
+
 // A block owns rows_per_blk consecutive (sample, row) image rows; wave w computes output channels
 // 8w .. 8w + 7 (+ 32k) for every pixel quad of those rows: lanes take consecutive quads (1 KB per
 // store instruction), the 3 x 6 input window comes from L1/L2 (the input is 1/32 of the output).
@@ -83,12 +104,36 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Args a) {
         float s1[C1_CPW], s2[C1_CPW];
 #pragma unroll
         for (int j = 0; j < C1_CPW; ++j) s1[j] = s2[j] = 0.f;
-        for (int t = lane; t < ntask; t += 64) {
+        // FULL: the next quad's window is loaded before this quad's stores are issued, so waiting for
+        // it never waits for the stores (vmcnt counts both, in issue order)
+        float xn[3][6];
+        auto locate = [&](int t, int& b, int& hh, int& w0) {
             const int rr = t / nq, q = t - rr * nq;
-            const int gr = r0 + rr, b = gr / a.H, hh = gr - b * a.H;
-            const int w0 = 4 * q;
+            const int gr = r0 + rr;
+            b = gr / a.H;
+            hh = gr - b * a.H;
+            w0 = 4 * q;
+        };
+        if (FULL && lane < ntask) {
+            int b, hh, w0;
+            locate(lane, b, hh, w0);
+            c1_window_ld(a.x + (int64_t)b * HW, a.H, a.W, hh, w0, xn);
+        }
+        for (int t = lane; t < ntask; t += 64) {
+            int b, hh, w0;
+            locate(t, b, hh, w0);
             float xr[3][6];
-            c1_window<FULL>(a.x + (int64_t)b * HW, a.H, a.W, hh, w0, xr);
+            if (FULL) {
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+#pragma unroll
+                    for (int e = 0; e < 6; ++e) xr[i][e] = xn[i][e];
+                int bn, hn, wn;  // (unconditional: the last quad's prefetch repeats a valid one)
+                locate(min(t + 64, ntask - 1), bn, hn, wn);
+                c1_window_ld(a.x + (int64_t)bn * HW, a.H, a.W, hn, wn, xn);
+            } else {
+                c1_window<FULL>(a.x + (int64_t)b * HW, a.H, a.W, hh, w0, xr);
+            }
             float* ob = a.out + ((int64_t)b * a.cout + cg) * HW + (int64_t)hh * a.W + w0;
 #pragma unroll
             for (int j = 0; j < C1_CPW; ++j) {
