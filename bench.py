@@ -126,6 +126,15 @@ def deep_kernel_costs(B, F, T, bf16=False, D=128):
     C0 = DEEP_DIMS[0]
     out["maxpool_fwd"] = (0, B * C0 * (4 * H0 * W0 + 5 * H1 * W1))            # y0 -> a0 + first-max tap
     out["maxpool_bwd"] = (0, B * C0 * (4 * H0 * W0 * 2 + 5 * H1 * W1))        # tap, d a0, y0 -> dz0
+    if bf16 and C0 == 64 and W0 <= 256:
+        # fused stem (conv.hip stem_pool_kernel / stem_wgrad_rc_kernel): y0 is recomputed, never stored;
+        # the stem GEMM's FLOPs count once per recomputation
+        stem = 2 * B * H0 * W0 * C0 * 49
+        xb = 4 * B * H0 * W0
+        out["conv_fwd_L0"] = (stem, xb)                                        # BN0 statistics only
+        out["maxpool_fwd"] = (stem, xb + B * C0 * (9 * H1 * W1 + img * (H1 + 2) * (W1 + 2)))  # a0, tap, ysel, NHWC
+        out["maxpool_bwd"] = (0, B * C0 * (9 * H1 * W1 + 4 * H0 * W0))        # tap, d a0, ysel -> dz0
+        out["wgrad_L0"] = (2 * stem, xb + 4 * B * C0 * H0 * W0)                # dz0 + x (recompute + gradient)
     out["bwd_prep_L0"] = (0, B * C0 * 4 * H0 * W0 * 3)
     H, W, cin = H1, W1, C0
     for i, co in enumerate(DEEP_DIMS):

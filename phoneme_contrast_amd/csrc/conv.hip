@@ -454,7 +454,7 @@ __global__ __launch_bounds__(256) void stem_fwd_mfma_kernel(StemArgs a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) K[r] = __shfl(acc[r], 32 * h, 64);
         }
-        float* ob = a.out + ((int64_t)b * a.cout + 32 * mt) * HW;
+        float* ob = a.out ? a.out + ((int64_t)b * a.cout + 32 * mt) * HW : nullptr;  // none: statistics only
         for (int tt = wt; tt < ntile; tt += 2) {
             int p;
             const f32x16 acc = tile(tt, p);
@@ -463,7 +463,7 @@ __global__ __launch_bounds__(256) void stem_fwd_mfma_kernel(StemArgs a) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const float v = acc[r];
-                    op[acc_row(r, h) * HW] = v;
+                    if (ob) op[acc_row(r, h) * HW] = v;
                     const float d = v - K[r];
                     s1[r] += d;
                     s2[r] = fmaf(d, d, s2[r]);
@@ -497,6 +497,270 @@ __global__ __launch_bounds__(256) void stem_fwd_mfma_kernel(StemArgs a) {
         }
     }
     if (threadIdx.x == 0) a.partn[blockIdx.x] = n;
+}
+
+// ------------------------------------------------------------------ fused bf16 stem (no y0 plane)
+// At T = 200 the stem's 64 x 40 x 200 fp32 output is 8.4 GB per 4096-sample step, written once and
+// read three times (pool, pool backward, weight gradient) -- more HBM traffic than the rest of the
+// network's activations.  The bf16 stem GEMM is ~65 MFLOP per sample (0.1 ms of MFMA per step), so
+// the fused form recomputes y0 wherever it is needed instead: stem_fwd_mfma_kernel with out = nullptr
+// (BN statistics), stem_pool_kernel (pool outputs), stem_wgrad_rc_kernel (weight gradient from dz0).
+// Every recomputation multiplies the same bf16 operands in the same K order as the statistics pass.
+typedef __bf16 st_bf16x4 __attribute__((ext_vector_type(4)));
+constexpr int SP_PO = 36;  // bf16 row stride of the pooled NHWC staging rows (2-way LDS conflicts)
+
+__device__ __forceinline__ float sp_relu(float y, float4 k) { return fmaxf(fmaf(y, k.x, k.y), 0.f); }
+
+// Block (sample b, cout half mt), 4 waves; the sample's x as bf16 in LDS ((H + 7) rows of RW, the
+// stem_fwd_mfma_kernel placement).  Column blocks of cbw <= 32 pixels (ncb = a multiple of 4, wave w
+// owns blocks w, w + 4); per pooled row i a wave computes the y0 tiles of rows 2i and 2i + 1 for its
+// blocks (MFMA: C[cout][pixel], the statistics pass's orientation -> the same values bit for bit),
+// keeps row 2i + 1 in registers as the next step's row 2i - 1, and reduces the window rows in
+// registers: per (cout, column) the y0 of the first row holding the column maximum of ReLU(BN0(y0))
+// and that row's index go to LDS.  Then the block finishes the 3-column windows with the
+// maxpool3_fwd tie rule (first maximum in row-major window order; 255 when the maximum is <= 0),
+// writing a0, the tap, y0 at the tap and (optional) the NHWC bf16 row of a0.
+__global__ __launch_bounds__(256) void stem_pool_kernel(StemArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
+    const int b = blockIdx.x >> 1, mt = blockIdx.x & 1;
+    const int H = a.H, W = a.W, RW = st_rw(W), OH = a.OH, OW = a.OW, OHW = OH * OW, C = a.cout;
+    __bf16* xs = reinterpret_cast<__bf16*>(smem);
+    const int xsb = ((H + 7) * RW * 2 + 15) & ~15;
+    float* vy = reinterpret_cast<float*>(reinterpret_cast<char*>(smem) + xsb);  // [32][W]
+    uint8_t* vk = reinterpret_cast<uint8_t*>(vy + 32 * W);                     // [32][W]
+    __bf16* po = reinterpret_cast<__bf16*>(vk + ((32 * W + 15) & ~15));        // [OW][SP_PO]
+    // the sample, bf16, zero border (every LDS element written once)
+    {
+        const float* xb = a.x + (int64_t)b * H * W;
+        for (int i = threadIdx.x; i < (H + 7) * RW; i += 256) {
+            const int r = i / RW - 3, cc = i - (i / RW) * RW - 4;
+            xs[i] = (__bf16)((r >= 0 && r < H && cc >= 0 && cc < W) ? xb[r * W + cc] : 0.f);
+        }
+    }
+    st_bf16x8 A[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int dh = 2 * s + h, dw = j;
+            A[s][j] = (__bf16)((dh < ST_K && dw < ST_K) ? a.w[(32 * mt + l32) * ST_T + dh * ST_K + dw] : 0.f);
+        }
+    float kx[16], ky[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const float4 k = a.cf[32 * mt + acc_row(r, h)];
+        kx[r] = k.x;
+        ky[r] = k.y;
+    }
+    const int ncb = ((W + 31) / 32 + 3) & ~3, cbw = (W + ncb - 1) / ncb;
+    auto tile = [&](int row, int col) {  // y0 of (row, col .. col + 31) for the lane's 16 couts
+        const __bf16* xb = xs + (row + h) * RW + col + 1;
+        f32x16 acc = {0.f};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            st_bf16x8 Bv;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) Bv[j] = xb[2 * s * RW + j];
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[s], Bv, acc, 0, 0, 0);
+        }
+        return acc;
+    };
+    f32x16 carry[2] = {f32x16{0.f}, f32x16{0.f}};
+    __bf16* nimg = a.pool_nhwc ? static_cast<__bf16*>(a.pool_nhwc) + (int64_t)b * (OH + 2) * (OW + 2) * C + 32 * mt
+                               : nullptr;
+    __syncthreads();
+    for (int i = 0; i < OH; ++i) {
+        const int r0 = 2 * i, r1 = 2 * i + 1;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int cb = wave + 4 * u;
+            if (cb >= ncb) break;
+            const int col = min(cb * cbw + l32, W - 1);  // (clamped lanes compute a real column, unused)
+            const bool own = l32 < cbw && cb * cbw + l32 < W;
+            const f32x16 t0 = tile(r0, col);
+            const f32x16 t1 = r1 < H ? tile(r1, col) : f32x16{0.f};
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float4 k = make_float4(kx[r], ky[r], 0.f, 0.f);
+                float m = -INFINITY, yy = 0.f;
+                int kh = 0;
+                if (i > 0) { m = sp_relu(carry[u][r], k); yy = carry[u][r]; }
+                float v = sp_relu(t0[r], k);
+                if (v > m) { m = v; yy = t0[r]; kh = 1; }
+                if (r1 < H) {
+                    v = sp_relu(t1[r], k);
+                    if (v > m) { m = v; yy = t1[r]; kh = 2; }
+                }
+                if (own) {
+                    const int o = acc_row(r, h) * W + cb * cbw + l32;
+                    vy[o] = yy;
+                    vk[o] = (uint8_t)kh;
+                }
+            }
+            carry[u] = t1;
+        }
+        __syncthreads();
+        // windows: item (c, j), j fastest (coalesced rows of a0 / tap / ysel)
+        const int64_t obase = ((int64_t)b * C + 32 * mt) * OHW + (int64_t)i * OW;
+        for (int idx = threadIdx.x; idx < 32 * OW; idx += 256) {
+            const int c = idx / OW, j = idx - c * OW;
+            const float4 k = a.cf[32 * mt + c];
+            float m = -INFINITY, ys = 0.f;
+            int bkh = 0, bkw = 0;
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+                const int iw = 2 * j - 1 + kw;
+                if (iw < 0 || iw >= W) continue;
+                const float yv = vy[c * W + iw];
+                const int kh = vk[c * W + iw];
+                const float v = sp_relu(yv, k);
+                if (v > m || (v == m && kh < bkh)) { m = v; bkh = kh; bkw = kw; ys = yv; }
+            }
+            const int64_t o = obase + (int64_t)c * OHW + j;
+            a.pool[o] = m;
+            a.pool_arg[o] = m > 0.f ? (uint8_t)(bkh * 3 + bkw) : (uint8_t)255;
+            a.pool_ysel[o] = ys;
+            if (nimg) po[j * SP_PO + c] = (__bf16)m;
+        }
+        __syncthreads();
+        if (nimg) {  // padded NHWC row i + 1 (zero columns 0 and OW + 1; zero rows 0 and OH + 1 at the ends)
+            const int Wp = OW + 2;
+            for (int q = threadIdx.x; q < Wp * 4; q += 256) {
+                const int wp = q >> 2, g = q & 3;
+                st_bf16x8 v{};
+                if (wp >= 1 && wp <= OW) {
+                    const __bf16* src = po + (wp - 1) * SP_PO + 8 * g;
+                    const st_bf16x4 lo = *reinterpret_cast<const st_bf16x4*>(src);
+                    const st_bf16x4 hi = *reinterpret_cast<const st_bf16x4*>(src + 4);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) { v[e] = lo[e]; v[4 + e] = hi[e]; }
+                }
+                *reinterpret_cast<st_bf16x8*>(nimg + ((int64_t)(i + 1) * Wp + wp) * C + 8 * g) = v;
+                if (i == 0) *reinterpret_cast<st_bf16x8*>(nimg + (int64_t)wp * C + 8 * g) = st_bf16x8{};
+                if (i == OH - 1)
+                    *reinterpret_cast<st_bf16x8*>(nimg + ((int64_t)(OH + 1) * Wp + wp) * C + 8 * g) = st_bf16x8{};
+            }
+        }
+    }
+}
+
+// Weight gradient from dz0 with y0 recomputed (the fused stem).  Block = a slice of samples; wave
+// (mt, wt): couts 32 mt .. + 31, every other 32-pixel tile of the sample's virtual pixels (rows
+// padded to WV = W rounded up to 8).  Per tile the recomputation runs transposed, C[pixel][cout] =
+// im2col x W^T, so that lane (cout l32, half h) holds y0 of pixels acc_row(r, h): runs of 4
+// consecutive pixels, which is also where it loads dz0 (16-byte loads) and forms dy = BN backward
+// (stem_wgrad_mfma_kernel's expression, rounded to bf16) in registers.  Those 16 dy values are the A
+// operand of the gradient GEMM dW[cout][tap] = sum_p dy[cout][p] x[p + tap] directly -- K-step ks
+// takes registers 8 ks .. + 7, i.e. pixels 16 ks + 4 h + {0..3, 8..11} -- and the B operand (x at
+// the tap offsets, fp32 LDS as stem_wgrad_mfma_kernel stages it) is read at those same pixels.  No
+// transposition, no dy tile in LDS.
+__global__ __launch_bounds__(256) void stem_wgrad_rc_kernel(StemArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float xs[];  // (H + 8) rows of the sample
+    __shared__ float red[2][32][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
+    const int mt = wave >> 1, wt = wave & 1;
+    const int H = a.H, W = a.W, HW = H * W, RW = st_rw(W), WV = (W + 7) & ~7, HWV = H * WV;
+    const int slice = blockIdx.x;
+    const int b0 = slice * a.rows_per_blk, b1 = min(a.B, b0 + a.rows_per_blk);
+    const int co = 32 * mt + l32;
+    float A1, A2, A3;
+    {
+        const float4 k = a.cf_dy[co];
+        A1 = k.x;
+        A2 = -k.x * k.z;
+        A3 = k.x * (k.w * k.z - k.y);
+    }
+    st_bf16x8 Wt[4];  // B operand of the recomputation: W^T[tap][cout], taps dh = 2 s + h, dw = j
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int dh = 2 * s + h, dw = j;
+            Wt[s][j] = (__bf16)((dh < ST_K && dw < ST_K) ? a.w[co * ST_T + dh * ST_K + dw] : 0.f);
+        }
+    int boff[2];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+        const int t = 32 * nt + l32, dh = t >> 3, dw = t & 7;
+        boff[nt] = dh * RW + dw;
+    }
+    f32x16 acc[2] = {f32x16{0.f}, f32x16{0.f}};
+    for (int i = threadIdx.x; i < (H + 8) * RW; i += 256) xs[i] = 0.f;
+    const int ntile = (HWV + 31) >> 5;
+    for (int b = b0; b < b1; ++b) {
+        __syncthreads();
+        st_stage<true>(a.x + (int64_t)b * HW, H, W, xs);
+        __syncthreads();
+        const float* gp = a.dz + ((int64_t)b * a.cout + co) * HW;
+        for (int tt = wt; tt < ntile; tt += 2) {
+            const int p0 = tt * 32;
+            // y0 of pixel p0 + l32 (A operand: im2col row, taps 8 h .. 8 h + 7 of each K-step)
+            f32x16 y;
+            {
+                const int p = min(p0 + l32, HWV - 1);
+                const int hh = p / WV, ww = p - hh * WV;
+                const float* xb = xs + (hh + h) * RW + ww + 1;
+                y = f32x16{0.f};
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    st_bf16x8 Xv;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) Xv[j] = (__bf16)xb[2 * s * RW + j];
+                    y = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Xv, Wt[s], y, 0, 0, 0);
+                }
+            }
+            // the lane's four pixel runs q: p0 + 8 q + 4 h .. + 3 (one padded row each)
+            int xoff[4];
+            st_bf16x8 dy[2];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int pq = p0 + 8 * q + 4 * h;
+                const int hh = pq / WV, ww = pq - hh * WV;
+                const int nv = hh < H ? min(4, W - ww) : 0;  // real pixels of the run (<= 0: padding)
+                xoff[q] = min(hh, H - 1) * RW + ww + 1;
+                float g[4];
+                if ((W & 3) == 0) {
+                    const float4 t = nv == 4 ? ld4(gp + hh * W + ww) : make_float4(0.f, 0.f, 0.f, 0.f);
+                    g[0] = t.x; g[1] = t.y; g[2] = t.z; g[3] = t.w;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) g[e] = e < nv ? gp[hh * W + ww + e] : 0.f;
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    dy[q >> 1][4 * (q & 1) + e] = (__bf16)(e < nv ? fmaf(A1, g[e], fmaf(A2, y[4 * q + e], A3)) : 0.f);
+            }
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt) {
+                    st_bf16x8 Bv;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) Bv[e] = (__bf16)xs[xoff[2 * ks + (e >> 2)] + boff[nt] + (e & 3)];
+                    acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dy[ks], Bv, acc[nt], 0, 0, 0);
+                }
+        }
+    }
+    if (wt == 1) {
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) red[mt][acc_row(r, h)][32 * nt + l32] = acc[nt][r];
+    }
+    __syncthreads();
+    if (wt == 0) {
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int t = 32 * nt + l32, dh = t >> 3, dw = t & 7;
+                if (dh < ST_K && dw < ST_K) {
+                    const int c = 32 * mt + acc_row(r, h);
+                    a.part[((int64_t)slice * a.cout + c) * ST_T + dh * ST_K + dw] = acc[nt][r] + red[mt][acc_row(r, h)][t];
+                }
+            }
+    }
 }
 
 // bf16 precision, cout = 64: the stem weight gradient as a bf16 MFMA GEMM,
@@ -809,6 +1073,7 @@ int launch_stem_fwd(StemArgs a, int bf16, float* wround, hipStream_t s) {
         PCX_LAUNCH_CHECK("stem_fwd_mfma_kernel");
         return PCX_OK;
     }
+    PCX_CHECK_ARG(a.out, "stem: statistics-only pass needs the bf16 MFMA form");
 #define PCX_STEM_F(B_, C_)                                                                          \
     if ((bf16 != 0) == B_ && a.cout == 4 * C_) {                                                    \
         (void)hipFuncSetAttribute((const void*)stem_fwd_kernel<B_, C_>,                              \
@@ -824,6 +1089,42 @@ int launch_stem_fwd(StemArgs a, int bf16, float* wround, hipStream_t s) {
 
 bool stem_wgrad_mfma_ok(int cout, int H, int W) {
     return cout == 64 && (size_t)(H + 8) * st_rw(W) * 4 + 48 * 1024 <= 160 * 1024;
+}
+
+static size_t stem_pool_smem(int H, int W) {
+    const int OW = (W - 1) / 2 + 1;
+    return (((size_t)(H + 7) * st_rw(W) * 2 + 15) & ~(size_t)15) + (size_t)32 * W * 4 +
+           (((size_t)32 * W + 15) & ~(size_t)15) + (size_t)OW * SP_PO * 2;
+}
+
+bool stem_fused_ok(int cout, int H, int W) {
+    return cout == 64 && W <= 256 && stem_pool_smem(H, W) <= 80 * 1024 &&
+           (size_t)(H + 8) * st_rw(W) * 4 + 16 * 1024 <= 160 * 1024 &&
+           maxpool3_bwd_prep_fits(H, W, (H - 1) / 2 + 1, (W - 1) / 2 + 1);
+}
+
+int launch_stem_pool(StemArgs a, hipStream_t s) {
+    PCX_CHECK_ARG(stem_fused_ok(a.cout, a.H, a.W), "stem_pool: cout %d at %dx%d unsupported", a.cout, a.H, a.W);
+    PCX_CHECK_ARG(a.OH == (a.H - 1) / 2 + 1 && a.OW == (a.W - 1) / 2 + 1, "stem_pool: output %dx%d for %dx%d", a.OH,
+                  a.OW, a.H, a.W);
+    PCX_CHECK_ARG(a.cf && a.pool && a.pool_arg && a.pool_ysel, "stem_pool: missing output");
+    PCX_CHECK_ARG((int64_t)2 * a.B < ((int64_t)1 << 31), "stem_pool: batch %d too large", a.B);
+    const size_t sm = stem_pool_smem(a.H, a.W);
+    (void)hipFuncSetAttribute((const void*)stem_pool_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    stem_pool_kernel<<<(unsigned)(2 * a.B), 256, sm, s>>>(a);
+    PCX_LAUNCH_CHECK("stem_pool_kernel");
+    return PCX_OK;
+}
+
+int launch_stem_wgrad_rc(StemArgs a, hipStream_t s) {
+    PCX_CHECK_ARG(stem_fused_ok(a.cout, a.H, a.W), "stem_wgrad_rc: cout %d at %dx%d unsupported", a.cout, a.H, a.W);
+    PCX_CHECK_ARG(a.dz && a.cf_dy && a.part && a.nblk >= 1 && (int64_t)a.nblk * a.rows_per_blk >= a.B,
+                  "stem_wgrad_rc: bad arguments");
+    const size_t sm = (size_t)(a.H + 8) * st_rw(a.W) * 4;
+    (void)hipFuncSetAttribute((const void*)stem_wgrad_rc_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    stem_wgrad_rc_kernel<<<(unsigned)a.nblk, 256, sm, s>>>(a);
+    PCX_LAUNCH_CHECK("stem_wgrad_rc_kernel");
+    return PCX_OK;
 }
 
 int launch_stem_wgrad(StemArgs a, int bf16, hipStream_t s) {

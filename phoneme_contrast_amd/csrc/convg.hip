@@ -661,20 +661,24 @@ __global__ __launch_bounds__(256) void maxpool3_fwd_lds_kernel(const float* __re
 // maxpool3_bwd_kernel + bwd_prep_kernel on the stem): block (c, slice) walks its samples' planes of
 // channel c; per plane the pooled gradient and the recorded taps are staged in LDS, every input
 // pixel gathers its (at most 2 x 2) windows, g is written once and sum(g), sum(g * xhat) go to the
-// same [C][nslice] partials bwd_prep_kernel produces.
-template <int VEC>
+// same [C][nslice] partials bwd_prep_kernel produces.  SEL: the BN input of a pixel is the pooled
+// ysel value of a window that selected it (every gradient-carrying pixel is some window's selection;
+// the others contribute 0), so no y plane is read.
+template <int VEC, bool SEL>
 __global__ __launch_bounds__(256) void maxpool3_bwd_prep_kernel(const uint8_t* __restrict__ arg,
                                                                 const float* __restrict__ dout,
                                                                 const float* __restrict__ y,
                                                                 const float4* __restrict__ cf, float* __restrict__ g,
                                                                 float* __restrict__ p_g, float* __restrict__ p_x, int B,
                                                                 int C, int H, int W, int OH, int OW, int bps) {
-    extern __shared__ __attribute__((aligned(16))) float dl[];  // [OH*OW] gradients, then [OH*OW] taps
+    // [OH*OW] gradients, (SEL) [OH*OW] selected inputs, then [OH*OW] taps
+    extern __shared__ __attribute__((aligned(16))) float dl[];
     __shared__ double red[4];
     const int c = blockIdx.x, sl = blockIdx.y, nsl = gridDim.y;
     const int b0 = sl * bps, b1 = min(B, b0 + bps);
     const int HW = H * W, OHW = OH * OW, WQ = W / VEC, HWQ = HW / VEC;
-    uint8_t* al = reinterpret_cast<uint8_t*>(dl + OHW);
+    float* ysl = dl + OHW;
+    uint8_t* al = reinterpret_cast<uint8_t*>(dl + (SEL ? 2 : 1) * OHW);
     const float4 k = cf[c];
     double sg = 0.0, sx = 0.0;
     const int q0h = threadIdx.x / WQ, q0w = threadIdx.x - q0h * WQ;
@@ -684,6 +688,7 @@ __global__ __launch_bounds__(256) void maxpool3_bwd_prep_kernel(const uint8_t* _
         for (int i = threadIdx.x; i < OHW; i += 256) {
             dl[i] = dout[row * OHW + i];
             al[i] = arg[row * OHW + i];
+            if (SEL) ysl[i] = y[row * OHW + i];
         }
         __syncthreads();
         const float* yp = y + row * HW;
@@ -691,7 +696,10 @@ __global__ __launch_bounds__(256) void maxpool3_bwd_prep_kernel(const uint8_t* _
         int ih = q0h, iq = q0w;
         for (int q = threadIdx.x; q < HWQ; q += 256) {
             float gv[VEC], yv[VEC];
-            if (VEC == 4) {
+            if (SEL) {
+#pragma unroll
+                for (int e = 0; e < VEC; ++e) yv[e] = 0.f;
+            } else if (VEC == 4) {
                 const float4 t = reinterpret_cast<const float4*>(yp)[q];
                 yv[0] = t.x; yv[1] = t.y; yv[2] = t.z; yv[3] = t.w;
             } else {
@@ -706,7 +714,10 @@ __global__ __launch_bounds__(256) void maxpool3_bwd_prep_kernel(const uint8_t* _
                 for (int oh = oh_lo; oh <= oh_hi; ++oh)
                     for (int ow = ow_lo; ow <= ow_hi; ++ow) {
                         const int kh = ih - (2 * oh - 1), kw = iw - (2 * ow - 1);
-                        if (al[oh * OW + ow] == kh * 3 + kw) acc += dl[oh * OW + ow];
+                        if (al[oh * OW + ow] == kh * 3 + kw) {
+                            acc += dl[oh * OW + ow];
+                            if (SEL) yv[e] = ysl[oh * OW + ow];
+                        }
                     }
                 gv[e] = acc;
                 sg += (double)acc;
@@ -984,23 +995,31 @@ int launch_maxpool3_fwd(const float* y, const float4* cf, float* out, uint8_t* a
 bool maxpool3_bwd_prep_fits(int H, int W, int OH, int OW) {
     (void)H;
     (void)W;
-    return (size_t)OH * OW * 5 <= 64 * 1024;
+    return (size_t)OH * OW * 9 <= 64 * 1024;
 }
 
-int launch_maxpool3_bwd_prep(const uint8_t* arg, const float* dout, const float* y, const float4* cf, float* g,
-                             float* p_g, float* p_x, int B, int C, int H, int W, int OH, int OW, int* nslice,
+int launch_maxpool3_bwd_prep(const uint8_t* arg, const float* dout, const float* y, const float* ysel, const float4* cf,
+                             float* g, float* p_g, float* p_x, int B, int C, int H, int W, int OH, int OW, int* nslice,
                              hipStream_t s) {
     PCX_CHECK_ARG(OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1, "maxpool3: output %dx%d for input %dx%d", OH, OW,
                   H, W);
     PCX_CHECK_ARG(maxpool3_bwd_prep_fits(H, W, OH, OW), "maxpool3_bwd_prep: %dx%d pooled plane exceeds LDS", OH, OW);
+    PCX_CHECK_ARG(y || ysel, "maxpool3_bwd_prep: no BN input");
     int bps;
     const int ns = chan_slices(B, C, &bps);
     *nslice = ns;
-    const size_t lds = ((size_t)OH * OW * 5 + 15) / 16 * 16;
-    if (W % 4 == 0)
-        maxpool3_bwd_prep_kernel<4><<<dim3(C, ns), 256, lds, s>>>(arg, dout, y, cf, g, p_g, p_x, B, C, H, W, OH, OW, bps);
-    else
-        maxpool3_bwd_prep_kernel<1><<<dim3(C, ns), 256, lds, s>>>(arg, dout, y, cf, g, p_g, p_x, B, C, H, W, OH, OW, bps);
+    const size_t lds = ((size_t)OH * OW * (ysel ? 9 : 5) + 15) / 16 * 16;
+#define PCX_MPB(V_, S_)                                                                                         \
+    maxpool3_bwd_prep_kernel<V_, S_><<<dim3(C, ns), 256, lds, s>>>(arg, dout, S_ ? ysel : y, cf, g, p_g, p_x, B, C, \
+                                                                   H, W, OH, OW, bps)
+    if (W % 4 == 0) {
+        if (ysel) PCX_MPB(4, true);
+        else PCX_MPB(4, false);
+    } else {
+        if (ysel) PCX_MPB(1, true);
+        else PCX_MPB(1, false);
+    }
+#undef PCX_MPB
     PCX_LAUNCH_CHECK("maxpool3_bwd_prep_kernel");
     return PCX_OK;
 }

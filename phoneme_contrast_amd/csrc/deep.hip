@@ -45,6 +45,8 @@ struct DeepPlan {
     int h[4];
     int H0, W0, H1, W1;
     size_t y0, a0, cf0, cfb0, dz0, mparg;
+    bool stem_fused;               // bf16 stem with y0 recomputed (no y0 plane; conv.hip stem_pool_kernel)
+    size_t ysel;                   // fused stem: y0 at each window's selected tap
     size_t stemw;                  // bf16-rounded stem weights (precision "bf16")
     int stem_nblk, stem_rows, stem_ns, stem_srows;  // stem forward blocks / weight-gradient slices
     size_t wpk, identw;           // packed 3x3 weights of a routed conv; identity BN coefficients
@@ -88,10 +90,12 @@ int build_deep(Plan& p) {
     d.H0 = p.F; d.W0 = p.T;
     d.H1 = (d.H0 - 1) / 2 + 1; d.W1 = (d.W0 - 1) / 2 + 1;
     const int C0 = d.h[0];
-    d.y0 = p.carve("y0", planes(B, C0, d.H0, d.W0) * 4);
+    d.stem_fused = d.bf16 && stem_fused_ok(C0, d.H0, d.W0);
+    d.y0 = d.stem_fused ? 0 : p.carve("y0", planes(B, C0, d.H0, d.W0) * 4);
     d.dz0 = p.carve("dz0", planes(B, C0, d.H0, d.W0) * 4);
     d.a0 = p.carve("a0", planes(B, C0, d.H1, d.W1) * 4);
     d.mparg = p.carve("maxpool_arg", planes(B, C0, d.H1, d.W1));  // first-max tap per window (uint8)
+    d.ysel = d.stem_fused ? p.carve("ysel", planes(B, C0, d.H1, d.W1) * 4) : 0;
     d.cf0 = p.carve("cf0", C0 * 16);
     d.cfb0 = p.carve("cfb0", C0 * 16);
     int pidx = 4, bnidx = 1, cin = C0, H = d.H1, W = d.W1;
@@ -110,7 +114,8 @@ int build_deep(Plan& p) {
     };
     // the 7x7 stem runs on its own direct kernels (conv.hip): forward partials, gradient slices
     d.stem_nblk = stem_nblk(B, d.H0, &d.stem_rows);
-    d.stem_ns = stem_wgrad_nslice(B, d.H0, &d.stem_srows, d.bf16 && stem_wgrad_mfma_ok(d.h[0], d.H0, d.W0));
+    d.stem_ns = stem_wgrad_nslice(B, d.H0, &d.stem_srows,
+                                  d.stem_fused || (d.bf16 && stem_wgrad_mfma_ok(d.h[0], d.H0, d.W0)));
     stat = std::max(stat, (size_t)3 * C0 * d.stem_nblk + d.stem_nblk);
     wg = std::max(wg, (size_t)d.stem_ns * C0 * 49);
     d.stemw = p.carve("stem_w16", (size_t)C0 * 49 * 4);
@@ -446,7 +451,7 @@ int deep_forward(const Plan& p, const float* const* P, float* const* bnstat, int
     {
         StemArgs sa{};
         sa.B = B; sa.H = d.H0; sa.W = d.W0; sa.cout = C0;
-        sa.x = x; sa.w = P[0]; sa.out = c.w<float>(d.y0);
+        sa.x = x; sa.w = P[0]; sa.out = d.stem_fused ? nullptr : c.w<float>(d.y0);  // fused: statistics only
         sa.nblk = d.stem_nblk; sa.rows_per_blk = d.stem_rows;
         float* part = c.w<float>(d.stat);
         sa.part0 = part;
@@ -463,7 +468,17 @@ int deep_forward(const Plan& p, const float* const* P, float* const* bnstat, int
         Scope sc(&p.prof, s, "bn_fwd_finalize");
         RC(launch_bn_fwd_finalize(f, s));
     }
-    {
+    if (d.stem_fused) {  // y0 recomputed: a0, taps, y0 at the taps and block 0's NHWC input in one pass
+        StemArgs sa{};
+        sa.B = B; sa.H = d.H0; sa.W = d.W0; sa.cout = C0;
+        sa.x = x; sa.w = c.w<float>(d.stemw);
+        sa.cf = c.w<float4>(d.cf0);
+        sa.pool = c.w<float>(d.a0); sa.pool_arg = c.w<uint8_t>(d.mparg); sa.pool_ysel = c.w<float>(d.ysel);
+        sa.pool_nhwc = d.blk[0].cn ? c.w<void>(d.blk[0].an) : nullptr;
+        sa.OH = d.H1; sa.OW = d.W1;
+        Scope sc(&p.prof, s, "maxpool_fwd");
+        RC(launch_stem_pool(sa, s));
+    } else {
         Scope sc(&p.prof, s, "maxpool_fwd");
         RC(launch_maxpool3_fwd(c.w<float>(d.y0), c.w<float4>(d.cf0), c.w<float>(d.a0), c.w<uint8_t>(d.mparg), B, C0,
                                d.H0, d.W0, d.H1, d.W1, s));
@@ -474,7 +489,8 @@ int deep_forward(const Plan& p, const float* const* P, float* const* bnstat, int
         const int q = k.pidx, L = 2 * i + 1;
         const void* an = k.cn ? c.w<void>(k.an) : nullptr;
         const void* d1n = k.cn ? c.w<void>(k.d1n) : nullptr;
-        if (k.cn && (i == 0 || !d.blk[i - 1].cn)) {  // (otherwise written by the previous block's activation)
+        // (otherwise written by the previous block's activation, or for block 0 by the fused stem pool)
+        if (k.cn && (i == 0 ? !d.stem_fused : !d.blk[i - 1].cn)) {
             Scope sc(&p.prof, s, "to_nhwc", L);
             RC(launch_to_nhwc(nhwc_args(NHWC_COPY, B, k.cin, k.Hi, k.Wi, a, c.w<void>(k.an)), s));
         }
@@ -770,7 +786,8 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
         float* p_x = part + (size_t)C0 * nsl;
         {
             Scope sc(&p.prof, s, "maxpool_bwd");
-            RC(launch_maxpool3_bwd_prep(c.w<uint8_t>(d.mparg), dout, c.w<float>(d.y0), c.w<float4>(d.cf0), dz0, p_g,
+            RC(launch_maxpool3_bwd_prep(c.w<uint8_t>(d.mparg), dout, d.stem_fused ? nullptr : c.w<float>(d.y0),
+                                        d.stem_fused ? c.w<float>(d.ysel) : nullptr, c.w<float4>(d.cf0), dz0, p_g,
                                         p_x, B, C0, d.H0, d.W0, d.H1, d.W1, &ns, s));
         }
         RC(bn_bwd(c, C0, ns, p_g, p_x, P[2], c.w<float4>(d.cf0), G[2], G[3], c.w<float4>(d.cfb0), (double)B * P0));
@@ -799,11 +816,19 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
     {
         StemArgs sa{};
         sa.B = B; sa.H = d.H0; sa.W = d.W0; sa.cout = C0;
-        sa.x = x; sa.dz = dz0; sa.y = c.w<float>(d.y0); sa.cf_dy = c.w<float4>(d.cfb0);
+        sa.x = x; sa.dz = dz0; sa.cf_dy = c.w<float4>(d.cfb0);
         float* wgp = c.w<float>(d.wgp);
         sa.part = wgp;
         sa.nblk = d.stem_ns; sa.rows_per_blk = d.stem_srows;
-        { Scope sc(&p.prof, s, "wgrad", 0); RC(launch_stem_wgrad(sa, d.bf16, s)); }
+        if (d.stem_fused) {  // y0 recomputed from the bf16-rounded weights of the forward
+            sa.w = c.w<float>(d.stemw);
+            Scope sc(&p.prof, s, "wgrad", 0);
+            RC(launch_stem_wgrad_rc(sa, s));
+        } else {
+            sa.y = c.w<float>(d.y0);
+            Scope sc(&p.prof, s, "wgrad", 0);
+            RC(launch_stem_wgrad(sa, d.bf16, s));
+        }
         RC(launch_sum_slices(wgp, sa.nblk, (int64_t)C0 * 49, G[0], s));
         // the stem conv feeds a train-mode BN: its bias gradient is exactly 0
         RC(hip_status_ok(hipMemsetAsync(G[1], 0, (size_t)C0 * 4, s), "memset bias grad"));

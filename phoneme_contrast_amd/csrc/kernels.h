@@ -145,10 +145,22 @@ struct StemArgs {
     const float4* cf_dy;
     float* part;          // weight gradient: [nblk slices][cout][49]
     int nblk, rows_per_blk;
+    // fused bf16 stem (y0 recomputed instead of stored): MaxPool(3,2,1)(ReLU(BN0(y0))) outputs
+    const float4* cf;     // BN0 forward coefficients {scale, shift, mean, istd}
+    float* pool;          // a0 [B][cout][OH][OW]
+    uint8_t* pool_arg;    // first-max tap per window (255: window max <= 0)
+    float* pool_ysel;     // y0 at the selected tap (the BN0 backward's xhat input)
+    void* pool_nhwc;      // optional: padded NHWC bf16 image of a0 [B][OH + 2][OW + 2][cout]
+    int OH, OW;
 };
 int stem_nblk(int B, int H, int* rows_per_blk);
 int stem_wgrad_nslice(int B, int H, int* rows_per_slice, bool mfma = false);
 bool stem_wgrad_mfma_ok(int cout, int H, int W);  // bf16: the MFMA weight-gradient form applies
+// fused bf16 stem: forward statistics only (a.out = nullptr), then the pooled outputs from a
+// recomputed y0; weight gradient from dz0 and a recomputed y0 (no y0 plane anywhere)
+bool stem_fused_ok(int cout, int H, int W);
+int launch_stem_pool(StemArgs a, hipStream_t s);
+int launch_stem_wgrad_rc(StemArgs a, hipStream_t s);
 int launch_stem_fwd(StemArgs a, int bf16, float* wround, hipStream_t s);  // wround: [cout][49] scratch (bf16)
 int launch_stem_wgrad(StemArgs a, int bf16, hipStream_t s);
 
@@ -365,9 +377,11 @@ int launch_maxpool3_fwd(const float* y, const float4* cf, float* out, uint8_t* a
                         int OH, int OW, hipStream_t s);
 int launch_maxpool3_bwd(const uint8_t* arg, const float* dout, float* dz, int B, int C, int H, int W, int OH, int OW,
                         hipStream_t s);
-// MaxPool(3,2,1) + ReLU backward fused with the stem BN's backward partial sums (g written once)
+// MaxPool(3,2,1) + ReLU backward fused with the stem BN's backward partial sums (g written once).
+// The BN input comes from the y plane, or (ysel != nullptr, y unused) from the pooled plane of the
+// selected taps' inputs (the fused stem, which keeps no y plane).
 bool maxpool3_bwd_prep_fits(int H, int W, int OH, int OW);
-int launch_maxpool3_bwd_prep(const uint8_t* arg, const float* dout, const float* y, const float4* cf, float* g,
+int launch_maxpool3_bwd_prep(const uint8_t* arg, const float* dout, const float* y, const float* ysel, const float4* cf, float* g,
                              float* p_g, float* p_x, int B, int C, int H, int W, int OH, int OW, int* nslice,
                              hipStream_t s);
 int launch_fill_cf(float4* cf, int C, float4 v, hipStream_t s);
