@@ -1,5 +1,7 @@
 // Host-side network plan shared by the cnn_small (net.hip) and cnn_deep (deep.hip) orchestrators.
 #pragma once
+#include <dlfcn.h>
+
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -41,19 +43,51 @@ struct Profiler {
     }
 };
 
+// Optional ROCTx ranges named like the profiler labels (env PCX_ROCTX=1): under
+// `rocprofv3 --kernel-trace --marker-trace --kernel-rename` every dispatch of a labelled launch
+// carries its label, which scripts/pmc_summary.py uses to key the --pmc passes of the same command
+// by dispatch order.  The library is dlopen'ed, so libpcx has no profiler dependency.
+struct Roctx {
+    int (*push)(const char*) = nullptr;
+    int (*pop)() = nullptr;
+    static Roctx& get() {
+        static Roctx r = [] {
+            Roctx x;
+            const char* e = std::getenv("PCX_ROCTX");
+            if (!e || std::strcmp(e, "1") != 0) return x;
+            void* h = dlopen("librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_GLOBAL);
+            if (!h) h = dlopen("libroctx64.so.4", RTLD_NOW | RTLD_GLOBAL);
+            if (!h) return x;
+            x.push = reinterpret_cast<int (*)(const char*)>(dlsym(h, "roctxRangePushA"));
+            x.pop = reinterpret_cast<int (*)()>(dlsym(h, "roctxRangePop"));
+            if (!x.push || !x.pop) x.push = nullptr, x.pop = nullptr;
+            return x;
+        }();
+        return r;
+    }
+};
+
 struct Scope {
     Profiler* p;
     hipStream_t s;
     hipEvent_t a = nullptr;
     std::string label;
+    bool tx = false;
     Scope(Profiler* prof, hipStream_t st, const char* lab, int layer = -1) : p(prof), s(st) {
-        if (!p->on) return;
+        const Roctx& r = Roctx::get();
+        if (!p->on && !r.push) return;
         label = lab;
         if (layer >= 0) label += "_L" + std::to_string(layer);
+        if (r.push) {
+            r.push(label.c_str());
+            tx = true;
+        }
+        if (!p->on) return;
         a = p->get();
         if (a) (void)hipEventRecord(a, s);
     }
     ~Scope() {
+        if (tx) Roctx::get().pop();
         if (!p->on || !a) return;
         hipEvent_t b = p->get();
         if (!b) return;

@@ -111,6 +111,61 @@ def main(prof_dir, out_json, out_dur=None, key="cnn_small/fp32"):
         print(json.dumps(d, indent=1))
 
 
+def labelled(rename_trace, csv_path, counter):
+    """Per-label values of `counter` from a --pmc pass, keyed by the labels of a kernel trace of the
+    same command run with PCX_ROCTX=1 under `--marker-trace --kernel-rename` (the plan's labels as
+    ROCTx ranges): both runs dispatch the same sequence, so dispatch k of one is dispatch k of the
+    other.  Unlabelled dispatches keep their kernel family name; a name mismatch there aborts."""
+    names = [r["Kernel_Name"] for r in _rows(rename_trace)]
+    disp = defaultdict(dict)
+    for r in _rows(csv_path):
+        disp[int(r["Dispatch_Id"])].setdefault("name", r["Kernel_Name"])
+        if r.get("Counter_Name") == counter:
+            disp[int(r["Dispatch_Id"])]["v"] = disp[int(r["Dispatch_Id"])].get("v", 0.0) + float(r["Counter_Value"])
+    ids = sorted(disp)
+    if len(ids) != len(names):
+        raise SystemExit(f"dispatch counts differ: trace {len(names)} vs pmc {len(ids)}")
+    out = defaultdict(list)
+    prev = None
+    for lab, i in zip(names, ids):
+        pname = disp[i]["name"]
+        base = lambda n: n.replace("(anonymous namespace)", "").split("(")[0].split("<")[0].split("::")[-1].strip()
+        renamed = not ("(" in lab or "<" in lab or "::" in lab)
+        if not renamed:  # not renamed: must be the same kernel
+            if base(lab) != base(pname):
+                raise SystemExit(f"dispatch {i}: trace {base(lab)} vs pmc {base(pname)}")
+            lab = base(lab)
+        if "v" in disp[i]:
+            if lab == prev and renamed:  # consecutive dispatches of one labelled scope: one launch
+                out[lab][-1] += disp[i]["v"]
+            else:
+                out[lab].append(disp[i]["v"])
+        prev = lab
+    return out
+
+
+def main_labelled(rename_trace, prof_dir, out_json, key):
+    fetch = labelled(rename_trace, f"{prof_dir}/pmc_fetch/run_counter_collection.csv", "FETCH_SIZE")
+    write = labelled(rename_trace, f"{prof_dir}/pmc_write/run_counter_collection.csv", "WRITE_SIZE")
+    res = {}
+    for lab in sorted(set(fetch) | set(write)):
+        fv, wv = sorted(fetch.get(lab, [0.0])), sorted(write.get(lab, [0.0]))
+        f, w = fv[len(fv) // 2], wv[len(wv) // 2]
+        res[lab] = {"fetch_size_kb": f, "write_size_kb": w, "launches_seen": len(fv),
+                    "hbm_bytes_per_launch": int(2 * f * 1024 + w * 1024),
+                    "note": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE half-count correction); "
+                            "median over the launches of the label (summed over its dispatches)"}
+    try:
+        with open(out_json) as fi:
+            allres = json.load(fi)
+    except (OSError, ValueError):
+        allres = {}
+    allres[key] = res
+    with open(out_json, "w") as fo:
+        json.dump(allres, fo, indent=1)
+    print(json.dumps(res, indent=1))
+
+
 def stalls(csv_path, out_json):
     """Median of every counter of one --pmc pass, per layer label (analysis aid)."""
     names = sorted({r["Counter_Name"] for r in _rows(csv_path)})
@@ -134,5 +189,7 @@ def stalls(csv_path, out_json):
 if __name__ == "__main__":
     if sys.argv[1] == "--stalls":
         stalls(sys.argv[2], sys.argv[3])
+    elif sys.argv[1] == "--labels":
+        main_labelled(*sys.argv[2:6])
     else:
         main(*sys.argv[1:5])
