@@ -553,6 +553,13 @@ __global__ __launch_bounds__(256) void stem_pool_kernel(StemArgs a) {
         kx[r] = k.x;
         ky[r] = k.y;
     }
+    // the window pass reads the BN coefficients per item: from LDS (a global load per item exposed its
+    // latency once per window)
+    __shared__ float2 kcs[32];
+    if (threadIdx.x < 32) {
+        const float4 k = a.cf[32 * mt + threadIdx.x];
+        kcs[threadIdx.x] = make_float2(k.x, k.y);
+    }
     const int ncb = ((W + 31) / 32 + 3) & ~3, cbw = (W + ncb - 1) / ncb;
     auto tile = [&](int row, int col) {  // y0 of (row, col .. col + 31) for the lane's 16 couts
         const __bf16* xb = xs + (row + h) * RW + col + 1;
@@ -605,7 +612,8 @@ __global__ __launch_bounds__(256) void stem_pool_kernel(StemArgs a) {
         const int64_t obase = ((int64_t)b * C + 32 * mt) * OHW + (int64_t)i * OW;
         for (int idx = threadIdx.x; idx < 32 * OW; idx += 256) {
             const int c = idx / OW, j = idx - c * OW;
-            const float4 k = a.cf[32 * mt + c];
+            const float2 k2 = kcs[c];
+            const float4 k = make_float4(k2.x, k2.y, 0.f, 0.f);
             float m = -INFINITY, ys = 0.f;
             int bkh = 0, bkw = 0;
 #pragma unroll

@@ -335,23 +335,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
 }
 
 // dW[n][c] = G^T dU G per (n, c) from the slices' sum (float64, fixed order); the partials carry
-// row / column 3 of the Winograd domain negated (Yh' of the kernel).
-__global__ void wgrad_wino_reduce_kernel(const float* __restrict__ part, int nslice, int npair, float* __restrict__ dw) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= npair) return;
+// row / column 3 of the Winograd domain negated (Yh' of the kernel).  Block = 16 (n, c) pairs x 16
+// slice groups: thread (group g, pair j) sums slices g, g + 16, ... of its pair (the 16 pairs of a
+// slice are 1 KB contiguous), the groups are added in order through LDS, then 16 threads transform.
+constexpr int RP = 16, RG = 16;
+__global__ __launch_bounds__(256) void wgrad_wino_reduce_kernel(const float* __restrict__ part, int nslice, int npair,
+                                                                float* __restrict__ dw) {
+    __shared__ double red[RG][RP][17];
+    const int j = threadIdx.x & (RP - 1), g = threadIdx.x / RP;
+    const int i = blockIdx.x * RP + j;
     double u[16];
 #pragma unroll
     for (int x = 0; x < 16; ++x) u[x] = 0.0;
-    for (int s = 0; s < nslice; ++s) {
-        const float4* p = reinterpret_cast<const float4*>(part + ((int64_t)s * npair + i) * 16);
+    if (i < npair) {
+        for (int s = g; s < nslice; s += RG) {
+            const float4* p = reinterpret_cast<const float4*>(part + ((int64_t)s * npair + i) * 16);
+            float4 v[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float4 v = p[q];
-            u[4 * q + 0] += v.x;
-            u[4 * q + 1] += v.y;
-            u[4 * q + 2] += v.z;
-            u[4 * q + 3] += v.w;
+            for (int q = 0; q < 4; ++q) v[q] = p[q];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                u[4 * q + 0] += v[q].x;
+                u[4 * q + 1] += v[q].y;
+                u[4 * q + 2] += v[q].z;
+                u[4 * q + 3] += v[q].w;
+            }
         }
+    }
+#pragma unroll
+    for (int x = 0; x < 16; ++x) red[g][j][x] = u[x];
+    __syncthreads();
+    if (g != 0 || i >= npair) return;
+#pragma unroll
+    for (int x = 0; x < 16; ++x) {
+        double t = red[0][j][x];
+        for (int q = 1; q < RG; ++q) t += red[q][j][x];
+        u[x] = t;
     }
     // undo the folded signs: dU[q][e] = s_q s_e dU'[q][e], s_3 = -1
 #pragma unroll
@@ -452,7 +471,7 @@ int launch_wgrad_wino(int pro, WinoWgradArgs a, hipStream_t s) {
 
 int launch_wgrad_wino_reduce(const float* part, int nslice, int cout, int cin, float* dw, hipStream_t s) {
     const int npair = cout * cin;
-    wgrad_wino_reduce_kernel<<<ceil_div(npair, 256), 256, 0, s>>>(part, nslice, npair, dw);
+    wgrad_wino_reduce_kernel<<<ceil_div(npair, RP), RP * RG, 0, s>>>(part, nslice, npair, dw);
     PCX_LAUNCH_CHECK("wgrad_wino_reduce_kernel");
     return PCX_OK;
 }
