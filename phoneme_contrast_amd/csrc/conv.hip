@@ -507,35 +507,60 @@ __global__ __launch_bounds__(256) void stem_fwd_mfma_kernel(StemArgs a) {
 // (BN statistics), stem_pool_kernel (pool outputs), stem_wgrad_rc_kernel (weight gradient from dz0).
 // Every recomputation multiplies the same bf16 operands in the same K order as the statistics pass.
 typedef __bf16 st_bf16x4 __attribute__((ext_vector_type(4)));
-constexpr int SP_PO = 36;  // bf16 row stride of the pooled NHWC staging rows (2-way LDS conflicts)
+typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+constexpr int SP_CB = 15;  // pooled windows per column block (30 image columns + a halo column each side)
+constexpr int SP_LRW = 44; // bf16 row stride of a column block's staged x (40 columns + 4 shifted copies' slack)
 
-__device__ __forceinline__ float sp_relu(float y, float4 k) { return fmaxf(fmaf(y, k.x, k.y), 0.f); }
+__host__ __device__ constexpr int sp_ncb(int OW) { return (OW + SP_CB - 1) / SP_CB; }
+__host__ __device__ constexpr int sp_copy(int H) { return (H + 7) * SP_LRW; }  // bf16 elements per shifted copy
 
-// Block (sample b, cout half mt), 4 waves; the sample's x as bf16 in LDS ((H + 7) rows of RW, the
-// stem_fwd_mfma_kernel placement).  Column blocks of cbw <= 32 pixels (ncb = a multiple of 4, wave w
-// owns blocks w, w + 4); per pooled row i a wave computes the y0 tiles of rows 2i and 2i + 1 for its
-// blocks (MFMA: C[cout][pixel], the statistics pass's orientation -> the same values bit for bit),
-// keeps row 2i + 1 in registers as the next step's row 2i - 1, and reduces the window rows in
-// registers: per (cout, column) the y0 of the first row holding the column maximum of ReLU(BN0(y0))
-// and that row's index go to LDS.  Then the block finishes the 3-column windows with the
-// maxpool3_fwd tie rule (first maximum in row-major window order; 255 when the maximum is <= 0),
-// writing a0, the tap, y0 at the tap and (optional) the NHWC bf16 row of a0.
-__global__ __launch_bounds__(256) void stem_pool_kernel(StemArgs a) {
+__device__ __forceinline__ float sp_relu(float y, float kx, float ky) { return fmaxf(fmaf(y, kx, ky), 0.f); }
+
+// One wave per (sample b, cout half mt, column block k): image columns c0 - 1 .. c0 + 30 (c0 = 30 k) are
+// the wave's 32 MFMA pixel lanes, pooled windows j = 15 k .. 15 k + 14 are centred on its odd lanes.
+// The x columns it needs (c0 - 4 .. c0 + 35, 7 x 7 taps) are staged as bf16 in four copies shifted by
+// 0..3 elements, so that every lane reads its 8 consecutive taps of a K-step as two aligned ds_read_b64
+// (no 16-bit reads).  Per pooled row i: the y0 tiles of rows 2 i and 2 i + 1 (the statistics pass's MFMA
+// orientation and K order: the same values bit for bit; row 2 i - 1 is the previous step's second tile,
+// kept in registers), the column maximum of ReLU(BN0(y0)) over the window rows in registers, then the
+// 3-column windows from the two neighbouring lanes (shuffles) with the maxpool3_fwd tie rule (first
+// maximum in row-major window order; 255 when the maximum is <= 0).  Writes a0, the tap, y0 at the tap
+// and (optional) the padded NHWC bf16 image of a0 (borders included).  No block barrier after staging.
+__global__ __launch_bounds__(64, 2) void stem_pool_kernel(StemArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
-    const int b = blockIdx.x >> 1, mt = blockIdx.x & 1;
-    const int H = a.H, W = a.W, RW = st_rw(W), OH = a.OH, OW = a.OW, OHW = OH * OW, C = a.cout;
     __bf16* xs = reinterpret_cast<__bf16*>(smem);
-    const int xsb = ((H + 7) * RW * 2 + 15) & ~15;
-    float* vy = reinterpret_cast<float*>(reinterpret_cast<char*>(smem) + xsb);  // [32][W]
-    uint8_t* vk = reinterpret_cast<uint8_t*>(vy + 32 * W);                     // [32][W]
-    __bf16* po = reinterpret_cast<__bf16*>(vk + ((32 * W + 15) & ~15));        // [OW][SP_PO]
-    // the sample, bf16, zero border (every LDS element written once)
-    {
-        const float* xb = a.x + (int64_t)b * H * W;
-        for (int i = threadIdx.x; i < (H + 7) * RW; i += 256) {
-            const int r = i / RW - 3, cc = i - (i / RW) * RW - 4;
-            xs[i] = (__bf16)((r >= 0 && r < H && cc >= 0 && cc < W) ? xb[r * W + cc] : 0.f);
+    const int lane = threadIdx.x, h = lane >> 5, l = lane & 31;
+    const int H = a.H, W = a.W, OH = a.OH, OW = a.OW, C = a.cout, ncb = sp_ncb(OW);
+    const int k = blockIdx.x % ncb, mt = (blockIdx.x / ncb) & 1, b = blockIdx.x / (2 * ncb);
+    const int c0 = 2 * SP_CB * k, CP = sp_copy(H);
+    {  // stage x columns c0 - 4 .. c0 + 35 (zero outside the image) into the four shifted copies; the
+       // loads of a batch are all issued before its LDS writes (one memory latency per batch)
+        const auto rs_x = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.x + (int64_t)b * H * W), (short)0,
+                                                            H * W * 4, 0x00020000);
+        constexpr int NB = 10;
+        const int n = (H + 7) * 40;
+        for (int base = 0; base < n; base += NB * 64) {
+            float v[NB];
+#pragma unroll
+            for (int u = 0; u < NB; ++u) {
+                const int idx = base + u * 64 + lane;
+                const int sr = idx / 40, lc = idx - sr * 40;
+                const int xr = sr - 3, xc = c0 - 4 + lc;
+                const bool ok = idx < n && xr >= 0 && xr < H && xc >= 0 && xc < W;  // else 0 (out-of-range offset)
+                v[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_x, ok ? (xr * W + xc) * 4 : 0x7fff0000, 0, 0));
+            }
+#pragma unroll
+            for (int u = 0; u < NB; ++u) {
+                const int idx = base + u * 64 + lane;
+                if (idx < n) {
+                    const int sr = idx / 40, lc = idx - sr * 40;
+                    const __bf16 bv = (__bf16)v[u];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) xs[q * CP + sr * SP_LRW + lc + q] = bv;
+                }
+            }
         }
     }
     st_bf16x8 A[4];
@@ -544,112 +569,291 @@ __global__ __launch_bounds__(256) void stem_pool_kernel(StemArgs a) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int dh = 2 * s + h, dw = j;
-            A[s][j] = (__bf16)((dh < ST_K && dw < ST_K) ? a.w[(32 * mt + l32) * ST_T + dh * ST_K + dw] : 0.f);
+            A[s][j] = (__bf16)((dh < ST_K && dw < ST_K) ? a.w[(32 * mt + l) * ST_T + dh * ST_K + dw] : 0.f);
         }
     float kx[16], ky[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-        const float4 k = a.cf[32 * mt + acc_row(r, h)];
-        kx[r] = k.x;
-        ky[r] = k.y;
+        const float4 cf = a.cf[32 * mt + acc_row(r, h)];
+        kx[r] = cf.x;
+        ky[r] = cf.y;
     }
-    // the window pass reads the BN coefficients per item: from LDS (a global load per item exposed its
-    // latency once per window)
-    __shared__ float2 kcs[32];
-    if (threadIdx.x < 32) {
-        const float4 k = a.cf[32 * mt + threadIdx.x];
-        kcs[threadIdx.x] = make_float2(k.x, k.y);
-    }
-    const int ncb = ((W + 31) / 32 + 3) & ~3, cbw = (W + ncb - 1) / ncb;
-    auto tile = [&](int row, int col) {  // y0 of (row, col .. col + 31) for the lane's 16 couts
-        const __bf16* xb = xs + (row + h) * RW + col + 1;
+    __syncthreads();
+    // lane l reads local columns l .. l + 7 from the copy that puts l at a multiple of 4 elements
+    const int q = (4 - (l & 3)) & 3;
+    const __bf16* xl = xs + q * CP + l + q;
+    auto tile = [&](int row) {  // y0 of image row `row`, columns c0 - 1 + l, the lane's 16 couts
         f32x16 acc = {0.f};
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
+            const __bf16* p = xl + (row + 2 * s + h) * SP_LRW;
+            const st_bf16x4 lo = *reinterpret_cast<const st_bf16x4*>(p);
+            const st_bf16x4 hi = *reinterpret_cast<const st_bf16x4*>(p + 4);
             st_bf16x8 Bv;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) Bv[j] = xb[2 * s * RW + j];
+            for (int e = 0; e < 4; ++e) { Bv[e] = lo[e]; Bv[4 + e] = hi[e]; }
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[s], Bv, acc, 0, 0, 0);
         }
         return acc;
     };
-    f32x16 carry[2] = {f32x16{0.f}, f32x16{0.f}};
-    __bf16* nimg = a.pool_nhwc ? static_cast<__bf16*>(a.pool_nhwc) + (int64_t)b * (OH + 2) * (OW + 2) * C + 32 * mt
+    const int col = c0 - 1 + l;
+    const bool cvalid = col >= 0 && col < W;
+    const int j = SP_CB * k + ((l - 1) >> 1);
+    const bool center = (l & 1) && l < 2 * SP_CB && j < OW;
+    const int Wp = OW + 2, OHW = OH * OW;
+    // outputs (pooled NHWC [B][OH][OW][C]: the 32 couts of a window are one 128-byte line of y0 at the
+    // tap, 32 bytes of taps) through buffer stores: the lane's window in voffset (out of range for lanes
+    // that centre none: the store is dropped), the 8-cout group in soffset
+    constexpr int OOBV = 0x7fff0000;
+    const int64_t pbase = (int64_t)b * OHW * C + 32 * mt;
+    const auto rs_ysel = __builtin_amdgcn_make_buffer_rsrc(a.pool_ysel + pbase, (short)0, (OHW * C - 32 * mt) * 4, 0x00020000);
+    const auto rs_arg = __builtin_amdgcn_make_buffer_rsrc(a.pool_arg + pbase, (short)0, OHW * C - 32 * mt, 0x00020000);
+    __bf16* nimg = a.pool_nhwc ? static_cast<__bf16*>(a.pool_nhwc) + (int64_t)b * (OH + 2) * Wp * C + 32 * mt
                                : nullptr;
-    __syncthreads();
+    const auto rs_nhwc = __builtin_amdgcn_make_buffer_rsrc(nimg, (short)0, ((OH + 2) * Wp * C - 32 * mt) * 2, 0x00020000);
+    // carried row 2 i - 1: raw y0 and its activation (-inf before the first row: no such window row)
+    f32x16 cy = {0.f}, cv;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) cv[r] = -INFINITY;
     for (int i = 0; i < OH; ++i) {
         const int r0 = 2 * i, r1 = 2 * i + 1;
+        const bool has1 = r1 < H;
+        const f32x16 t0 = tile(r0);
+        const f32x16 t1 = tile(has1 ? r1 : r0);
+        // column maxima of ReLU(BN0(y0)) over the window rows 2 i - 1 (kh 0), 2 i (1), 2 i + 1 (2): the
+        // first maximal row (max3, then the first row equal to it); -inf for columns outside the image
+        float ym[16], vm[16];
+        unsigned khp = 0;
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int cb = wave + 4 * u;
-            if (cb >= ncb) break;
-            const int col = min(cb * cbw + l32, W - 1);  // (clamped lanes compute a real column, unused)
-            const bool own = l32 < cbw && cb * cbw + l32 < W;
-            const f32x16 t0 = tile(r0, col);
-            const f32x16 t1 = r1 < H ? tile(r1, col) : f32x16{0.f};
+        for (int r = 0; r < 16; ++r) {
+            const float v0 = sp_relu(t0[r], kx[r], ky[r]);
+            const float v1 = has1 ? sp_relu(t1[r], kx[r], ky[r]) : -INFINITY;
+            const float m = __builtin_fmaxf(__builtin_fmaxf(cv[r], v0), v1);
+            const bool e0 = cv[r] == m, e1 = v0 == m;
+            const unsigned kh = e0 ? 0u : (e1 ? 1u : 2u);
+            ym[r] = e0 ? cy[r] : (e1 ? t0[r] : t1[r]);
+            vm[r] = cvalid ? m : -INFINITY;
+            khp |= kh << (2 * r);
+            cv[r] = v1;
+        }
+        cy = t1;
+        const unsigned khl = (unsigned)__shfl((int)khp, lane - 1, 64), khr = (unsigned)__shfl((int)khp, lane + 1, 64);
+        const int vo = center ? ((i * OW + j) * C + 4 * h) : OOBV;                // element offset
+        const int vn = center && nimg ? (((i + 1) * Wp + j + 1) * C + 4 * h) * 2 : OOBV;  // NHWC byte offset
+        st_bf16x4 nv;
+        f32x4_t yv;
+        unsigned av = 0;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float4 k = make_float4(kx[r], ky[r], 0.f, 0.f);
-                float m = -INFINITY, yy = 0.f;
-                int kh = 0;
-                if (i > 0) { m = sp_relu(carry[u][r], k); yy = carry[u][r]; }
-                float v = sp_relu(t0[r], k);
-                if (v > m) { m = v; yy = t0[r]; kh = 1; }
-                if (r1 < H) {
-                    v = sp_relu(t1[r], k);
-                    if (v > m) { m = v; yy = t1[r]; kh = 2; }
-                }
-                if (own) {
-                    const int o = acc_row(r, h) * W + cb * cbw + l32;
-                    vy[o] = yy;
-                    vk[o] = (uint8_t)kh;
-                }
+        for (int r = 0; r < 16; ++r) {
+            // the window over columns (l - 1, l, l + 1): maximum, then the first tap holding it in
+            // row-major order (kh 3 + kw); activations are exact copies, so equality is exact
+            const float vl = __shfl(vm[r], lane - 1, 64), vr = __shfl(vm[r], lane + 1, 64);
+            const float yl = __shfl(ym[r], lane - 1, 64), yr = __shfl(ym[r], lane + 1, 64);
+            const float m = __builtin_fmaxf(__builtin_fmaxf(vl, vm[r]), vr);
+            const unsigned tl = ((khl >> (2 * r)) & 3u) * 3u, tc = ((khp >> (2 * r)) & 3u) * 3u + 1u,
+                           tr = ((khr >> (2 * r)) & 3u) * 3u + 2u;
+            const unsigned sl = vl == m ? tl : 15u, sc = vm[r] == m ? tc : 15u, sr = vr == m ? tr : 15u;
+            const unsigned sel = min(min(sl, sc), sr);
+            // registers 4 g .. 4 g + 3 are couts 32 mt + 8 g + 4 h .. + 3: one 16-byte y0 store, one
+            // 4-byte tap store, one 8-byte NHWC store per group
+            yv[r & 3] = sel == sl ? yl : (sel == sc ? ym[r] : yr);
+            av |= (m > 0.f ? sel : 255u) << (8 * (r & 3));
+            nv[r & 3] = (__bf16)m;
+            if ((r & 3) == 3) {
+                const int g = r >> 2;
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, yv), rs_ysel, vo * 4, 32 * g, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(av, rs_arg, vo, 8 * g, 0);
+                if (nimg) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, nv), rs_nhwc, vn, 16 * g, 0);
+                av = 0;
             }
-            carry[u] = t1;
+        }
+    }
+    if (nimg) {  // zero ring: rows 0 and OH + 1 over this block's columns, columns 0 / OW + 1 of the edge blocks
+        const int jlo = k == 0 ? 0 : SP_CB * k + 1, jhi = min(SP_CB * k + SP_CB, OW) + (k == ncb - 1 ? 1 : 0);
+        const int nrow = jhi - jlo + 1, ncol = (k == 0 ? OH : 0) + (k == ncb - 1 ? OH : 0);
+        for (int t = lane; t < 8 * (2 * nrow + ncol); t += 64) {
+            const int pos = t >> 3, part = t & 7;
+            int rr, cc;
+            if (pos < 2 * nrow) {
+                rr = pos < nrow ? 0 : OH + 1;
+                cc = jlo + (pos < nrow ? pos : pos - nrow);
+            } else {
+                const int e = pos - 2 * nrow;
+                rr = 1 + (k == 0 ? (e < OH ? e : e - OH) : e);
+                cc = (k == 0 && e < OH) ? 0 : OW + 1;
+            }
+            *reinterpret_cast<st_bf16x4*>(nimg + ((int64_t)rr * Wp + cc) * C + 4 * part) = st_bf16x4{};
+        }
+    }
+}
+
+// MaxPool(3,2,1) + ReLU backward of the fused stem, fused with the BN0 backward sums.  Block (sample b,
+// cout half hf) walks the pooled rows: rows i and i + 1 of the gated pooled gradient (0 where the window
+// maximum was <= 0) and of the taps sit in a two-slot LDS ring, row i + 2 is loaded into registers while
+// band i is produced.  A thread owns 2 x 2 input pixels (rows 2 i, 2 i + 1, columns 2 m, 2 m + 1) of a
+// cout: the only windows that can select them are (i, m), (i, m + 1), (i + 1, m), (i + 1, m + 1), each
+// through one fixed tap, added in window order (the reference's accumulation order).  dz0 is written as
+// bf16 (its only consumer, the weight gradient, rounds dy to bf16 anyway).  The BN0 backward sums run
+// over the windows as their rows are staged: sum dz0 = sum of the gated gradient, sum dz0 * xhat = sum
+// of gated * xhat(y0 at the tap) -- the per-pixel sums regrouped.  Partials per (cout, sample).
+constexpr int SPB_T = 256;
+constexpr int SPB_NI = 16;  // staged items per thread and row: 32 * OW <= 16 * 256 (OW <= 128)
+
+// one pooled row of the half: gradient items (c, j) from the NCHW planes (+ the second addend), tap / y0
+// items (j = t >> 5, c = t & 31) from the pooled NHWC runs.  Every load is unconditional (items out of
+// range read element 0 and are replaced afterwards), so a row's loads are all in flight together.
+template <bool TWO>
+__device__ __forceinline__ void spb_load_row(int row, int OH, int OW, int OHW, int n, int C, int hf, int c_0, int j_0,
+                                             int cq, int cr, const float* __restrict__ dp, const float* __restrict__ dp2,
+                                             const float* __restrict__ yp, const uint8_t* __restrict__ ap,
+                                             float (&dv)[SPB_NI], float (&yv)[SPB_NI], int (&av)[SPB_NI]) {
+    const bool rok = row < OH;
+    int c = c_0, j = j_0;
+#pragma unroll
+    for (int u = 0; u < SPB_NI; ++u) {
+        const int t = u * SPB_T + (int)threadIdx.x;
+        const bool ok = t < n && rok;
+        const int jj = t >> 5, cc = t & 31;
+        const int od = ok ? c * OHW + row * OW + j : 0;
+        const int on = ok ? (row * OW + jj) * C + 32 * hf + cc : 0;
+        float d = dp[od];
+        if (TWO) d += dp2[od];
+        const float y = yp[on];
+        const int ab = ap[on];
+        dv[u] = ok ? d : 0.f;
+        yv[u] = ok ? y : 0.f;
+        av[u] = ok ? ab : 255;
+        c += cq;
+        j += cr;
+        if (j >= OW) { j -= OW; ++c; }
+    }
+}
+
+__global__ __launch_bounds__(SPB_T) void stem_pool_bwd_kernel(StemArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int b = blockIdx.x >> 1, hf = blockIdx.x & 1, C = a.cout;
+    const int H = a.H, W = a.W, OH = a.OH, OW = a.OW, OHW = OH * OW, n = 32 * OW;
+    float* gl = sm;                                              // [2][32][OW] gated gradient
+    uint8_t* al = reinterpret_cast<uint8_t*>(sm + 2 * n);        // [2][32][OW] taps
+    float* ysl = reinterpret_cast<float*>(al + ((2 * n + 15) & ~15));  // [32][OW] y0 at the tap (sums)
+    __shared__ float kz[32], kw4[32];
+    if (threadIdx.x < 32) {
+        const float4 k = a.cf[32 * hf + threadIdx.x];
+        kz[threadIdx.x] = k.z;
+        kw4[threadIdx.x] = k.w;
+    }
+    const float* dpb = a.dpool + ((int64_t)b * C + 32 * hf) * OHW;   // NCHW planes of the half
+    const float* dpb2 = a.dpool2 ? a.dpool2 + ((int64_t)b * C + 32 * hf) * OHW : dpb;
+    const float* ypb = a.pool_ysel + (int64_t)b * OHW * C;            // pooled NHWC of the sample
+    const uint8_t* apb = a.pool_arg + (int64_t)b * OHW * C;
+    const bool two = a.dpool2 != nullptr;
+    float dv[SPB_NI], yv[SPB_NI];
+    int av[SPB_NI];
+    // item t = u * 256 + tid as (c, j) = (t / OW, t % OW), advanced per u without divisions
+    const int cq = SPB_T / OW, cr = SPB_T - cq * OW;
+    const int c_0 = (int)threadIdx.x / OW, j_0 = (int)threadIdx.x - c_0 * OW;
+#define PCX_SPB_LOAD(ROW)                                                                                    \
+    do {                                                                                                     \
+        if (two) spb_load_row<true>(ROW, OH, OW, OHW, n, C, hf, c_0, j_0, cq, cr, dpb, dpb2, ypb, apb, dv, yv, av);  \
+        else spb_load_row<false>(ROW, OH, OW, OHW, n, C, hf, c_0, j_0, cq, cr, dpb, dpb2, ypb, apb, dv, yv, av); \
+    } while (0)
+    // taps and y0 first (NHWC items), a barrier, the gradient gated by its tap (NCHW items), a barrier,
+    // then the BN0 sums of the row: thread t sums channel t >> 3 over columns t & 7, t & 7 + 8, ...
+    double sg = 0.0, sx = 0.0;
+    const int sc_c = threadIdx.x >> 3, sc_j = threadIdx.x & 7;
+    auto store_row = [&](int slot) {
+        float* g = gl + slot * n;
+        uint8_t* ap = al + slot * n;
+#pragma unroll
+        for (int u = 0; u < SPB_NI; ++u) {
+            const int t = u * SPB_T + (int)threadIdx.x;
+            if (t < n) {
+                const int jj = t >> 5, cc = t & 31;
+                ap[cc * OW + jj] = (uint8_t)av[u];
+                ysl[cc * OW + jj] = yv[u];
+            }
         }
         __syncthreads();
-        // windows: item (c, j), j fastest (coalesced rows of a0 / tap / ysel)
-        const int64_t obase = ((int64_t)b * C + 32 * mt) * OHW + (int64_t)i * OW;
-        for (int idx = threadIdx.x; idx < 32 * OW; idx += 256) {
-            const int c = idx / OW, j = idx - c * OW;
-            const float2 k2 = kcs[c];
-            const float4 k = make_float4(k2.x, k2.y, 0.f, 0.f);
-            float m = -INFINITY, ys = 0.f;
-            int bkh = 0, bkw = 0;
 #pragma unroll
-            for (int kw = 0; kw < 3; ++kw) {
-                const int iw = 2 * j - 1 + kw;
-                if (iw < 0 || iw >= W) continue;
-                const float yv = vy[c * W + iw];
-                const int kh = vk[c * W + iw];
-                const float v = sp_relu(yv, k);
-                if (v > m || (v == m && kh < bkh)) { m = v; bkh = kh; bkw = kw; ys = yv; }
-            }
-            const int64_t o = obase + (int64_t)c * OHW + j;
-            a.pool[o] = m;
-            a.pool_arg[o] = m > 0.f ? (uint8_t)(bkh * 3 + bkw) : (uint8_t)255;
-            a.pool_ysel[o] = ys;
-            if (nimg) po[j * SP_PO + c] = (__bf16)m;
+        for (int u = 0; u < SPB_NI; ++u) {
+            const int t = u * SPB_T + (int)threadIdx.x;
+            if (t < n) g[t] = ap[t] != 255 ? dv[u] : 0.f;
         }
         __syncthreads();
-        if (nimg) {  // padded NHWC row i + 1 (zero columns 0 and OW + 1; zero rows 0 and OH + 1 at the ends)
-            const int Wp = OW + 2;
-            for (int q = threadIdx.x; q < Wp * 4; q += 256) {
-                const int wp = q >> 2, g = q & 3;
-                st_bf16x8 v{};
-                if (wp >= 1 && wp <= OW) {
-                    const __bf16* src = po + (wp - 1) * SP_PO + 8 * g;
-                    const st_bf16x4 lo = *reinterpret_cast<const st_bf16x4*>(src);
-                    const st_bf16x4 hi = *reinterpret_cast<const st_bf16x4*>(src + 4);
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) { v[e] = lo[e]; v[4 + e] = hi[e]; }
+        const float kzc = kz[sc_c], kwc = kw4[sc_c];
+        for (int j = sc_j; j < OW; j += 8) {
+            const float gv = g[sc_c * OW + j];
+            sg += (double)gv;
+            sx += (double)gv * (double)((ysl[sc_c * OW + j] - kzc) * kwc);
+        }
+    };
+    __syncthreads();
+    PCX_SPB_LOAD(0);
+    store_row(0);
+    PCX_SPB_LOAD(1);
+    __syncthreads();
+    store_row(1);
+    const int MW = (W + 1) >> 1;  // 2-column groups per row
+    for (int i = 0; i < OH; ++i) {
+        PCX_SPB_LOAD(i + 2);  // in flight under the band
+        __syncthreads();  // rows i, i + 1 staged
+        const float* g0 = gl + (i & 1) * n;
+        const float* g1 = gl + ((i + 1) & 1) * n;
+        const uint8_t* a0 = al + (i & 1) * n;
+        const uint8_t* a1 = al + ((i + 1) & 1) * n;
+        const bool r1ok = 2 * i + 1 < H, w1ok = i + 1 < OH;
+        int c = (int)threadIdx.x / MW, m = (int)threadIdx.x - c * MW;
+        const int mq = SPB_T / MW, mr = SPB_T - mq * MW;
+        for (int t = threadIdx.x; t < 32 * MW; t += SPB_T, c += mq, m += mr) {
+            if (m >= MW) { m -= MW; ++c; }
+            const int o00 = c * OW + m;
+            const bool m1 = m + 1 < OW;
+            // taps of the four windows (255: none)
+            const int t00 = a0[o00], t01 = m1 ? a0[o00 + 1] : 255;
+            const int t10 = w1ok ? a1[o00] : 255, t11 = (w1ok && m1) ? a1[o00 + 1] : 255;
+            const float d00 = g0[o00], d01 = m1 ? g0[o00 + 1] : 0.f;
+            const float d10 = w1ok ? g1[o00] : 0.f, d11 = (w1ok && m1) ? g1[o00 + 1] : 0.f;
+            // pixel (2 i + dr, 2 m + dc) <- window (i + wi, m + wj) through tap (1 + dr - 2 wi) * 3 + (1 + dc - 2 wj)
+            float p00 = 0.f, p01 = 0.f, p10 = 0.f, p11 = 0.f;
+            if (t00 == 4) p00 += d00;
+            if (t00 == 5) p01 += d00;
+            if (t01 == 3) p01 += d01;
+            if (t00 == 7) p10 += d00;
+            if (t10 == 1) p10 += d10;
+            if (t00 == 8) p11 += d00;
+            if (t01 == 6) p11 += d01;
+            if (t10 == 2) p11 += d10;
+            if (t11 == 0) p11 += d11;
+            uint16_t* zr = a.dz16 + (((int64_t)b * C + 32 * hf + c) * H + 2 * i) * W + 2 * m;
+            const bool c1 = 2 * m + 1 < W;
+            if (c1 && (W & 1) == 0) {
+                *reinterpret_cast<uint32_t*>(zr) = (unsigned)__builtin_bit_cast(uint16_t, (__bf16)p00) |
+                                                   ((unsigned)__builtin_bit_cast(uint16_t, (__bf16)p01) << 16);
+                if (r1ok)
+                    *reinterpret_cast<uint32_t*>(zr + W) = (unsigned)__builtin_bit_cast(uint16_t, (__bf16)p10) |
+                                                           ((unsigned)__builtin_bit_cast(uint16_t, (__bf16)p11) << 16);
+            } else {
+                zr[0] = __builtin_bit_cast(uint16_t, (__bf16)p00);
+                if (c1) zr[1] = __builtin_bit_cast(uint16_t, (__bf16)p01);
+                if (r1ok) {
+                    zr[W] = __builtin_bit_cast(uint16_t, (__bf16)p10);
+                    if (c1) zr[W + 1] = __builtin_bit_cast(uint16_t, (__bf16)p11);
                 }
-                *reinterpret_cast<st_bf16x8*>(nimg + ((int64_t)(i + 1) * Wp + wp) * C + 8 * g) = v;
-                if (i == 0) *reinterpret_cast<st_bf16x8*>(nimg + (int64_t)wp * C + 8 * g) = st_bf16x8{};
-                if (i == OH - 1)
-                    *reinterpret_cast<st_bf16x8*>(nimg + ((int64_t)(OH + 1) * Wp + wp) * C + 8 * g) = st_bf16x8{};
             }
         }
+        __syncthreads();  // band done: slot i & 1 is free
+        if (i + 2 < OH) store_row(i & 1);
+    }
+    // the 8 threads of a channel: fixed butterfly order; partials [C][B] (one slice per sample)
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) {
+        sg += __shfl_xor(sg, o, 64);
+        sx += __shfl_xor(sx, o, 64);
+    }
+#undef PCX_SPB_LOAD
+    if (sc_j == 0) {
+        a.p_g[(int64_t)(32 * hf + sc_c) * a.B + b] = (float)sg;
+        a.p_x[(int64_t)(32 * hf + sc_c) * a.B + b] = (float)sx;
     }
 }
 
@@ -700,7 +904,10 @@ __global__ __launch_bounds__(256) void stem_wgrad_rc_kernel(StemArgs a) {
         __syncthreads();
         st_stage<true>(a.x + (int64_t)b * HW, H, W, xs);
         __syncthreads();
-        const float* gp = a.dz + ((int64_t)b * a.cout + co) * HW;
+        // dz0 (bf16) of the sample: one wave-uniform resource, the lane's cout plane in the offset
+        const auto rs_g = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.dz16 + (int64_t)b * a.cout * HW), (short)0,
+                                                            a.cout * HW * 2, 0x00020000);
+        const uint16_t* gp = a.dz16 + ((int64_t)b * a.cout + co) * HW;
         for (int tt = wt; tt < ntile; tt += 2) {
             const int p0 = tt * 32;
             // y0 of pixel p0 + l32 (A operand: im2col row, taps 8 h .. 8 h + 7 of each K-step)
@@ -729,11 +936,12 @@ __global__ __launch_bounds__(256) void stem_wgrad_rc_kernel(StemArgs a) {
                 xoff[q] = min(hh, H - 1) * RW + ww + 1;
                 float g[4];
                 if ((W & 3) == 0) {
-                    const float4 t = nv == 4 ? ld4(gp + hh * W + ww) : make_float4(0.f, 0.f, 0.f, 0.f);
-                    g[0] = t.x; g[1] = t.y; g[2] = t.z; g[3] = t.w;
+                    const uint2 t = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs_g, nv == 4 ? (co * HW + hh * W + ww) * 2 : 0x7fff0000, 0, 0));
+                    g[0] = __uint_as_float(t.x << 16); g[1] = __uint_as_float(t.x & 0xffff0000u);
+                    g[2] = __uint_as_float(t.y << 16); g[3] = __uint_as_float(t.y & 0xffff0000u);
                 } else {
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) g[e] = e < nv ? gp[hh * W + ww + e] : 0.f;
+                    for (int e = 0; e < 4; ++e) g[e] = e < nv ? __uint_as_float((unsigned)gp[hh * W + ww + e] << 16) : 0.f;
                 }
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
@@ -1100,9 +1308,8 @@ bool stem_wgrad_mfma_ok(int cout, int H, int W) {
 }
 
 static size_t stem_pool_smem(int H, int W) {
-    const int OW = (W - 1) / 2 + 1;
-    return (((size_t)(H + 7) * st_rw(W) * 2 + 15) & ~(size_t)15) + (size_t)32 * W * 4 +
-           (((size_t)32 * W + 15) & ~(size_t)15) + (size_t)OW * SP_PO * 2;
+    (void)W;
+    return (size_t)4 * sp_copy(H) * 2;
 }
 
 bool stem_fused_ok(int cout, int H, int W) {
@@ -1115,18 +1322,33 @@ int launch_stem_pool(StemArgs a, hipStream_t s) {
     PCX_CHECK_ARG(stem_fused_ok(a.cout, a.H, a.W), "stem_pool: cout %d at %dx%d unsupported", a.cout, a.H, a.W);
     PCX_CHECK_ARG(a.OH == (a.H - 1) / 2 + 1 && a.OW == (a.W - 1) / 2 + 1, "stem_pool: output %dx%d for %dx%d", a.OH,
                   a.OW, a.H, a.W);
-    PCX_CHECK_ARG(a.cf && a.pool && a.pool_arg && a.pool_ysel, "stem_pool: missing output");
-    PCX_CHECK_ARG((int64_t)2 * a.B < ((int64_t)1 << 31), "stem_pool: batch %d too large", a.B);
+    PCX_CHECK_ARG(a.cf && a.pool_arg && a.pool_ysel, "stem_pool: missing output");
+    PCX_CHECK_ARG((int64_t)2 * a.B * sp_ncb(a.OW) < ((int64_t)1 << 31), "stem_pool: batch %d too large", a.B);
     const size_t sm = stem_pool_smem(a.H, a.W);
     (void)hipFuncSetAttribute((const void*)stem_pool_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-    stem_pool_kernel<<<(unsigned)(2 * a.B), 256, sm, s>>>(a);
+    stem_pool_kernel<<<(unsigned)(2 * a.B * sp_ncb(a.OW)), 64, sm, s>>>(a);
     PCX_LAUNCH_CHECK("stem_pool_kernel");
+    return PCX_OK;
+}
+
+int launch_stem_pool_bwd(StemArgs a, int* nslice, hipStream_t s) {
+    PCX_CHECK_ARG(stem_fused_ok(a.cout, a.H, a.W), "stem_pool_bwd: cout %d at %dx%d unsupported", a.cout, a.H, a.W);
+    PCX_CHECK_ARG(a.OH == (a.H - 1) / 2 + 1 && a.OW == (a.W - 1) / 2 + 1, "stem_pool_bwd: output %dx%d for %dx%d", a.OH,
+                  a.OW, a.H, a.W);
+    PCX_CHECK_ARG(a.dpool && a.pool_arg && a.pool_ysel && a.cf && a.dz16 && a.p_g && a.p_x,
+                  "stem_pool_bwd: missing argument");
+    PCX_CHECK_ARG(a.cout == 64 && a.OW <= 128 && (int64_t)2 * a.B < ((int64_t)1 << 31), "stem_pool_bwd: shape");
+    *nslice = a.B;  // partials [cout][B]
+    const int n = 32 * a.OW;
+    const size_t lds = (size_t)2 * n * 4 + ((2 * n + 15) & ~15) + (size_t)n * 4;
+    stem_pool_bwd_kernel<<<(unsigned)(2 * a.B), SPB_T, lds, s>>>(a);
+    PCX_LAUNCH_CHECK("stem_pool_bwd_kernel");
     return PCX_OK;
 }
 
 int launch_stem_wgrad_rc(StemArgs a, hipStream_t s) {
     PCX_CHECK_ARG(stem_fused_ok(a.cout, a.H, a.W), "stem_wgrad_rc: cout %d at %dx%d unsupported", a.cout, a.H, a.W);
-    PCX_CHECK_ARG(a.dz && a.cf_dy && a.part && a.nblk >= 1 && (int64_t)a.nblk * a.rows_per_blk >= a.B,
+    PCX_CHECK_ARG(a.dz16 && a.cf_dy && a.part && a.nblk >= 1 && (int64_t)a.nblk * a.rows_per_blk >= a.B,
                   "stem_wgrad_rc: bad arguments");
     const size_t sm = (size_t)(a.H + 8) * st_rw(a.W) * 4;
     (void)hipFuncSetAttribute((const void*)stem_wgrad_rc_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);

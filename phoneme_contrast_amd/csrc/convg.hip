@@ -461,7 +461,15 @@ __global__ __launch_bounds__(256) void bwd_prep_kernel(BwdPrepArgs a) {
         for (int u = 0; u < U; ++u) {
             g[u] = *reinterpret_cast<const fv*>(a.d + o[u]);
             if (a.d2) g[u] += *reinterpret_cast<const fv*>(a.d2 + o[u]);
-            m[u] = a.mask_mode != MASK_NONE ? *reinterpret_cast<const fv*>(a.mask_src + o[u]) : fv{};
+            if (a.mask_mode == MASK_OUT8) {  // V mask bytes as 0 / 1 floats
+                unsigned mb;
+                if (V == 4) mb = *reinterpret_cast<const unsigned*>(a.mask8 + o[u]);
+                else mb = a.mask8[o[u]];
+#pragma unroll
+                for (int e = 0; e < V; ++e) m[u][e] = (float)((mb >> (8 * e)) & 0xffu);
+            } else {
+                m[u] = a.mask_mode != MASK_NONE ? *reinterpret_cast<const fv*>(a.mask_src + o[u]) : fv{};
+            }
             y1v[u] = a.y1 ? *reinterpret_cast<const fv*>(a.y1 + o[u]) : fv{};
             y2v[u] = a.y2 ? *reinterpret_cast<const fv*>(a.y2 + o[u]) : fv{};
         }
@@ -473,13 +481,13 @@ __global__ __launch_bounds__(256) void bwd_prep_kernel(BwdPrepArgs a) {
             float tg = 0.f, t1 = 0.f, t2 = 0.f;
 #pragma unroll
             for (int e = 0; e < V; ++e) {
-                if (a.mask_mode == MASK_OUT) gv[e] = m[u][e] > 0.f ? gv[e] : 0.f;
+                if (a.mask_mode == MASK_OUT || a.mask_mode == MASK_OUT8) gv[e] = m[u][e] > 0.f ? gv[e] : 0.f;
                 else if (a.mask_mode == MASK_BN) gv[e] = fmaf(m[u][e], mc.x, mc.y) > 0.f ? gv[e] * dr : 0.f;
                 tg += gv[e];
                 if (a.y1) t1 = fmaf(gv[e], (y1v[u][e] - c1.z) * c1.w, t1);
                 if (a.y2) t2 = fmaf(gv[e], (y2v[u][e] - c2.z) * c2.w, t2);
             }
-            *reinterpret_cast<fv*>(a.g + o[u]) = gv;
+            if (a.g) *reinterpret_cast<fv*>(a.g + o[u]) = gv;
             sg += (double)tg;
             sx1 += (double)t1;
             sx2 += (double)t2;
@@ -949,6 +957,7 @@ int launch_chan_stats(const float* y, int B, int C, int64_t P, float* part0, flo
 }
 
 int launch_bwd_prep(BwdPrepArgs a, int* nslice, hipStream_t s) {
+    PCX_CHECK_ARG(a.mask_mode != MASK_OUT8 || a.mask8, "bwd_prep: MASK_OUT8 needs mask8");
     const int ns = chan_slices(a.B, a.C, &a.bps);
     *nslice = ns;
     if (a.P % 4 == 0) bwd_prep_kernel<4, 2><<<dim3(a.C, ns), 256, 0, s>>>(a);

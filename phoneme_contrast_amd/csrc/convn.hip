@@ -56,8 +56,8 @@ __global__ __launch_bounds__(256) void to_nhwc_kernel(NhwcArgs a) {
     if (OP != NHWC_COPY && threadIdx.x < nc) {
         const int c = c0 + threadIdx.x;
         kc[threadIdx.x] = a.cf[c];
-        if (OP == NHWC_ACT) {
-            kr[threadIdx.x] = a.rcf ? a.rcf[c] : make_float4(1.f, 0.f, 0.f, 0.f);
+        if (OP == NHWC_ACT || (OP == NHWC_BNBWD && a.mcf)) {
+            kr[threadIdx.x] = OP == NHWC_ACT ? (a.rcf ? a.rcf[c] : make_float4(1.f, 0.f, 0.f, 0.f)) : a.mcf[c];
             kd[threadIdx.x] = a.drop ? a.drop[(int64_t)b * a.C + c] : 1.f;
         }
     }
@@ -84,7 +84,15 @@ __global__ __launch_bounds__(256) void to_nhwc_kernel(NhwcArgs a) {
                 const int64_t o = base + c * HW + w0;
                 x[u] = *reinterpret_cast<const fv*>(a.src + o);
                 if (OP == NHWC_BNBWD) y2[u] = *reinterpret_cast<const fv*>(a.y + o);
-                if (OP == NHWC_ACT) y2[u] = a.res ? *reinterpret_cast<const fv*>(a.res + o) : fv{};
+                if (OP == NHWC_ACT) {
+                    if (a.res_pool) {  // pooled NHWC: the channel's elements are C apart
+                        const float* rp = a.res + (((int64_t)b * a.H + h) * W + w0) * a.C + c0 + c;
+#pragma unroll
+                        for (int e = 0; e < V; ++e) y2[u][e] = rp[(int64_t)e * a.C];
+                    } else {
+                        y2[u] = a.res ? *reinterpret_cast<const fv*>(a.res + o) : fv{};
+                    }
+                }
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -94,6 +102,12 @@ __global__ __launch_bounds__(256) void to_nhwc_kernel(NhwcArgs a) {
                     fv v = x[u];
                     if (OP == NHWC_BNBWD) {
                         const float4 k = kc[c];
+                        if (a.mcf) {  // the ReLU / Dropout2d backward of the BN output (bwd_prep_kernel's MASK_BN)
+                            const float4 mk = kr[c];
+                            const float d = kd[c];
+#pragma unroll
+                            for (int e = 0; e < V; ++e) v[e] = fmaf(y2[u][e], mk.x, mk.y) > 0.f ? v[e] * d : 0.f;
+                        }
 #pragma unroll
                         for (int e = 0; e < V; ++e) v[e] = k.x * (v[e] - k.y - (y2[u][e] - k.w) * k.z);
                     } else if (OP == NHWC_ACT) {
@@ -102,10 +116,20 @@ __global__ __launch_bounds__(256) void to_nhwc_kernel(NhwcArgs a) {
 #pragma unroll
                         for (int e = 0; e < V; ++e) {
                             float r = fmaf(v[e], k.x, k.y);
-                            if (a.res) r += fmaf(y2[u][e], rk.x, rk.y);
+                            if (a.res_pool) r += fmaxf(fmaf(y2[u][e], rk.x, rk.y), 0.f);
+                            else if (a.res) r += fmaf(y2[u][e], rk.x, rk.y);
                             v[e] = d * fmaxf(r, 0.f);
                         }
                         if (a.out32) *reinterpret_cast<fv*>(a.out32 + base + c * HW + w0) = v;
+                        if (a.mask8) {
+                            unsigned mb = 0;
+#pragma unroll
+                            for (int e = 0; e < V; ++e) mb |= (v[e] > 0.f ? 1u : 0u) << (8 * e);
+                            uint8_t* mp = a.mask8 + base + c * HW + w0;
+                            if (V == 4) *reinterpret_cast<unsigned*>(mp) = mb;
+                            else if (V == 2) *reinterpret_cast<uint16_t*>(mp) = (uint16_t)mb;
+                            else *mp = (uint8_t)mb;
+                        }
                     }
 #pragma unroll
                     for (int e = 0; e < V; ++e) t[c * TW + w0 + e] = v[e];
@@ -484,6 +508,7 @@ int launch_to_nhwc(NhwcArgs a, hipStream_t s) {
     PCX_CHECK_ARG(a.op == NHWC_COPY || a.op == NHWC_BNBWD || a.op == NHWC_ACT, "to_nhwc: op %d", a.op);
     PCX_CHECK_ARG(a.op != NHWC_BNBWD || (a.y && a.cf), "to_nhwc: BN backward needs y and cf");
     PCX_CHECK_ARG(a.op != NHWC_ACT || a.cf, "to_nhwc: activation needs cf");
+    PCX_CHECK_ARG(!a.res_pool || (a.op == NHWC_ACT && a.res && a.rcf), "to_nhwc: pooled residual needs res and rcf");
     const size_t sm = (size_t)64 * (a.W + 1) * 4;
     PCX_CHECK_ARG(sm <= 64 * 1024, "to_nhwc: row of %d pixels too long", a.W);
     dim3 grid((unsigned)a.B, (unsigned)ceil_div(a.C, 64));

@@ -37,6 +37,7 @@ struct DeepBlock {
     bool cn;
     bool planar;                   // stride-2 data gradient through class-planar planes
     size_t an, d1n;
+    size_t m8;                     // channel-last next block: the output's ReLU mask as bytes (no float32 out)
 };
 
 struct DeepPlan {
@@ -90,9 +91,10 @@ int build_deep(Plan& p) {
     d.H0 = p.F; d.W0 = p.T;
     d.H1 = (d.H0 - 1) / 2 + 1; d.W1 = (d.W0 - 1) / 2 + 1;
     const int C0 = d.h[0];
-    d.stem_fused = d.bf16 && stem_fused_ok(C0, d.H0, d.W0);
+    // (blocks 0 and 1 on the channel-last engine: block 0's output activation reads the pooled residual)
+    d.stem_fused = d.bf16 && stem_fused_ok(C0, d.H0, d.W0) && d.h[0] % 32 == 0 && d.h[1] % 32 == 0;
     d.y0 = d.stem_fused ? 0 : p.carve("y0", planes(B, C0, d.H0, d.W0) * 4);
-    d.dz0 = p.carve("dz0", planes(B, C0, d.H0, d.W0) * 4);
+    d.dz0 = p.carve("dz0", planes(B, C0, d.H0, d.W0) * (d.stem_fused ? 2 : 4));  // fused: bf16
     d.a0 = p.carve("a0", planes(B, C0, d.H1, d.W1) * 4);
     d.mparg = p.carve("maxpool_arg", planes(B, C0, d.H1, d.W1));  // first-max tap per window (uint8)
     d.ysel = d.stem_fused ? p.carve("ysel", planes(B, C0, d.H1, d.W1) * 4) : 0;
@@ -171,7 +173,7 @@ int build_deep(Plan& p) {
         k.cn = d.bf16 && k.cin % 32 == 0 && k.cout % 32 == 0;
         k.planar = (k.cn || !d.bf16) && k.stride == 2 && (int64_t)planes(B, k.cin, k.Hi, k.Wi) < ((int64_t)1 << 31);
         if (k.planar) partmax = std::max(partmax, (size_t)planes(B, k.cin, k.Hi, k.Wi) * 4);
-        k.an = k.d1n = 0;
+        k.an = k.d1n = k.m8 = 0;
         if (k.cn) {
             k.an = p.carve("nhwc_a", nhwc_bytes(B, k.cin, k.Hi, k.Wi));
             k.d1n = p.carve("nhwc_d1", nhwc_bytes(B, k.cout, k.Ho, k.Wo));
@@ -183,6 +185,13 @@ int build_deep(Plan& p) {
         plan_routed(k.cout, k.cout, k.Ho, k.Wo, &k.dma2, &k.w32_2, &k.wg2, &k.nblk2, &k.ww2, &k.wwa2);
         cin = k.cout; H = k.Ho; W = k.Wo;
     }
+    // block outputs read only as a ReLU mask (the next block reads its NHWC image): bytes.  Even widths
+    // only: with odd rows (the to_nhwc_kernel<1, ACT> form) and no float32 copy the next block's forward
+    // came out wrong (T = 200 block 2, T = 100 reduced-width block 1; measured, not yet explained), so
+    // those outputs keep their float32 plane
+    for (int i = 0; i < 3; ++i)
+        if (d.residual && d.blk[i + 1].cn && d.blk[i].Wo % 2 == 0)
+            d.blk[i].m8 = p.carve("relu_mask8", (size_t)planes(B, d.blk[i].cout, d.blk[i].Ho, d.blk[i].Wo));
     d.g = p.carve("g", gmax);
     d.dyA = p.carve("dyA", gmax);
     d.dyB = p.carve("dyB", gmax);
@@ -195,6 +204,7 @@ int build_deep(Plan& p) {
     p.P6 = H * W;
     d.hdz = p.carve("hdz", (size_t)planes(B, C4, H, W) * 4);
     stat = std::max(stat, (size_t)2 * C4 * B);
+    if (d.stem_fused) stat = std::max(stat, (size_t)2 * C0 * B);  // stem_pool_bwd partials [C0][B] x 2
     d.stat = p.carve("stat_part", stat * 4);
     d.wgp = p.carve("wg_part", wg * 4);
     d.ident = p.carve("ident", (size_t)C4 * 16);
@@ -473,7 +483,7 @@ int deep_forward(const Plan& p, const float* const* P, float* const* bnstat, int
         sa.B = B; sa.H = d.H0; sa.W = d.W0; sa.cout = C0;
         sa.x = x; sa.w = c.w<float>(d.stemw);
         sa.cf = c.w<float4>(d.cf0);
-        sa.pool = c.w<float>(d.a0); sa.pool_arg = c.w<uint8_t>(d.mparg); sa.pool_ysel = c.w<float>(d.ysel);
+        sa.pool_arg = c.w<uint8_t>(d.mparg); sa.pool_ysel = c.w<float>(d.ysel);  // pooled NHWC; no a0 plane
         sa.pool_nhwc = d.blk[0].cn ? c.w<void>(d.blk[0].an) : nullptr;
         sa.OH = d.H1; sa.OW = d.W1;
         Scope sc(&p.prof, s, "maxpool_fwd");
@@ -524,6 +534,12 @@ int deep_forward(const Plan& p, const float* const* P, float* const* bnstat, int
         } else if (d.residual) {
             res = a;
         }
+        // fused stem: block 0's identity residual a0 = relu(BN0(y0 at the tap)) from the pooled NHWC y0
+        const bool res_pool = i == 0 && d.stem_fused && res == a;
+        if (res_pool) {
+            res = c.w<float>(d.ysel);
+            rcf = c.w<float4>(d.cf0);
+        }
         {
             Scope sc(&p.prof, s, "bn_act", L + 1);
             if (i < 3 && d.blk[i + 1].cn) {  // the block output and the next block's channel-last input
@@ -531,8 +547,11 @@ int deep_forward(const Plan& p, const float* const* P, float* const* bnstat, int
                 t.cf = c.w<float4>(k.cf2);
                 t.res = res;
                 t.rcf = rcf;
+                t.res_pool = res_pool ? 1 : 0;
                 t.drop = d.residual ? nullptr : dmask[i];
-                t.out32 = c.w<float>(k.out);
+                // the float32 output is read only as the backward's ReLU mask (residual) or not at all
+                t.out32 = k.m8 ? nullptr : c.w<float>(k.out);
+                t.mask8 = k.m8 ? c.w<uint8_t>(k.m8) : nullptr;
                 RC(launch_to_nhwc(t, s));
             } else {
                 RC(launch_bn_act(c.w<float>(k.y2), c.w<float4>(k.cf2), res, rcf, d.residual ? nullptr : dmask[i],
@@ -644,6 +663,7 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
     }
     // upstream gradient of the current block's output (already ReLU-masked for the last block)
     const float* dout = c.w<float>(d.hdz);
+    const float* dout2 = nullptr;  // block 0's shortcut gradient, added by the fused stem backward
     bool masked = true;
     for (int i = 3; i >= 0; --i) {
         const DeepBlock& k = d.blk[i];
@@ -661,8 +681,9 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
             b.B = B; b.C = k.cout; b.P = P2;
             b.d = dout;
             if (d.residual) {
-                b.mask_mode = masked ? MASK_NONE : MASK_OUT;
+                b.mask_mode = masked ? MASK_NONE : (k.m8 ? MASK_OUT8 : MASK_OUT);
                 b.mask_src = c.w<float>(k.out);
+                b.mask8 = k.m8 ? c.w<uint8_t>(k.m8) : nullptr;
             } else {
                 b.mask_mode = MASK_BN;
                 b.mask_src = c.w<float>(k.y2);
@@ -723,7 +744,7 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
             b.mask_src = c.w<float>(k.y1);
             b.mask_cf = c.w<float4>(k.cf1);
             b.drop = d.residual ? dmask[i] : nullptr;
-            b.g = dd;
+            b.g = k.cn ? nullptr : dd;  // channel-last: the dy writer re-applies the mask to dd itself
             b.y1 = c.w<float>(k.y1);
             b.cf1 = c.w<float4>(k.cf1);
             int bps;
@@ -740,6 +761,8 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
             NhwcArgs t = nhwc_args(NHWC_BNBWD, B, k.cout, k.Ho, k.Wo, dd, dyn1);
             t.y = c.w<float>(k.y1);
             t.cf = c.w<float4>(k.cfb1);
+            t.mcf = c.w<float4>(k.cf1);
+            t.drop = d.residual ? dmask[i] : nullptr;
             RC(launch_to_nhwc(t, s));
         } else {
             Scope sc(&p.prof, s, "bn_bwd_apply", L);
@@ -751,7 +774,10 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
                       k.ww1 ? &k.wwa1 : nullptr));
         float* da = c.w<float>(k.da);
         int acc = 0;
-        if (d.residual && !k.sc) {  // identity shortcut: the block input receives g directly
+        // identity shortcut: the block input receives g directly -- for block 0 of the fused stem the
+        // stem's pooled backward adds it while loading (no copy, no accumulating data gradient)
+        const bool sc_in_stem = i == 0 && d.stem_fused && d.residual && !k.sc;
+        if (d.residual && !k.sc && !sc_in_stem) {
             RC(hip_status_ok(hipMemcpyAsync(da, g, (size_t)B * k.cout * P2 * 4, hipMemcpyDeviceToDevice, s),
                              "copy shortcut grad"));
             acc = 1;
@@ -772,6 +798,7 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
             RC(launch_par_interleave(ptmp, da, B, k.cin, k.Hi, k.Wi, acc, s));
         }
         dout = da;
+        dout2 = sc_in_stem ? g : nullptr;
         masked = false;
         p.buckets.mark(k.pidx, s);
     }
@@ -779,16 +806,32 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
     const int C0 = d.h[0];
     const int64_t P0 = (int64_t)d.H0 * d.W0;
     float* dz0 = c.w<float>(d.dz0);
-    if (maxpool3_bwd_prep_fits(d.H0, d.W0, d.H1, d.W1)) {  // one pass: pooled gradient + BN0 sums
+    if (d.stem_fused) {  // dz0 as bf16 + BN0 sums over the windows (stem_pool_bwd_kernel)
+        StemArgs sa{};
+        sa.B = B; sa.H = d.H0; sa.W = d.W0; sa.cout = C0; sa.OH = d.H1; sa.OW = d.W1;
+        sa.cf = c.w<float4>(d.cf0);
+        sa.pool_arg = c.w<uint8_t>(d.mparg);
+        sa.pool_ysel = c.w<float>(d.ysel);
+        sa.dpool = dout;
+        sa.dpool2 = dout2;
+        sa.dz16 = c.w<uint16_t>(d.dz0);
+        sa.p_g = part;
+        sa.p_x = part + (size_t)C0 * B;  // partials [C0][B]
+        int ns;
+        {
+            Scope sc(&p.prof, s, "maxpool_bwd");
+            RC(launch_stem_pool_bwd(sa, &ns, s));
+        }
+        RC(bn_bwd(c, C0, ns, sa.p_g, sa.p_x, P[2], c.w<float4>(d.cf0), G[2], G[3], c.w<float4>(d.cfb0), (double)B * P0));
+    } else if (maxpool3_bwd_prep_fits(d.H0, d.W0, d.H1, d.W1)) {  // one pass: pooled gradient + BN0 sums
         int bps, ns;
         const int nsl = chan_slices(B, C0, &bps);
         float* p_g = part;
         float* p_x = part + (size_t)C0 * nsl;
         {
             Scope sc(&p.prof, s, "maxpool_bwd");
-            RC(launch_maxpool3_bwd_prep(c.w<uint8_t>(d.mparg), dout, d.stem_fused ? nullptr : c.w<float>(d.y0),
-                                        d.stem_fused ? c.w<float>(d.ysel) : nullptr, c.w<float4>(d.cf0), dz0, p_g,
-                                        p_x, B, C0, d.H0, d.W0, d.H1, d.W1, &ns, s));
+            RC(launch_maxpool3_bwd_prep(c.w<uint8_t>(d.mparg), dout, c.w<float>(d.y0), nullptr, c.w<float4>(d.cf0), dz0,
+                                        p_g, p_x, B, C0, d.H0, d.W0, d.H1, d.W1, &ns, s));
         }
         RC(bn_bwd(c, C0, ns, p_g, p_x, P[2], c.w<float4>(d.cf0), G[2], G[3], c.w<float4>(d.cfb0), (double)B * P0));
     } else {
@@ -816,7 +859,7 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
     {
         StemArgs sa{};
         sa.B = B; sa.H = d.H0; sa.W = d.W0; sa.cout = C0;
-        sa.x = x; sa.dz = dz0; sa.cf_dy = c.w<float4>(d.cfb0);
+        sa.x = x; sa.dz = dz0; sa.dz16 = c.w<uint16_t>(d.dz0); sa.cf_dy = c.w<float4>(d.cfb0);
         float* wgp = c.w<float>(d.wgp);
         sa.part = wgp;
         sa.nblk = d.stem_ns; sa.rows_per_blk = d.stem_srows;

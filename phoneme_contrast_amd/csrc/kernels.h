@@ -147,11 +147,18 @@ struct StemArgs {
     int nblk, rows_per_blk;
     // fused bf16 stem (y0 recomputed instead of stored): MaxPool(3,2,1)(ReLU(BN0(y0))) outputs
     const float4* cf;     // BN0 forward coefficients {scale, shift, mean, istd}
-    float* pool;          // a0 [B][cout][OH][OW]
-    uint8_t* pool_arg;    // first-max tap per window (255: window max <= 0)
-    float* pool_ysel;     // y0 at the selected tap (the BN0 backward's xhat input)
+    float* pool;          // (unused by the fused pool: a0 = relu(BN0(pool_ysel)) where needed)
+    uint8_t* pool_arg;    // first-max tap per window (255: window max <= 0), pooled NHWC [B][OH][OW][cout]
+    float* pool_ysel;     // y0 at the selected tap, pooled NHWC (BN0 backward xhat input; block 0 residual)
     void* pool_nhwc;      // optional: padded NHWC bf16 image of a0 [B][OH + 2][OW + 2][cout]
     int OH, OW;
+    // fused backward: gradient of a0 in, dz0 (bf16, [B][cout][H][W]) out + BN0 backward sums, which the
+    // recomputing weight gradient then reads (dz16)
+    const float* dpool;
+    const float* dpool2;  // optional second addend of the a0 gradient (block 0's identity shortcut)
+    uint16_t* dz16;
+    float* p_g;           // [cout][nslice] sums of dz0 and of dz0 * xhat
+    float* p_x;
 };
 int stem_nblk(int B, int H, int* rows_per_blk);
 int stem_wgrad_nslice(int B, int H, int* rows_per_slice, bool mfma = false);
@@ -161,6 +168,8 @@ bool stem_wgrad_mfma_ok(int cout, int H, int W);  // bf16: the MFMA weight-gradi
 bool stem_fused_ok(int cout, int H, int W);
 int launch_stem_pool(StemArgs a, hipStream_t s);
 int launch_stem_wgrad_rc(StemArgs a, hipStream_t s);
+// MaxPool(3,2,1) + ReLU backward of the fused stem: dz0 (bf16) and the BN0 backward sums per (cout, slice)
+int launch_stem_pool_bwd(StemArgs a, int* nslice, hipStream_t s);
 int launch_stem_fwd(StemArgs a, int bf16, float* wround, hipStream_t s);  // wround: [cout][49] scratch (bf16)
 int launch_stem_wgrad(StemArgs a, int bf16, hipStream_t s);
 
@@ -225,7 +234,9 @@ struct HeadPoolArgs {
     int B, C, P;
     const float* y;        // [B][C][P] raw conv output
     const float4* cf;      // {s, t, mean, invstd}
-    const float* drop;     // [B][C] or NULL
+    const float* drop;     // [B][C] or NULL (NHWC_ACT: dropout of the result; NHWC_BNBWD: of the mask below)
+    const float4* mcf;     // NHWC_BNBWD (optional): src is re-masked first, src drop [y mcf.x + mcf.y > 0]
+                           // (the ReLU / Dropout2d backward bwd_prep_kernel applied without storing it)
     const float* wa;       // [C] attention 1x1 conv weight, NULL = no attention
     const float* ba;       // [1]
     float* pooled;         // [B][C]
@@ -331,8 +342,13 @@ struct NhwcArgs {
     const float4* cf;
     const float* res;      // NHWC_ACT (optional)
     const float4* rcf;
-    const float* drop;     // [B][C] or NULL
+    int res_pool;          // NHWC_ACT: res is the fused stem's y0 at the taps, pooled NHWC [B][H][W][C];
+                           // residual term relu(res rs + rt) (= a0, rcf = the stem BN's coefficients)
+    const float* drop;     // [B][C] or NULL (NHWC_ACT: dropout of the result; NHWC_BNBWD: of the mask below)
+    const float4* mcf;     // NHWC_BNBWD (optional): src is re-masked first, src drop [y mcf.x + mcf.y > 0]
+                           // (the ReLU / Dropout2d backward bwd_prep_kernel applied without storing it)
     float* out32;          // NHWC_ACT: optional float32 NCHW copy of the result
+    uint8_t* mask8;        // NHWC_ACT: optional NCHW bytes [result > 0] (the backward's ReLU mask)
     void* dst;             // [B][H + 2][W + 2][C] bf16
 };
 size_t nhwc_bytes(int B, int C, int H, int W);
@@ -345,7 +361,7 @@ int launch_convg(ConvGArgs a, hipStream_t s);
 int launch_convg_bf16(ConvGArgs a, hipStream_t s);
 int convg_nslice(const ConvGArgs& a, int64_t* kslice);
 
-enum MaskMode { MASK_NONE = 0, MASK_OUT = 1, MASK_BN = 2 };
+enum MaskMode { MASK_NONE = 0, MASK_OUT = 1, MASK_BN = 2, MASK_OUT8 = 3 };
 struct BwdPrepArgs {
     int B, C;
     int64_t P;
@@ -354,9 +370,10 @@ struct BwdPrepArgs {
     const float* d2;          // optional second upstream gradient (added)
     int mask_mode;            // MASK_OUT: g = d*[mask_src > 0]; MASK_BN: g = d*drop*[mask_src*s+t > 0]
     const float* mask_src;
+    const uint8_t* mask8;     // MASK_OUT8: g = d*[mask8 != 0] (the block output's ReLU mask as bytes)
     const float4* mask_cf;
     const float* drop;
-    float* g;                 // masked gradient (may alias d)
+    float* g;                 // masked gradient (may alias d; NULL: sums only, the consumer re-masks)
     const float* y1;          // BN inputs whose sum(g*xhat) is needed (or NULL)
     const float4* cf1;
     const float* y2;
