@@ -408,13 +408,75 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(StemArgs a) {
 // lane's (pixel, h) base.  Per tile: 32 LDS reads, 8 MFMAs, 32 coalesced 128-byte row stores; BN partials
 // as stem_fwd_kernel's (per-block shift = the outputs of the block's first pixel, sum and M2).
 typedef __bf16 st_bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned st_u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned st_u32x2 __attribute__((ext_vector_type(2)));
+
+// bf16 image of one stem sample for the MFMA forms: rows of st_rw2 elements, the input at (row 3,
+// column 4), zeros around, held twice -- copy k shifted right by k elements -- so that any run of
+// consecutive elements starting at column c is read as dwords from copy (c & 1) (2-element aligned);
+// the copy stride makes copy 1's dwords start half-way round the banks.
+__host__ __device__ constexpr int st_rw2(int W) { return st_rw(W) + 2; }
+__host__ __device__ constexpr int st_cp2(int rows, int W) {
+    return ((rows * st_rw2(W) / 2 + 31) / 32 * 32 + 16) * 2;  // elements; (st_cp2 / 2) % 32 == 16
+}
+__device__ __forceinline__ void st2_zero(__bf16* xs, int rows, int W) {
+    const int n = st_cp2(rows, W);  // both copies: 2 n elements = n dwords
+    for (int i = threadIdx.x; i < n; i += blockDim.x) reinterpret_cast<unsigned*>(xs)[i] = 0u;
+}
+// the interior (rows 3 .. H + 2, columns 4 .. W + 3) of both copies; loads batched ahead of the writes
+__device__ __forceinline__ void st2_stage(const float* __restrict__ xb, int H, int W, __bf16* xs, int rows) {
+    const int RW2 = st_rw2(W), CP = st_cp2(rows, W), n = H * W;
+    constexpr int U = 8;
+    const int dq = (int)blockDim.x / W, dr = (int)blockDim.x - dq * W;
+    int r0 = (int)threadIdx.x / W, c0 = (int)threadIdx.x - r0 * W;
+    for (int base = 0; base < n; base += U * (int)blockDim.x) {
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = base + u * (int)blockDim.x + (int)threadIdx.x;
+            v[u] = xb[i < n ? i : 0];
+        }
+        int r = r0, c = c0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = base + u * (int)blockDim.x + (int)threadIdx.x;
+            if (i < n) {
+                const __bf16 bv = (__bf16)v[u];
+                const int o = (r + 3) * RW2 + c + 4;
+                xs[o] = bv;
+                xs[CP + o + 1] = bv;
+            }
+            r += dq;
+            c += dr;
+            if (c >= W) { c -= W; ++r; }
+        }
+        r0 = r;
+        c0 = c;
+    }
+}
+// 8 consecutive elements of row r from column c (both copies: 4 dword reads)
+__device__ __forceinline__ st_bf16x8 st2_ld8(const __bf16* xs, int CP, int o) {
+    const int k = o & 1;  // (RW2 even: the column's parity)
+    const unsigned* p = reinterpret_cast<const unsigned*>(xs + k * CP + o + k);
+    st_u32x4 v;
+    v.x = p[0]; v.y = p[1]; v.z = p[2]; v.w = p[3];
+    return __builtin_bit_cast(st_bf16x8, v);
+}
+__device__ __forceinline__ st_u32x2 st2_ld4(const __bf16* xs, int CP, int o) {
+    const int k = o & 1;
+    const unsigned* p = reinterpret_cast<const unsigned*>(xs + k * CP + o + k);
+    st_u32x2 v;
+    v.x = p[0]; v.y = p[1];
+    return v;
+}
 
 __global__ __launch_bounds__(256) void stem_fwd_mfma_kernel(StemArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float xs[];  // (H + 7) rows: one spare zero row for dh = 7
+    extern __shared__ __attribute__((aligned(16))) float xs_f[];  // two bf16 copies of (H + 7) rows (spare zero row)
+    __bf16* xs = reinterpret_cast<__bf16*>(xs_f);
     __shared__ float red[2][64][2];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
     const int mt = wave >> 1, wt = wave & 1;  // waves 2 mt, 2 mt + 1: couts 32 mt .. 32 mt + 31, alternate tiles
-    const int H = a.H, W = a.W, HW = H * W, RW = st_rw(W);
+    const int H = a.H, W = a.W, HW = H * W, RW2 = st_rw2(W), CP = st_cp2(H + 7, W);
     st_bf16x8 A[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s)
@@ -423,21 +485,16 @@ __global__ __launch_bounds__(256) void stem_fwd_mfma_kernel(StemArgs a) {
             const int dh = 2 * s + h, dw = j;
             A[s][j] = (__bf16)((dh < ST_K && dw < ST_K) ? a.w[(32 * mt + l32) * ST_T + dh * ST_K + dw] : 0.f);
         }
-    for (int i = threadIdx.x; i < (H + 7) * RW; i += 256) xs[i] = 0.f;
+    st2_zero(xs, H + 7, W);
     const int ntile = (HW + 31) >> 5;
     auto tile = [&](int tt, int& p) {
         p = tt * 32 + l32;
         const int pc = min(p, HW - 1);
         const int hh = pc / W, ww = pc - hh * W;
-        const float* xb = xs + (hh + h) * RW + ww + 1;
+        const int o = (hh + h) * RW2 + ww + 1;
         f32x16 acc = {0.f};
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            st_bf16x8 Bv;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) Bv[j] = (__bf16)xb[2 * s * RW + j];
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[s], Bv, acc, 0, 0, 0);
-        }
+        for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[s], st2_ld8(xs, CP, o + 2 * s * RW2), acc, 0, 0, 0);
         return acc;
     };
     float K[16], s1[16], s2[16];
@@ -446,7 +503,7 @@ __global__ __launch_bounds__(256) void stem_fwd_mfma_kernel(StemArgs a) {
     int nsamp = 0;
     for (int b = blockIdx.x; b < a.B; b += gridDim.x, ++nsamp) {
         __syncthreads();
-        st_stage<true>(a.x + (int64_t)b * HW, H, W, xs);
+        st2_stage(a.x + (int64_t)b * HW, H, W, xs, H + 7);
         __syncthreads();
         if (b == (int)blockIdx.x) {  // shift: every wave evaluates the block's first pixel itself
             int p;
@@ -868,11 +925,12 @@ __global__ __launch_bounds__(SPB_T) void stem_pool_bwd_kernel(StemArgs a) {
 // the tap offsets, fp32 LDS as stem_wgrad_mfma_kernel stages it) is read at those same pixels.  No
 // transposition, no dy tile in LDS.
 __global__ __launch_bounds__(256) void stem_wgrad_rc_kernel(StemArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float xs[];  // (H + 8) rows of the sample
+    extern __shared__ __attribute__((aligned(16))) float xs_f[];  // two bf16 copies of (H + 8) rows of the sample
+    __bf16* xs = reinterpret_cast<__bf16*>(xs_f);
     __shared__ float red[2][32][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
     const int mt = wave >> 1, wt = wave & 1;
-    const int H = a.H, W = a.W, HW = H * W, RW = st_rw(W), WV = (W + 7) & ~7, HWV = H * WV;
+    const int H = a.H, W = a.W, HW = H * W, RW2 = st_rw2(W), CP = st_cp2(H + 8, W), WV = (W + 7) & ~7, HWV = H * WV;
     const int slice = blockIdx.x;
     const int b0 = slice * a.rows_per_blk, b1 = min(a.B, b0 + a.rows_per_blk);
     const int co = 32 * mt + l32;
@@ -895,14 +953,14 @@ __global__ __launch_bounds__(256) void stem_wgrad_rc_kernel(StemArgs a) {
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
         const int t = 32 * nt + l32, dh = t >> 3, dw = t & 7;
-        boff[nt] = dh * RW + dw;
+        boff[nt] = dh * RW2 + dw;
     }
     f32x16 acc[2] = {f32x16{0.f}, f32x16{0.f}};
-    for (int i = threadIdx.x; i < (H + 8) * RW; i += 256) xs[i] = 0.f;
+    st2_zero(xs, H + 8, W);
     const int ntile = (HWV + 31) >> 5;
     for (int b = b0; b < b1; ++b) {
         __syncthreads();
-        st_stage<true>(a.x + (int64_t)b * HW, H, W, xs);
+        st2_stage(a.x + (int64_t)b * HW, H, W, xs, H + 8);
         __syncthreads();
         // dz0 (bf16) of the sample: one wave-uniform resource, the lane's cout plane in the offset
         const auto rs_g = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.dz16 + (int64_t)b * a.cout * HW), (short)0,
@@ -915,15 +973,11 @@ __global__ __launch_bounds__(256) void stem_wgrad_rc_kernel(StemArgs a) {
             {
                 const int p = min(p0 + l32, HWV - 1);
                 const int hh = p / WV, ww = p - hh * WV;
-                const float* xb = xs + (hh + h) * RW + ww + 1;
+                const int o = (hh + h) * RW2 + ww + 1;
                 y = f32x16{0.f};
 #pragma unroll
-                for (int s = 0; s < 4; ++s) {
-                    st_bf16x8 Xv;
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) Xv[j] = (__bf16)xb[2 * s * RW + j];
-                    y = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Xv, Wt[s], y, 0, 0, 0);
-                }
+                for (int s = 0; s < 4; ++s)
+                    y = __builtin_amdgcn_mfma_f32_32x32x16_bf16(st2_ld8(xs, CP, o + 2 * s * RW2), Wt[s], y, 0, 0, 0);
             }
             // the lane's four pixel runs q: p0 + 8 q + 4 h .. + 3 (one padded row each)
             int xoff[4];
@@ -933,7 +987,7 @@ __global__ __launch_bounds__(256) void stem_wgrad_rc_kernel(StemArgs a) {
                 const int pq = p0 + 8 * q + 4 * h;
                 const int hh = pq / WV, ww = pq - hh * WV;
                 const int nv = hh < H ? min(4, W - ww) : 0;  // real pixels of the run (<= 0: padding)
-                xoff[q] = min(hh, H - 1) * RW + ww + 1;
+                xoff[q] = min(hh, H - 1) * RW2 + ww + 1;
                 float g[4];
                 if ((W & 3) == 0) {
                     const uint2 t = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs_g, nv == 4 ? (co * HW + hh * W + ww) * 2 : 0x7fff0000, 0, 0));
@@ -951,10 +1005,11 @@ __global__ __launch_bounds__(256) void stem_wgrad_rc_kernel(StemArgs a) {
             for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
                 for (int nt = 0; nt < 2; ++nt) {
-                    st_bf16x8 Bv;
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) Bv[e] = (__bf16)xs[xoff[2 * ks + (e >> 2)] + boff[nt] + (e & 3)];
-                    acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dy[ks], Bv, acc[nt], 0, 0, 0);
+                    st_u32x4 bv;
+                    const st_u32x2 lo = st2_ld4(xs, CP, xoff[2 * ks] + boff[nt]);
+                    const st_u32x2 hi = st2_ld4(xs, CP, xoff[2 * ks + 1] + boff[nt]);
+                    bv.x = lo.x; bv.y = lo.y; bv.z = hi.x; bv.w = hi.y;
+                    acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dy[ks], __builtin_bit_cast(st_bf16x8, bv), acc[nt], 0, 0, 0);
                 }
         }
     }
@@ -1281,8 +1336,8 @@ int launch_stem_fwd(StemArgs a, int bf16, float* wround, hipStream_t s) {
         a.w = wround;
     }
     const size_t sm = stem_smem(a.H, a.W);
-    if (bf16 && a.cout == 64 && (size_t)(a.H + 7) * st_rw(a.W) * 4 <= 160 * 1024) {  // bf16 MFMA form
-        const size_t smm = (size_t)(a.H + 7) * st_rw(a.W) * 4;
+    if (bf16 && a.cout == 64 && (size_t)st_cp2(a.H + 7, a.W) * 4 <= 160 * 1024) {  // bf16 MFMA form
+        const size_t smm = (size_t)st_cp2(a.H + 7, a.W) * 4;
         (void)hipFuncSetAttribute((const void*)stem_fwd_mfma_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)smm);
         stem_fwd_mfma_kernel<<<a.nblk, 256, smm, s>>>(a);
@@ -1314,7 +1369,7 @@ static size_t stem_pool_smem(int H, int W) {
 
 bool stem_fused_ok(int cout, int H, int W) {
     return cout == 64 && W <= 256 && stem_pool_smem(H, W) <= 80 * 1024 &&
-           (size_t)(H + 8) * st_rw(W) * 4 + 16 * 1024 <= 160 * 1024 &&
+           (size_t)st_cp2(H + 8, W) * 4 + 16 * 1024 <= 160 * 1024 &&
            maxpool3_bwd_prep_fits(H, W, (H - 1) / 2 + 1, (W - 1) / 2 + 1);
 }
 
@@ -1350,7 +1405,7 @@ int launch_stem_wgrad_rc(StemArgs a, hipStream_t s) {
     PCX_CHECK_ARG(stem_fused_ok(a.cout, a.H, a.W), "stem_wgrad_rc: cout %d at %dx%d unsupported", a.cout, a.H, a.W);
     PCX_CHECK_ARG(a.dz16 && a.cf_dy && a.part && a.nblk >= 1 && (int64_t)a.nblk * a.rows_per_blk >= a.B,
                   "stem_wgrad_rc: bad arguments");
-    const size_t sm = (size_t)(a.H + 8) * st_rw(a.W) * 4;
+    const size_t sm = (size_t)st_cp2(a.H + 8, a.W) * 4;
     (void)hipFuncSetAttribute((const void*)stem_wgrad_rc_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
     stem_wgrad_rc_kernel<<<(unsigned)a.nblk, 256, sm, s>>>(a);
     PCX_LAUNCH_CHECK("stem_wgrad_rc_kernel");
