@@ -132,9 +132,11 @@ def deep_kernel_costs(B, F, T, bf16=False, D=128):
         stem = 2 * B * H0 * W0 * C0 * 49
         xb = 4 * B * H0 * W0
         out["conv_fwd_L0"] = (stem, xb)                                        # BN0 statistics only
-        out["maxpool_fwd"] = (stem, xb + B * C0 * (9 * H1 * W1 + img * (H1 + 2) * (W1 + 2)))  # a0, tap, ysel, NHWC
-        out["maxpool_bwd"] = (0, B * C0 * (9 * H1 * W1 + 4 * H0 * W0))        # tap, d a0, ysel -> dz0
-        out["wgrad_L0"] = (2 * stem, xb + 4 * B * C0 * H0 * W0)                # dz0 + x (recompute + gradient)
+        # pooled NHWC y0 at the tap (4 B) + tap (1 B) + block 0's NHWC image; no a0 plane
+        out["maxpool_fwd"] = (stem, xb + B * C0 * (5 * H1 * W1 + img * (H1 + 2) * (W1 + 2)))
+        # d a0 + block 0's shortcut gradient + tap + y0 at the tap -> dz0 in bf16
+        out["maxpool_bwd"] = (0, B * C0 * (13 * H1 * W1 + 2 * H0 * W0))
+        out["wgrad_L0"] = (2 * stem, xb + 2 * B * C0 * H0 * W0)                # bf16 dz0 + x (recompute + gradient)
     out["bwd_prep_L0"] = (0, B * C0 * 4 * H0 * W0 * 3)
     H, W, cin = H1, W1, C0
     for i, co in enumerate(DEEP_DIMS):
@@ -145,12 +147,14 @@ def deep_kernel_costs(B, F, T, bf16=False, D=128):
         a_in, y = 4 * B * cin * Pi, 4 * B * co * Po
         out[f"to_nhwc_L{L}"] = (0, a_in + img * B * cin * (H + 2) * (W + 2))
         out[f"bn_act_L{L}"] = (0, y + img * B * co * Po)                         # y1 -> d1
-        out[f"bn_act_L{L + 1}"] = (0, 2 * y + y + img * B * co * Po)             # y2 + residual -> out (+ image)
+        # bf16: outputs of even-width blocks 0-1 leave a byte ReLU mask instead of the float32 plane
+        m8 = bf16 and i < 2 and Wo % 2 == 0
+        out[f"bn_act_L{L + 1}"] = (0, 2 * y + (y // 4 if m8 else y) + img * B * co * Po)  # y2 + residual -> out / mask (+ image)
         out[f"chan_stats_L{L}"] = (0, y)
         out[f"chan_stats_L{L + 1}"] = (0, y)
         out[f"chan_stats_L{100 + i}"] = (0, y)
-        out[f"bwd_prep_L{L + 1}"] = (0, y * (4 if sc else 3) + y)                # d, mask, y2 (, ysc) -> g
-        out[f"bwd_prep_L{L}"] = (0, 3 * y)                                       # d, y1 -> d
+        out[f"bwd_prep_L{L + 1}"] = (0, y * (4 if sc else 3) + y - (3 * y // 4 if m8 else 0))  # d, mask, y2 (, ysc) -> g
+        out[f"bwd_prep_L{L}"] = (0, (2 if bf16 else 3) * y)                      # d, y1 (-> d; bf16: sums only)
         out[f"dy_nhwc_L{L + 1}"] = (0, 2 * y + img * B * co * Po)
         out[f"dy_nhwc_L{L}"] = (0, 2 * y + img * B * co * Po)
         out[f"bn_bwd_apply_L{L + 1}"] = (0, 3 * y)
