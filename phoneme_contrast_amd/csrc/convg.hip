@@ -57,7 +57,11 @@ __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
     else if (MODE == 3) { M = a.cin; N = a.B * CHW; K = (int64_t)a.cout * KKp; }
     else { M = a.cout; N = (int64_t)a.cin * KK; K = a.B * OHW; }
     const int64_t mt = (M + BM - 1) / BM, nt = (N + BN - 1) / BN;
-    int64_t bid = blockIdx.x;
+    // XCD-aware order (grid padded to a multiple of 8): XCD x runs logical blocks [x per, (x + 1) per),
+    // so the M tiles of a pixel tile / the N tiles of a K slice, which read the same rows, share an L2
+    const int64_t nlog = mt * nt * (MODE == 2 ? a.nslice : 1), per = (nlog + 7) / 8;
+    int64_t bid = (int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    if (bid >= nlog) return;
     const int64_t tm = bid % mt;
     bid /= mt;
     const int64_t tn = bid % nt;
@@ -890,7 +894,7 @@ int launch_convg(ConvGArgs a, hipStream_t s) {
     const int64_t nblocks = mt * nt * (a.mode == 2 ? a.nslice : 1);
     PCX_CHECK_ARG(nblocks < ((int64_t)1 << 31), "convg: grid too large");
     if (a.mode == 2) PCX_CHECK_ARG(a.kslice % KC == 0 && a.nslice >= 1, "convg: bad weight-gradient split");
-    dim3 grid((unsigned)nblocks);
+    dim3 grid((unsigned)(8 * ((nblocks + 7) / 8)));  // (XCD-aware order inside the kernel)
     // tap-uniform K chunks: the K channel count (cin forward, cout data gradient) a multiple of 16
     // (mode 2 reuses the flag: false = dy computed as the BN backward of (bn_g, bn_y) while staging)
     const bool fk = a.mode == 2 ? a.bn_g == nullptr : (a.mode == 0 ? a.cin : a.cout) % KC == 0;

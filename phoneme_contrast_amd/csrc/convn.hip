@@ -172,6 +172,16 @@ __device__ __forceinline__ int swz(int r, int q) {
     return KC == 32 ? r * 64 + 16 * (q ^ ((r >> 2) & 3)) : r * 128 + 16 * (q ^ ((r >> 1) & 7));
 }
 
+// Workgroups are dealt to the 8 XCDs round-robin and each XCD has its own L2.  Launch 8 * per
+// workgroups and give XCD x the logical blocks [x per, (x + 1) per): the blocks that share operand rows
+// (the M tiles of a pixel tile; the N tiles of a weight-gradient K slice) are consecutive in logical
+// order, so they run on one XCD at about the same time and read those rows from its L2 instead of HBM.
+__host__ __device__ inline int64_t xcd_per(int64_t nblocks) { return (nblocks + 7) / 8; }
+__device__ __forceinline__ int64_t xcd_logical(int64_t nblocks) {
+    const int64_t bid = blockIdx.x;
+    return (bid & 7) * xcd_per(nblocks) + (bid >> 3);
+}
+
 template <int MODE, int WM, int KC>
 __global__ __launch_bounds__(256) void convn_kernel(ConvGArgs a) {
     constexpr int WN = 2;
@@ -202,7 +212,9 @@ __global__ __launch_bounds__(256) void convn_kernel(ConvGArgs a) {
     const int T = nth * ntw, nch = T * (CK / KC);
     const int64_t K = (int64_t)T * CK;  // packed row length (a multiple of 32)
     const int64_t mt = (M + BM - 1) / BM;
-    const int64_t tm = blockIdx.x % mt, tn = blockIdx.x / mt;
+    const int64_t lid = xcd_logical(mt * ((N + BN - 1) / BN));
+    if (lid >= mt * ((N + BN - 1) / BN)) return;  // (grid padded to a multiple of 8)
+    const int64_t tm = lid % mt, tn = lid / mt;
     const int64_t m0 = tm * BM, n0 = tn * BN;
 
     // DMA roles: wave instruction j covers tile rows RPI (wave + 4 j) ..; lane -> row lr, slot ls
@@ -341,7 +353,8 @@ __global__ __launch_bounds__(256) void convn_wgrad_kernel(ConvGArgs a) {
     const int64_t M = a.cout, N = (int64_t)a.cin * KK, K = a.B * OHW;
     const int Hp = a.IH + 2, Wp = a.IW + 2, Hq = a.OH + 2, Wq = a.OW + 2;
     const int64_t mt = (M + BM - 1) / BM, nt = (N + BN - 1) / BN;
-    int64_t bid = blockIdx.x;
+    int64_t bid = xcd_logical(mt * nt * a.nslice);
+    if (bid >= mt * nt * a.nslice) return;  // (grid padded to a multiple of 8)
     const int64_t tm = bid % mt;
     bid /= mt;
     const int64_t tn = bid % nt;
@@ -543,8 +556,9 @@ int launch_convn(const ConvGArgs& a, hipStream_t s) {
         const int wm = M >= 128 ? 2 : 1;
         const int64_t nblocks = ceil_div(M, 64 * wm) * ceil_div(N, 128) * a.nslice;
         PCX_CHECK_ARG(nblocks < ((int64_t)1 << 31), "convn: grid too large");
-        if (wm == 2) convn_wgrad_kernel<2><<<(unsigned)nblocks, 256, 0, s>>>(a);
-        else convn_wgrad_kernel<1><<<(unsigned)nblocks, 256, 0, s>>>(a);
+        const unsigned grid = (unsigned)(8 * xcd_per(nblocks));
+        if (wm == 2) convn_wgrad_kernel<2><<<grid, 256, 0, s>>>(a);
+        else convn_wgrad_kernel<1><<<grid, 256, 0, s>>>(a);
         PCX_LAUNCH_CHECK("convn_wgrad_kernel");
         return PCX_OK;
     }
@@ -583,7 +597,7 @@ int launch_convn(const ConvGArgs& a, hipStream_t s) {
     constexpr int wn = 2;  // (128 x 256 tiles measured slower: 2 blocks per CU instead of 4)
     const int64_t nblocks = ceil_div(M, 64 * wm) * ceil_div(N, 64 * wn);
     PCX_CHECK_ARG(nblocks < ((int64_t)1 << 31), "convn: grid too large");
-    dim3 grid((unsigned)nblocks);
+    dim3 grid((unsigned)(8 * xcd_per(nblocks)));
 #define PCX_CN(MODE_, WM_, KC_)                                                                \
     if (a.mode == MODE_ && wm == WM_ && kc == KC_) {                                           \
         convn_kernel<MODE_, WM_, KC_><<<grid, 256, 0, s>>>(a);                                 \
