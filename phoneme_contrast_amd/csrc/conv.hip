@@ -966,8 +966,25 @@ __global__ __launch_bounds__(256) void stem_wgrad_rc_kernel(StemArgs a) {
         const auto rs_g = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.dz16 + (int64_t)b * a.cout * HW), (short)0,
                                                             a.cout * HW * 2, 0x00020000);
         const uint16_t* gp = a.dz16 + ((int64_t)b * a.cout + co) * HW;
+        // the lane's four dz0 runs of tile tt (W % 4 == 0: 8-byte loads), issued one tile ahead
+        auto load_g = [&](int tt, uint2 (&gv)[4]) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int pq = tt * 32 + 8 * q + 4 * h;
+                const int hh = pq / WV, ww = pq - hh * WV;
+                const bool full = tt < ntile && hh < H && ww + 4 <= W;
+                gv[q] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(
+                                                      rs_g, full ? (co * HW + hh * W + ww) * 2 : 0x7fff0000, 0, 0));
+            }
+        };
+        uint2 gnx[4];
+        if ((W & 3) == 0) load_g(wt, gnx);
         for (int tt = wt; tt < ntile; tt += 2) {
             const int p0 = tt * 32;
+            uint2 gcur[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) gcur[q] = gnx[q];
+            if ((W & 3) == 0) load_g(tt + 2, gnx);  // in flight under this tile's MFMAs
             // y0 of pixel p0 + l32 (A operand: im2col row, taps 8 h .. 8 h + 7 of each K-step)
             f32x16 y;
             {
@@ -990,7 +1007,7 @@ __global__ __launch_bounds__(256) void stem_wgrad_rc_kernel(StemArgs a) {
                 xoff[q] = min(hh, H - 1) * RW2 + ww + 1;
                 float g[4];
                 if ((W & 3) == 0) {
-                    const uint2 t = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs_g, nv == 4 ? (co * HW + hh * W + ww) * 2 : 0x7fff0000, 0, 0));
+                    const uint2 t = gcur[q];
                     g[0] = __uint_as_float(t.x << 16); g[1] = __uint_as_float(t.x & 0xffff0000u);
                     g[2] = __uint_as_float(t.y << 16); g[3] = __uint_as_float(t.y & 0xffff0000u);
                 } else {
