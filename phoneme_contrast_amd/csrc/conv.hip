@@ -790,9 +790,17 @@ __global__ __launch_bounds__(SPB_T) void stem_pool_bwd_kernel(StemArgs a) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int b = blockIdx.x >> 1, hf = blockIdx.x & 1, C = a.cout;
     const int H = a.H, W = a.W, OH = a.OH, OW = a.OW, OHW = OH * OW, n = 32 * OW;
-    float* gl = sm;                                              // [2][32][OW] gated gradient
-    uint8_t* al = reinterpret_cast<uint8_t*>(sm + 2 * n);        // [2][32][OW] taps
-    float* ysl = reinterpret_cast<float*>(al + ((2 * n + 15) & ~15));  // [32][OW] y0 at the tap (sums)
+    // LDS rows of OWP = OW + 2 columns: the two sentinel columns (tap 255, gradient 0) stand for the
+    // windows past the right edge, so the band loop reads its six windows unconditionally
+    const int OWP = OW + 2, np_ = 32 * OWP;
+    float* gl = sm;                                                // [2][32][OWP] gated gradient
+    uint8_t* al = reinterpret_cast<uint8_t*>(sm + 2 * np_);        // [2][32][OWP] taps
+    float* ysl = reinterpret_cast<float*>(al + ((2 * np_ + 15) & ~15));  // [32][OWP] y0 at the tap (sums)
+    for (int t = threadIdx.x; t < 2 * 32 * 2; t += SPB_T) {        // sentinels of both slots
+        const int sl = t >> 6, cc = (t >> 1) & 31, e = t & 1;
+        gl[sl * np_ + cc * OWP + OW + e] = 0.f;
+        al[sl * np_ + cc * OWP + OW + e] = 255;
+    }
     __shared__ float kz[32], kw4[32];
     if (threadIdx.x < 32) {
         const float4 k = a.cf[32 * hf + threadIdx.x];
@@ -819,30 +827,39 @@ __global__ __launch_bounds__(SPB_T) void stem_pool_bwd_kernel(StemArgs a) {
     double sg = 0.0, sx = 0.0;
     const int sc_c = threadIdx.x >> 3, sc_j = threadIdx.x & 7;
     auto store_row = [&](int slot) {
-        float* g = gl + slot * n;
-        uint8_t* ap = al + slot * n;
+        float* g = gl + slot * np_;
+        uint8_t* ap = al + slot * np_;
 #pragma unroll
         for (int u = 0; u < SPB_NI; ++u) {
             const int t = u * SPB_T + (int)threadIdx.x;
             if (t < n) {
                 const int jj = t >> 5, cc = t & 31;
-                ap[cc * OW + jj] = (uint8_t)av[u];
-                ysl[cc * OW + jj] = yv[u];
+                ap[cc * OWP + jj] = (uint8_t)av[u];
+                ysl[cc * OWP + jj] = yv[u];
             }
         }
         __syncthreads();
+        {
+            int c = c_0, j = j_0;
 #pragma unroll
-        for (int u = 0; u < SPB_NI; ++u) {
-            const int t = u * SPB_T + (int)threadIdx.x;
-            if (t < n) g[t] = ap[t] != 255 ? dv[u] : 0.f;
+            for (int u = 0; u < SPB_NI; ++u) {
+                const int t = u * SPB_T + (int)threadIdx.x;
+                if (t < n) g[c * OWP + j] = ap[c * OWP + j] != 255 ? dv[u] : 0.f;
+                c += cq;
+                j += cr;
+                if (j >= OW) { j -= OW; ++c; }
+            }
         }
         __syncthreads();
         const float kzc = kz[sc_c], kwc = kw4[sc_c];
+        float tg = 0.f, tx = 0.f;  // (a row's dozen terms in float32, the running sums in float64)
         for (int j = sc_j; j < OW; j += 8) {
-            const float gv = g[sc_c * OW + j];
-            sg += (double)gv;
-            sx += (double)gv * (double)((ysl[sc_c * OW + j] - kzc) * kwc);
+            const float gv = g[sc_c * OWP + j];
+            tg += gv;
+            tx = fmaf(gv, (ysl[sc_c * OWP + j] - kzc) * kwc, tx);
         }
+        sg += (double)tg;
+        sx += (double)tx;
     };
     __syncthreads();
     PCX_SPB_LOAD(0);
@@ -850,56 +867,69 @@ __global__ __launch_bounds__(SPB_T) void stem_pool_bwd_kernel(StemArgs a) {
     PCX_SPB_LOAD(1);
     __syncthreads();
     store_row(1);
-    const int MW = (W + 1) >> 1;  // 2-column groups per row
+    // band item: channel c, 4-column group q -> pixels (2 i + dr, 4 q + dc), dr < 2, dc < 4; the
+    // windows (i + wi, 2 q + wj), wi < 2, wj < 3, reach pixel (2 wi - 1 + kh, 2 wj - 1 + kw) through tap
+    // kh 3 + kw; contributions are added in window (row-major) order
+    const int MQ = (W + 3) >> 2;
+    const int mq = SPB_T / MQ, mr = SPB_T - mq * MQ;
+    uint16_t* const zb = a.dz16 + ((int64_t)b * C + 32 * hf) * H * W;  // the half's 32 planes (32-bit offsets)
     for (int i = 0; i < OH; ++i) {
         PCX_SPB_LOAD(i + 2);  // in flight under the band
         __syncthreads();  // rows i, i + 1 staged
-        const float* g0 = gl + (i & 1) * n;
-        const float* g1 = gl + ((i + 1) & 1) * n;
-        const uint8_t* a0 = al + (i & 1) * n;
-        const uint8_t* a1 = al + ((i + 1) & 1) * n;
-        const bool r1ok = 2 * i + 1 < H, w1ok = i + 1 < OH;
-        int c = (int)threadIdx.x / MW, m = (int)threadIdx.x - c * MW;
-        const int mq = SPB_T / MW, mr = SPB_T - mq * MW;
-        for (int t = threadIdx.x; t < 32 * MW; t += SPB_T, c += mq, m += mr) {
-            if (m >= MW) { m -= MW; ++c; }
-            const int o00 = c * OW + m;
-            const bool m1 = m + 1 < OW;
-            // taps of the four windows (255: none)
-            const int t00 = a0[o00], t01 = m1 ? a0[o00 + 1] : 255;
-            const int t10 = w1ok ? a1[o00] : 255, t11 = (w1ok && m1) ? a1[o00 + 1] : 255;
-            const float d00 = g0[o00], d01 = m1 ? g0[o00 + 1] : 0.f;
-            const float d10 = w1ok ? g1[o00] : 0.f, d11 = (w1ok && m1) ? g1[o00 + 1] : 0.f;
-            // pixel (2 i + dr, 2 m + dc) <- window (i + wi, m + wj) through tap (1 + dr - 2 wi) * 3 + (1 + dc - 2 wj)
-            float p00 = 0.f, p01 = 0.f, p10 = 0.f, p11 = 0.f;
-            if (t00 == 4) p00 += d00;
-            if (t00 == 5) p01 += d00;
-            if (t01 == 3) p01 += d01;
-            if (t00 == 7) p10 += d00;
-            if (t10 == 1) p10 += d10;
-            if (t00 == 8) p11 += d00;
-            if (t01 == 6) p11 += d01;
-            if (t10 == 2) p11 += d10;
-            if (t11 == 0) p11 += d11;
-            uint16_t* zr = a.dz16 + (((int64_t)b * C + 32 * hf + c) * H + 2 * i) * W + 2 * m;
-            const bool c1 = 2 * m + 1 < W;
-            if (c1 && (W & 1) == 0) {
-                *reinterpret_cast<uint32_t*>(zr) = (unsigned)__builtin_bit_cast(uint16_t, (__bf16)p00) |
-                                                   ((unsigned)__builtin_bit_cast(uint16_t, (__bf16)p01) << 16);
-                if (r1ok)
-                    *reinterpret_cast<uint32_t*>(zr + W) = (unsigned)__builtin_bit_cast(uint16_t, (__bf16)p10) |
-                                                           ((unsigned)__builtin_bit_cast(uint16_t, (__bf16)p11) << 16);
-            } else {
-                zr[0] = __builtin_bit_cast(uint16_t, (__bf16)p00);
-                if (c1) zr[1] = __builtin_bit_cast(uint16_t, (__bf16)p01);
-                if (r1ok) {
-                    zr[W] = __builtin_bit_cast(uint16_t, (__bf16)p10);
-                    if (c1) zr[W + 1] = __builtin_bit_cast(uint16_t, (__bf16)p11);
+        const float* g0 = gl + (i & 1) * np_;
+        const float* g1 = gl + ((i + 1) & 1) * np_;
+        const uint8_t* a0 = al + (i & 1) * np_;
+        const uint8_t* a1 = al + ((i + 1) & 1) * np_;
+        const bool r1ok = 2 * i + 1 < H;
+        int c = (int)threadIdx.x / MQ, q = (int)threadIdx.x - c * MQ;
+        for (int t = threadIdx.x; t < 32 * MQ; t += SPB_T, c += mq, q += mr) {
+            if (q >= MQ) { q -= MQ; ++c; }
+            const int o = c * OWP + 2 * q;
+            int tp[2][3];
+            float dd[2][3];
+#pragma unroll
+            for (int wj = 0; wj < 3; ++wj) {
+                tp[0][wj] = a0[o + wj];
+                tp[1][wj] = a1[o + wj];
+                dd[0][wj] = g0[o + wj];
+                dd[1][wj] = g1[o + wj];
+            }
+            float px[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+            for (int wi = 0; wi < 2; ++wi)
+#pragma unroll
+                for (int wj = 0; wj < 3; ++wj)
+#pragma unroll
+                    for (int dr = 0; dr < 2; ++dr)
+#pragma unroll
+                        for (int dc = 0; dc < 4; ++dc) {
+                            const int kh = dr + 1 - 2 * wi, kw = dc + 1 - 2 * wj;
+                            if (kh < 0 || kh > 2 || kw < 0 || kw > 2) continue;
+                            if (tp[wi][wj] == kh * 3 + kw) px[dr][dc] += dd[wi][wj];
+                        }
+            const int col = 4 * q;
+            uint16_t* zr = zb + (c * H + 2 * i) * W + col;
+            if ((W & 3) == 0) {
+#pragma unroll
+                for (int dr = 0; dr < 2; ++dr) {
+                    if (dr == 1 && !r1ok) break;
+                    uint2 v;
+                    v.x = (unsigned)__builtin_bit_cast(uint16_t, (__bf16)px[dr][0]) |
+                          ((unsigned)__builtin_bit_cast(uint16_t, (__bf16)px[dr][1]) << 16);
+                    v.y = (unsigned)__builtin_bit_cast(uint16_t, (__bf16)px[dr][2]) |
+                          ((unsigned)__builtin_bit_cast(uint16_t, (__bf16)px[dr][3]) << 16);
+                    *reinterpret_cast<uint2*>(zr + dr * W) = v;
                 }
+            } else {
+#pragma unroll
+                for (int dr = 0; dr < 2; ++dr)
+#pragma unroll
+                    for (int dc = 0; dc < 4; ++dc)
+                        if ((dr == 0 || r1ok) && col + dc < W) zr[dr * W + dc] = __builtin_bit_cast(uint16_t, (__bf16)px[dr][dc]);
             }
         }
         __syncthreads();  // band done: slot i & 1 is free
-        if (i + 2 < OH) store_row(i & 1);
+        store_row(i & 1);  // row i + 2 (past the last row: taps 255, gradient 0)
     }
     // the 8 threads of a channel: fixed butterfly order; partials [C][B] (one slice per sample)
 #pragma unroll
@@ -1411,8 +1441,8 @@ int launch_stem_pool_bwd(StemArgs a, int* nslice, hipStream_t s) {
                   "stem_pool_bwd: missing argument");
     PCX_CHECK_ARG(a.cout == 64 && a.OW <= 128 && (int64_t)2 * a.B < ((int64_t)1 << 31), "stem_pool_bwd: shape");
     *nslice = a.B;  // partials [cout][B]
-    const int n = 32 * a.OW;
-    const size_t lds = (size_t)2 * n * 4 + ((2 * n + 15) & ~15) + (size_t)n * 4;
+    const int np_ = 32 * (a.OW + 2);
+    const size_t lds = (size_t)2 * np_ * 4 + ((2 * np_ + 15) & ~15) + (size_t)np_ * 4;
     stem_pool_bwd_kernel<<<(unsigned)(2 * a.B), SPB_T, lds, s>>>(a);
     PCX_LAUNCH_CHECK("stem_pool_bwd_kernel");
     return PCX_OK;

@@ -50,12 +50,15 @@ __global__ __launch_bounds__(256) void to_nhwc_kernel(NhwcArgs a) {
     const int b = blockIdx.x;
     const int c0 = blockIdx.y * 64, nc = min(64, a.C - c0), ng = nc >> 3;
     __bf16* dimg = static_cast<__bf16*>(a.dst) + (int64_t)b * Hp * Wp * a.C + c0;
+    const bool two = OP == NHWC_BNBWD && a.dst_b != nullptr;
+    __bf16* dimg2 = two ? static_cast<__bf16*>(a.dst_b) + (int64_t)b * Hp * Wp * a.C + c0 : nullptr;
     // per-channel coefficients in LDS first: the element loop then waits on nothing but its loads
-    __shared__ float4 kc[64], kr[64];
+    __shared__ float4 kc[64], kr[64], kc2[64];
     __shared__ float kd[64];
     if (OP != NHWC_COPY && threadIdx.x < nc) {
         const int c = c0 + threadIdx.x;
         kc[threadIdx.x] = a.cf[c];
+        if (two) kc2[threadIdx.x] = a.cf_b[c];
         if (OP == NHWC_ACT || (OP == NHWC_BNBWD && a.mcf)) {
             kr[threadIdx.x] = OP == NHWC_ACT ? (a.rcf ? a.rcf[c] : make_float4(1.f, 0.f, 0.f, 0.f)) : a.mcf[c];
             kd[threadIdx.x] = a.drop ? a.drop[(int64_t)b * a.C + c] : 1.f;
@@ -66,8 +69,13 @@ __global__ __launch_bounds__(256) void to_nhwc_kernel(NhwcArgs a) {
         const int r = i / (Wp * ng), j = i - r * (Wp * ng);
         const int wp = j / ng, g = j - wp * ng;
         *reinterpret_cast<bf16x8*>(dimg + ((int64_t)r * (Hp - 1) * Wp + wp) * a.C + 8 * g) = bf16x8{};
+        if (two) *reinterpret_cast<bf16x8*>(dimg2 + ((int64_t)r * (Hp - 1) * Wp + wp) * a.C + 8 * g) = bf16x8{};
     }
-    const int W = a.W, TW = W + 1, nv = W / V, n = nc * nv;
+    // LDS tile [64][TW] with channel c's row at c TW + 4 (c >> 3): TW a multiple of 4 keeps the V-wide
+    // row writes aligned, and the 4 (c >> 3) shift puts the 8 channel rows a row-out read touches (lanes
+    // g = 0..7 of one pixel, 4 pixels per 32 lanes) on 32 different banks
+    const int W = a.W, TW = (W + 3) & ~3, nv = W / V, n = nc * nv;
+    float* t2 = t + 64 * TW + 32;  // (two: the second image's tile)
     const int64_t HW = (int64_t)a.H * W;
     const int64_t pbase = ((int64_t)b * a.C + c0) * HW;
     constexpr int U = 4;
@@ -76,7 +84,7 @@ __global__ __launch_bounds__(256) void to_nhwc_kernel(NhwcArgs a) {
         const int64_t base = pbase + (int64_t)h * W;
         __syncthreads();  // (coefficients ready; previous row's LDS reads done)
         for (int i0 = 0; i0 < n; i0 += U * 256) {
-            fv x[U], y2[U];
+            fv x[U], y2[U], y3[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {  // (tail items load a valid element and are dropped below)
                 const int i = min(i0 + u * 256 + (int)threadIdx.x, n - 1);
@@ -84,6 +92,7 @@ __global__ __launch_bounds__(256) void to_nhwc_kernel(NhwcArgs a) {
                 const int64_t o = base + c * HW + w0;
                 x[u] = *reinterpret_cast<const fv*>(a.src + o);
                 if (OP == NHWC_BNBWD) y2[u] = *reinterpret_cast<const fv*>(a.y + o);
+                if (OP == NHWC_BNBWD && two) y3[u] = *reinterpret_cast<const fv*>(a.y_b + o);
                 if (OP == NHWC_ACT) {
                     if (a.res_pool) {  // pooled NHWC: the channel's elements are C apart
                         const float* rp = a.res + (((int64_t)b * a.H + h) * W + w0) * a.C + c0 + c;
@@ -108,6 +117,13 @@ __global__ __launch_bounds__(256) void to_nhwc_kernel(NhwcArgs a) {
 #pragma unroll
                             for (int e = 0; e < V; ++e) v[e] = fmaf(y2[u][e], mk.x, mk.y) > 0.f ? v[e] * d : 0.f;
                         }
+                        if (two) {
+                            const float4 k2 = kc2[c];
+                            fv v2;
+#pragma unroll
+                            for (int e = 0; e < V; ++e) v2[e] = k2.x * (v[e] - k2.y - (y3[u][e] - k2.w) * k2.z);
+                            *reinterpret_cast<fv*>(t2 + c * TW + 4 * (c >> 3) + w0) = v2;
+                        }
 #pragma unroll
                         for (int e = 0; e < V; ++e) v[e] = k.x * (v[e] - k.y - (y2[u][e] - k.w) * k.z);
                     } else if (OP == NHWC_ACT) {
@@ -131,8 +147,7 @@ __global__ __launch_bounds__(256) void to_nhwc_kernel(NhwcArgs a) {
                             else *mp = (uint8_t)mb;
                         }
                     }
-#pragma unroll
-                    for (int e = 0; e < V; ++e) t[c * TW + w0 + e] = v[e];
+                    *reinterpret_cast<fv*>(t + c * TW + 4 * (c >> 3) + w0) = v;
                 }
             }
         }
@@ -143,9 +158,17 @@ __global__ __launch_bounds__(256) void to_nhwc_kernel(NhwcArgs a) {
             bf16x8 o{};
             if (wp > 0 && wp <= W) {
 #pragma unroll
-                for (int j = 0; j < 8; ++j) o[j] = (__bf16)t[(8 * g + j) * TW + wp - 1];
+                for (int j = 0; j < 8; ++j) o[j] = (__bf16)t[(8 * g + j) * TW + 4 * g + wp - 1];
             }
             *reinterpret_cast<bf16x8*>(drow + (int64_t)wp * a.C + 8 * g) = o;
+            if (two) {
+                bf16x8 o2{};
+                if (wp > 0 && wp <= W) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) o2[j] = (__bf16)t2[(8 * g + j) * TW + 4 * g + wp - 1];
+                }
+                *reinterpret_cast<bf16x8*>(dimg2 + (int64_t)(h + 1) * Wp * a.C + (int64_t)wp * a.C + 8 * g) = o2;
+            }
         }
     }
 }
@@ -522,7 +545,8 @@ int launch_to_nhwc(NhwcArgs a, hipStream_t s) {
     PCX_CHECK_ARG(a.op != NHWC_BNBWD || (a.y && a.cf), "to_nhwc: BN backward needs y and cf");
     PCX_CHECK_ARG(a.op != NHWC_ACT || a.cf, "to_nhwc: activation needs cf");
     PCX_CHECK_ARG(!a.res_pool || (a.op == NHWC_ACT && a.res && a.rcf), "to_nhwc: pooled residual needs res and rcf");
-    const size_t sm = (size_t)64 * (a.W + 1) * 4;
+    PCX_CHECK_ARG(!a.dst_b || (a.op == NHWC_BNBWD && a.y_b && a.cf_b), "to_nhwc: second image needs y_b and cf_b");
+    const size_t sm = ((size_t)64 * ((a.W + 3) & ~3) + 32) * 4 * (a.dst_b ? 2 : 1);
     PCX_CHECK_ARG(sm <= 64 * 1024, "to_nhwc: row of %d pixels too long", a.W);
     dim3 grid((unsigned)a.B, (unsigned)ceil_div(a.C, 64));
     const int v = a.W % 4 == 0 ? 4 : a.W % 2 == 0 ? 2 : 1;

@@ -716,13 +716,12 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
             NhwcArgs t = nhwc_args(NHWC_BNBWD, B, k.cout, k.Ho, k.Wo, g, dyn1);
             t.y = c.w<float>(k.y2);
             t.cf = c.w<float4>(k.cfb2);
-            RC(launch_to_nhwc(t, s));
-            if (k.sc) {
-                t.y = c.w<float>(k.ysc);
-                t.cf = c.w<float4>(k.cfbsc);
-                t.dst = dyn2;
-                RC(launch_to_nhwc(t, s));
+            if (k.sc) {  // the shortcut's dy image from the same g in the same pass
+                t.y_b = c.w<float>(k.ysc);
+                t.cf_b = c.w<float4>(k.cfbsc);
+                t.dst_b = dyn2;
             }
+            RC(launch_to_nhwc(t, s));
         } else {
             Scope sc(&p.prof, s, "bn_bwd_apply", L + 1);
             // (a routed conv2's dy is produced by its weight-gradient kernel's staging)

@@ -350,6 +350,11 @@ struct NhwcArgs {
     float* out32;          // NHWC_ACT: optional float32 NCHW copy of the result
     uint8_t* mask8;        // NHWC_ACT: optional NCHW bytes [result > 0] (the backward's ReLU mask)
     void* dst;             // [B][H + 2][W + 2][C] bf16
+    // NHWC_BNBWD (optional): a second image from the same src through a second BN backward (the
+    // shortcut BN of a residual block shares the upstream gradient: read once, two images written)
+    const float* y_b;
+    const float4* cf_b;
+    void* dst_b;
 };
 size_t nhwc_bytes(int B, int C, int H, int W);
 int launch_to_nhwc(NhwcArgs a, hipStream_t s);
