@@ -80,8 +80,21 @@ __global__ __launch_bounds__(256) void to_nhwc_kernel(NhwcArgs a) {
     const int64_t pbase = ((int64_t)b * a.C + c0) * HW;
     constexpr int U = 4;
     // the block walks its sample's rows: consecutive rows of the same 64 planes (page / line reuse)
+    float* rres = t + (two ? 2 : 1) * (64 * TW + 32);  // res_pool: the row's residual, transposed like t
     for (int h = 0; h < a.H; ++h) {
         const int64_t base = pbase + (int64_t)h * W;
+        if (OP == NHWC_ACT && a.res_pool) {  // pooled NHWC row (b, h): 16-byte runs of 4 channels, coalesced
+            const float* rrow = a.res + ((int64_t)b * a.H + h) * W * a.C + c0;
+            const int nq = W * (nc >> 2);
+            for (int k = threadIdx.x; k < nq; k += 256) {
+                const int w = k / (nc >> 2), c4 = (k - w * (nc >> 2)) * 4;
+                const float4 r4 = *reinterpret_cast<const float4*>(rrow + (int64_t)w * a.C + c4);
+                rres[c4 * TW + 4 * (c4 >> 3) + w] = r4.x;
+                rres[(c4 + 1) * TW + 4 * ((c4 + 1) >> 3) + w] = r4.y;
+                rres[(c4 + 2) * TW + 4 * ((c4 + 2) >> 3) + w] = r4.z;
+                rres[(c4 + 3) * TW + 4 * ((c4 + 3) >> 3) + w] = r4.w;
+            }
+        }
         __syncthreads();  // (coefficients ready; previous row's LDS reads done)
         for (int i0 = 0; i0 < n; i0 += U * 256) {
             fv x[U], y2[U], y3[U];
@@ -94,10 +107,8 @@ __global__ __launch_bounds__(256) void to_nhwc_kernel(NhwcArgs a) {
                 if (OP == NHWC_BNBWD) y2[u] = *reinterpret_cast<const fv*>(a.y + o);
                 if (OP == NHWC_BNBWD && two) y3[u] = *reinterpret_cast<const fv*>(a.y_b + o);
                 if (OP == NHWC_ACT) {
-                    if (a.res_pool) {  // pooled NHWC: the channel's elements are C apart
-                        const float* rp = a.res + (((int64_t)b * a.H + h) * W + w0) * a.C + c0 + c;
-#pragma unroll
-                        for (int e = 0; e < V; ++e) y2[u][e] = rp[(int64_t)e * a.C];
+                    if (a.res_pool) {  // staged above (transposed)
+                        y2[u] = *reinterpret_cast<const fv*>(rres + c * TW + 4 * (c >> 3) + w0);
                     } else {
                         y2[u] = a.res ? *reinterpret_cast<const fv*>(a.res + o) : fv{};
                     }
@@ -546,7 +557,8 @@ int launch_to_nhwc(NhwcArgs a, hipStream_t s) {
     PCX_CHECK_ARG(a.op != NHWC_ACT || a.cf, "to_nhwc: activation needs cf");
     PCX_CHECK_ARG(!a.res_pool || (a.op == NHWC_ACT && a.res && a.rcf), "to_nhwc: pooled residual needs res and rcf");
     PCX_CHECK_ARG(!a.dst_b || (a.op == NHWC_BNBWD && a.y_b && a.cf_b), "to_nhwc: second image needs y_b and cf_b");
-    const size_t sm = ((size_t)64 * ((a.W + 3) & ~3) + 32) * 4 * (a.dst_b ? 2 : 1);
+    const size_t sm = ((size_t)64 * ((a.W + 3) & ~3) + 32) * 4 * (a.dst_b || a.res_pool ? 2 : 1);
+    PCX_CHECK_ARG(!a.res_pool || a.C % 4 == 0, "to_nhwc: pooled residual needs C %% 4 == 0");
     PCX_CHECK_ARG(sm <= 64 * 1024, "to_nhwc: row of %d pixels too long", a.W);
     dim3 grid((unsigned)a.B, (unsigned)ceil_div(a.C, 64));
     const int v = a.W % 4 == 0 ? 4 : a.W % 2 == 0 ? 2 : 1;
