@@ -1194,6 +1194,108 @@ __global__ __launch_bounds__(256) void stem_wgrad_mfma_kernel(StemArgs a) {
     }
 }
 
+// float32 precision, cout = 64: the stem weight gradient on fp32 MFMA (v_mfma_f32_32x32x2_f32),
+// dW[cout][tap] = sum_p dy[cout][p] x[p + tap], with stem_wgrad_mfma_kernel's waves, slices and tap
+// grid.  Per 16-pixel chunk (virtual pixels over rows padded to WV = W rounded up to 8), lane (cout
+// l32, half h) loads its 8 pixels p0 + 8 h .. + 7 of dz0 and y0 (16-byte loads, one chunk ahead),
+// forms dy = BN backward in float32 and feeds them as the A operand of 8 K-steps (K-step ks: pixel
+// p0 + 8 h + ks in lane half h); B = x at tap column 32 nt + l32 of the same pixels, 8 consecutive
+// floats of one LDS row.  Products and sums in float32; only the summation order differs from
+// stem_wgrad_kernel<false>.
+__global__ __launch_bounds__(256) void stem_wgrad_f32_kernel(StemArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float xs[];  // (H + 8) rows of the sample
+    __shared__ float red[2][32][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
+    const int mt = wave >> 1, wt = wave & 1;
+    const int H = a.H, W = a.W, HW = H * W, RW = st_rw(W), WV = (W + 7) & ~7, HWV = H * WV;
+    const int slice = blockIdx.x;
+    const int b0 = slice * a.rows_per_blk, b1 = min(a.B, b0 + a.rows_per_blk);
+    const int co = 32 * mt + l32;
+    float A1, A2, A3;
+    {
+        const float4 k = a.cf_dy[co];  // dy = a (dz - mb - (y - mean) mgi)
+        A1 = k.x;
+        A2 = -k.x * k.z;
+        A3 = k.x * (k.w * k.z - k.y);
+    }
+    int boff[2];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+        const int t = 32 * nt + l32, dh = t >> 3, dw = t & 7;
+        boff[nt] = dh * RW + dw;
+    }
+    f32x16 acc[2] = {f32x16{0.f}, f32x16{0.f}};
+    for (int i = threadIdx.x; i < (H + 8) * RW; i += 256) xs[i] = 0.f;
+    const int nchunk = (HWV + 15) >> 4;
+    for (int b = b0; b < b1; ++b) {
+        __syncthreads();
+        st_stage<false>(a.x + (int64_t)b * HW, H, W, xs);
+        __syncthreads();
+        const float* zb = a.dz + ((int64_t)b * a.cout + co) * HW;
+        const float* yb = a.y + ((int64_t)b * a.cout + co) * HW;
+        // the lane's run of chunk ch: 8 pixels of one padded row (nv real ones, <= 0: padding)
+        auto load = [&](int ch, float (&z)[8], float (&y)[8]) {
+            const int p = ch * 16 + 8 * h;
+            const int hh = p / WV, ww = p - hh * WV;
+            const int nv = (ch < nchunk && hh < H) ? min(8, W - ww) : 0;
+            const int o = min(hh, H - 1) * W + ww;
+            if ((W & 3) == 0) {  // nv is 0, 4 or 8
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const bool v = nv >= 4 * q + 4;
+                    const float4 tz = v ? ld4(zb + o + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+                    const float4 ty = v ? ld4(yb + o + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+                    z[4 * q] = tz.x; z[4 * q + 1] = tz.y; z[4 * q + 2] = tz.z; z[4 * q + 3] = tz.w;
+                    y[4 * q] = ty.x; y[4 * q + 1] = ty.y; y[4 * q + 2] = ty.z; y[4 * q + 3] = ty.w;
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    z[e] = e < nv ? zb[o + e] : 0.f;
+                    y[e] = e < nv ? yb[o + e] : 0.f;
+                }
+            }
+            return nv;
+        };
+        float zn[8], yn[8];
+        int nvn = load(wt, zn, yn);
+        for (int ch = wt; ch < nchunk; ch += 2) {
+            float dy[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) dy[e] = e < nvn ? fmaf(A1, zn[e], fmaf(A2, yn[e], A3)) : 0.f;
+            nvn = load(ch + 2, zn, yn);  // in flight under this chunk's MFMAs
+            const int p = min(ch * 16 + 8 * h, HWV - 8);
+            const int hh = p / WV, ww = p - hh * WV;
+            const float* xb = xs + hh * RW + ww + 1;
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt)
+                    acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(dy[ks], xb[boff[nt] + ks], acc[nt], 0, 0, 0);
+        }
+    }
+    // the two waves of a cout half: fixed-order sum through LDS, then the 49 real taps to the slice
+    if (wt == 1) {
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) red[mt][acc_row(r, h)][32 * nt + l32] = acc[nt][r];
+    }
+    __syncthreads();
+    if (wt == 0) {
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int t = 32 * nt + l32, dh = t >> 3, dw = t & 7;
+                if (dh < ST_K && dw < ST_K) {
+                    const int c = 32 * mt + acc_row(r, h);
+                    a.part[((int64_t)slice * a.cout + c) * ST_T + dh * ST_K + dw] = acc[nt][r] + red[mt][acc_row(r, h)][t];
+                }
+            }
+    }
+}
+
 template <bool BF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void stem_wgrad_kernel(StemArgs a) {
     extern __shared__ __attribute__((aligned(16))) float xs[];
@@ -1405,7 +1507,7 @@ int launch_stem_fwd(StemArgs a, int bf16, float* wround, hipStream_t s) {
     return PCX_OK;
 }
 
-bool stem_wgrad_mfma_ok(int cout, int H, int W) {
+bool stem_wgrad_mfma_ok(int cout, int H, int W) {  // (the bf16 and the fp32 MFMA forms)
     return cout == 64 && (size_t)(H + 8) * st_rw(W) * 4 + 48 * 1024 <= 160 * 1024;
 }
 
@@ -1468,6 +1570,14 @@ int launch_stem_wgrad(StemArgs a, int bf16, hipStream_t s) {
                                   (int)smm);
         stem_wgrad_mfma_kernel<<<(unsigned)a.nblk, 256, smm, s>>>(a);
         PCX_LAUNCH_CHECK("stem_wgrad_mfma_kernel");
+        return PCX_OK;
+    }
+    if (!bf16 && stem_wgrad_mfma_ok(a.cout, a.H, a.W)) {  // fp32 MFMA form: one block per slice
+        const size_t smm = (size_t)(a.H + 8) * st_rw(a.W) * 4;
+        (void)hipFuncSetAttribute((const void*)stem_wgrad_f32_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)smm);
+        stem_wgrad_f32_kernel<<<(unsigned)a.nblk, 256, smm, s>>>(a);
+        PCX_LAUNCH_CHECK("stem_wgrad_f32_kernel");
         return PCX_OK;
     }
     const size_t sm = stem_smem(a.H, a.W);

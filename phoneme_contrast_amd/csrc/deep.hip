@@ -117,7 +117,7 @@ int build_deep(Plan& p) {
     // the 7x7 stem runs on its own direct kernels (conv.hip): forward partials, gradient slices
     d.stem_nblk = stem_nblk(B, d.H0, &d.stem_rows);
     d.stem_ns = stem_wgrad_nslice(B, d.H0, &d.stem_srows,
-                                  d.stem_fused || (d.bf16 && stem_wgrad_mfma_ok(d.h[0], d.H0, d.W0)));
+                                  d.stem_fused || stem_wgrad_mfma_ok(d.h[0], d.H0, d.W0));
     stat = std::max(stat, (size_t)3 * C0 * d.stem_nblk + d.stem_nblk);
     wg = std::max(wg, (size_t)d.stem_ns * C0 * 49);
     d.stemw = p.carve("stem_w16", (size_t)C0 * 49 * 4);

@@ -162,7 +162,7 @@ struct StemArgs {
 };
 int stem_nblk(int B, int H, int* rows_per_blk);
 int stem_wgrad_nslice(int B, int H, int* rows_per_slice, bool mfma = false);
-bool stem_wgrad_mfma_ok(int cout, int H, int W);  // bf16: the MFMA weight-gradient form applies
+bool stem_wgrad_mfma_ok(int cout, int H, int W);  // the MFMA weight-gradient forms (bf16 / fp32) apply
 // fused bf16 stem: forward statistics only (a.out = nullptr), then the pooled outputs from a
 // recomputed y0; weight gradient from dz0 and a recomputed y0 (no y0 plane anywhere)
 bool stem_fused_ok(int cout, int H, int W);
