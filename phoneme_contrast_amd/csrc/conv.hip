@@ -556,6 +556,97 @@ __global__ __launch_bounds__(256) void stem_fwd_mfma_kernel(StemArgs a) {
     if (threadIdx.x == 0) a.partn[blockIdx.x] = n;
 }
 
+// float32 precision, cout = 64: the 7x7 stem on fp32 MFMA (v_mfma_f32_32x32x2_f32), C[cout][pixel] =
+// W[cout][tap] x im2col[tap][pixel] per 32-pixel tile, K = the 49 taps in 25 K-steps (tap 2 ks + h in
+// lane half h; the 50th carries a zero weight).  Weights stay in registers (A: 25 per lane), B = x of
+// the fp32 LDS image at the lane's pixel + the tap's offset (one ds_read_b32 per K-step).  Products
+// and sums in float32; only the summation order differs from stem_fwd_kernel<false>.  Stores and BN
+// partials as stem_fwd_mfma_kernel's.
+__global__ __launch_bounds__(256) void stem_fwd_f32_kernel(StemArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float xs[];  // (H + 8) rows of the sample
+    __shared__ float red[2][64][2];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
+    const int mt = wave >> 1, wt = wave & 1;
+    const int H = a.H, W = a.W, HW = H * W, RW = st_rw(W);
+    constexpr int NK = (ST_T + 1) / 2;
+    float A[NK];
+    int toff[NK];
+#pragma unroll
+    for (int s = 0; s < NK; ++s) {
+        const int t = 2 * s + h;
+        A[s] = t < ST_T ? a.w[(32 * mt + l32) * ST_T + t] : 0.f;
+        toff[s] = t < ST_T ? (t / ST_K) * RW + t % ST_K : 0;
+    }
+    for (int i = threadIdx.x; i < (H + 8) * RW; i += 256) xs[i] = 0.f;
+    const int ntile = (HW + 31) >> 5;
+    auto tile = [&](int tt, int& p) {
+        p = tt * 32 + l32;
+        const int pc = min(p, HW - 1);
+        const int hh = pc / W, ww = pc - hh * W;
+        const float* xb = xs + hh * RW + ww + 1;
+        f32x16 acc = {0.f};
+#pragma unroll
+        for (int s = 0; s < NK; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(A[s], xb[toff[s]], acc, 0, 0, 0);
+        return acc;
+    };
+    float K[16], s1[16], s2[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s1[r] = s2[r] = 0.f;
+    int nsamp = 0;
+    for (int b = blockIdx.x; b < a.B; b += gridDim.x, ++nsamp) {
+        __syncthreads();
+        st_stage<false>(a.x + (int64_t)b * HW, H, W, xs);
+        __syncthreads();
+        if (b == (int)blockIdx.x) {  // shift: every wave evaluates the block's first pixel itself
+            int p;
+            const f32x16 acc = tile(0, p);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) K[r] = __shfl(acc[r], 32 * h, 64);
+        }
+        float* ob = a.out + ((int64_t)b * a.cout + 32 * mt) * HW;
+        for (int tt = wt; tt < ntile; tt += 2) {
+            int p;
+            const f32x16 acc = tile(tt, p);
+            if (p < HW) {
+                float* op = ob + p;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float v = acc[r];
+                    op[acc_row(r, h) * HW] = v;
+                    const float d = v - K[r];
+                    s1[r] += d;
+                    s2[r] = fmaf(d, d, s2[r]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        float t1 = s1[r], t2 = s2[r];
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) {
+            t1 += __shfl_xor(t1, o, 64);
+            t2 += __shfl_xor(t2, o, 64);
+        }
+        if (l32 == 0) {
+            red[wt][32 * mt + acc_row(r, h)][0] = t1;
+            red[wt][32 * mt + acc_row(r, h)][1] = t2;
+        }
+    }
+    __syncthreads();
+    const float n = (float)nsamp * (float)HW;
+    if (wt == 0 && l32 == 0) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int c = 32 * mt + acc_row(r, h);
+            const float t1 = red[0][c][0] + red[1][c][0], t2 = red[0][c][1] + red[1][c][1];
+            a.part0[(int64_t)c * a.nblk + blockIdx.x] = n * K[r] + t1;
+            a.part1[(int64_t)c * a.nblk + blockIdx.x] = n > 0.f ? fmaxf(t2 - t1 * t1 / n, 0.f) : 0.f;
+        }
+    }
+    if (threadIdx.x == 0) a.partn[blockIdx.x] = n;
+}
+
 // ------------------------------------------------------------------ fused bf16 stem (no y0 plane)
 // At T = 200 the stem's 64 x 40 x 200 fp32 output is 8.4 GB per 4096-sample step, written once and
 // read three times (pool, pool backward, weight gradient) -- more HBM traffic than the rest of the
@@ -1494,6 +1585,14 @@ int launch_stem_fwd(StemArgs a, int bf16, float* wround, hipStream_t s) {
         return PCX_OK;
     }
     PCX_CHECK_ARG(a.out, "stem: statistics-only pass needs the bf16 MFMA form");
+    if (!bf16 && a.cout == 64 && (size_t)(a.H + 8) * st_rw(a.W) * 4 <= 128 * 1024) {  // fp32 MFMA form
+        const size_t smm = (size_t)(a.H + 8) * st_rw(a.W) * 4;
+        (void)hipFuncSetAttribute((const void*)stem_fwd_f32_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)smm);
+        stem_fwd_f32_kernel<<<a.nblk, 256, smm, s>>>(a);
+        PCX_LAUNCH_CHECK("stem_fwd_f32_kernel");
+        return PCX_OK;
+    }
 #define PCX_STEM_F(B_, C_)                                                                          \
     if ((bf16 != 0) == B_ && a.cout == 4 * C_) {                                                    \
         (void)hipFuncSetAttribute((const void*)stem_fwd_kernel<B_, C_>,                              \
