@@ -287,21 +287,20 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
             const float* q1 = dr1 + 4 * s0;
             kloop(w, u, q0, q1, sx, sy, acc, n);
         };
-        const int Ks = a.Ksteps, Kh = Ks >> 1;
+        const int Ks = a.Ksteps;
         for (int tr = 0; tr < TR; ++tr) {
             const bool pre = tr + 1 < TR;
             // the next tile row's dz / y now, its x rows half way (registers: dy is formed from dz, y
             // before the x loads are issued)
-            if (pre) load_dy(tr + 1);
+            if (pre) {
+                load_dy(tr + 1);
+                load_x(tr + 1);
+            }
             // x rows 2 tr - 1 + i of this tile row live in ring slot (2 tr + i) & 3
             const float* xw = xl + ((2 * tr + IW) & 3) * 32 * XCS + c32 * XCS + 2 * g;
             const float* xu = xl + ((2 * tr + IU) & 3) * 32 * XCS + c32 * XCS + 2 * g;
-            ksteps(xw, xu, 0, Kh);
-            if (pre) {
-                form_dy(tr + 1);
-                load_x(tr + 1);
-            }
-            ksteps(xw, xu, Kh, Ks);
+            ksteps(xw, xu, 0, Ks);
+            if (pre) form_dy(tr + 1);
             __syncthreads();  // the dy rows and the two oldest x rows are free
             if (pre) store(tr + 1);
             __syncthreads();
