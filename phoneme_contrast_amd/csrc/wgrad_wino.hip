@@ -227,26 +227,15 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
 #pragma unroll
             for (int m = 0; m < NIT; ++m) xv[m] = bload<V>(rx, (xm >> m) & 1 ? 4 * (xgo(m) + xb) : OOB);
         };
-        auto store = [&](int st) {
+        auto store_x = [&](int st, const vecf<V> (&xr)[NIT]) {
             unsigned dm, xm;
             masks(st, dm, xm);
-            const int db = 2 * st * W + c0;
-#pragma unroll
-            for (int m = 0; m < NIT; ++m) {
-                if (!((dex >> m) & 1)) continue;
-                const bool ok = (dm >> m) & 1;
-                const vecf<V> v = dzv[m];
-                float* d = dyl + dlb + (m / NIR) * 32 * DCS + 8 * V * (m % NIR);
-                *reinterpret_cast<f2*>(d) = f2{v[0], v[1]};
-                if constexpr (V == 4) *reinterpret_cast<f2*>(d + 2) = f2{v[2], v[3]};
-                if (write_dy) bstore<V>(rdo, ok ? 4 * (dgo(m) + db) : OOB, v);
-            }
             // x rows 2 st + 1, 2 st + 2 -> ring slots (2 st + 2) & 3, (2 st + 3) & 3
             const int sl0 = ((2 * st + 2) & 3) * 32 * XCS, sl1 = ((2 * st + 3) & 3) * 32 * XCS;
 #pragma unroll
             for (int m = 0; m < NIT; ++m) {
                 if (!((xex >> m) & 1)) continue;
-                vecf<V> v = xv[m];
+                vecf<V> v = xr[m];
                 if (PRO == PRO_BNRELU) {
                     const float tt = (xm >> m) & 1 ? xt : 0.f;
 #pragma unroll
@@ -264,12 +253,36 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
             }
         };
 
-        // task prologue: stages -1 and 0 (x rows -1 .. 2, dy rows 0, 1)
-        for (int st = -1; st <= 0; ++st) {
-            load_dy(st);
-            load_x(st);
-            form_dy(st);
-            store(st);
+        auto store = [&](int st) {
+            unsigned dm, xm;
+            masks(st, dm, xm);
+            const int db = 2 * st * W + c0;
+#pragma unroll
+            for (int m = 0; m < NIT; ++m) {
+                if (!((dex >> m) & 1)) continue;
+                const bool ok = (dm >> m) & 1;
+                const vecf<V> v = dzv[m];
+                float* d = dyl + dlb + (m / NIR) * 32 * DCS + 8 * V * (m % NIR);
+                *reinterpret_cast<f2*>(d) = f2{v[0], v[1]};
+                if constexpr (V == 4) *reinterpret_cast<f2*>(d + 2) = f2{v[2], v[3]};
+                if (write_dy) bstore<V>(rdo, ok ? 4 * (dgo(m) + db) : OOB, v);
+            }
+            store_x(st, xv);
+        };
+
+        // task prologue: stages -1 and 0 (x rows -1 .. 2, dy rows 0, 1) loaded together: one round trip
+        {
+            load_dy(0);
+            load_x(0);
+            vecf<V> xa[NIT];  // stage -1: x rows -1 (zeros: the ring slot holds the previous task's rows), 0
+            unsigned dm, xm;
+            masks(-1, dm, xm);
+            const int xb = -W + c0;
+#pragma unroll
+            for (int m = 0; m < NIT; ++m) xa[m] = bload<V>(rx, (xm >> m) & 1 ? 4 * (xgo(m) + xb) : OOB);
+            store_x(-1, xa);
+            form_dy(0);
+            store(0);
         }
         __syncthreads();
         // wave constants of row Q: e = w + sx u from x rows (w, u) of the tile row's four; the dy row
@@ -290,8 +303,7 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
         const int Ks = a.Ksteps;
         for (int tr = 0; tr < TR; ++tr) {
             const bool pre = tr + 1 < TR;
-            // the next tile row's dz / y now, its x rows half way (registers: dy is formed from dz, y
-            // before the x loads are issued)
+            // the next tile row's dz / y / x rows now (a whole row of MFMAs to land), dy formed after
             if (pre) {
                 load_dy(tr + 1);
                 load_x(tr + 1);
