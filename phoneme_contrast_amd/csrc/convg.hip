@@ -435,6 +435,15 @@ __global__ __launch_bounds__(256) void chan_stats_kernel(const float* __restrict
     }
 }
 
+// n / d for 0 <= n < 2^22 with inv = 1 / d (float): one correction step makes it exact
+__device__ __forceinline__ int wdiv_f(int n, int d, float inv) {
+    int q = (int)((float)n * inv);
+    const int r = n - q * d;
+    q += r >= d ? 1 : 0;
+    q -= r < 0 ? 1 : 0;
+    return q;
+}
+
 // Backward BN partials: g = d (+ d2) masked, written to g; sums of g and g*xhat_k for up to two
 // BNs (the main-path BN and the shortcut BN of a residual block share the same upstream g).
 // Units of V elements (16-byte accesses when P % 4 == 0), U units in flight per thread.
@@ -448,6 +457,7 @@ __global__ __launch_bounds__(256) void bwd_prep_kernel(BwdPrepArgs a) {
     const float4 mc = a.mask_cf ? a.mask_cf[c] : make_float4(1.f, 0.f, 0.f, 1.f);
     const float4 c1 = a.cf1 ? a.cf1[c] : make_float4(0.f, 0.f, 0.f, 0.f);
     const float4 c2 = a.cf2 ? a.cf2[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float a_invW = a.dpar ? 1.f / (float)a.W : 0.f;
     double sg = 0.0, sx1 = 0.0, sx2 = 0.0;
     PlaneWalk w(b0, PV);
     while (w.b < b1) {
@@ -463,7 +473,43 @@ __global__ __launch_bounds__(256) void bwd_prep_kernel(BwdPrepArgs a) {
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            g[u] = *reinterpret_cast<const fv*>(a.d + o[u]);
+            if (a.dpar) {  // class-planar d: the V elements from their parity classes
+                const int p0 = (int)(o[u] - bc[u] * P), W = a.W;
+                bool done = false;
+                if constexpr (V == 4) {
+                    if ((W & 3) == 0) {  // one row, columns w0 .. w0 + 3 (w0 % 4 == 0): two 8-byte loads
+                        const int h = wdiv_f(p0, W, a_invW), w0 = p0 - h * W;
+                        const int r = h & 1, IWc = W >> 1, IHc = (a.H - r + 1) >> 1;
+                        const int64_t so = bc[u] * IHc * IWc + (int64_t)(h >> 1) * IWc + (w0 >> 1);
+                        const float2 e = *reinterpret_cast<const float2*>(a.dpar + a.dpo[2 * r] + so);
+                        const float2 od = *reinterpret_cast<const float2*>(a.dpar + a.dpo[2 * r + 1] + so);
+                        g[u] = fv{e.x, od.x, e.y, od.y};
+                        done = true;
+                    } else if ((W & 1) == 0) {  // two column pairs (w, w + 1), w even: one division each
+                        const int IWc = W >> 1;
+#pragma unroll
+                        for (int k2 = 0; k2 < 2; ++k2) {
+                            const int pp = p0 + 2 * k2, h = wdiv_f(pp, W, a_invW), w = pp - h * W;
+                            const int r = h & 1, IHc = (a.H - r + 1) >> 1;
+                            const int64_t so = bc[u] * IHc * IWc + (int64_t)(h >> 1) * IWc + (w >> 1);
+                            g[u][2 * k2] = a.dpar[a.dpo[2 * r] + so];
+                            g[u][2 * k2 + 1] = a.dpar[a.dpo[2 * r + 1] + so];
+                        }
+                        done = true;
+                    }
+                }
+                if (!done) {
+#pragma unroll
+                    for (int e = 0; e < V; ++e) {
+                        const int pp = p0 + e, h = wdiv_f(pp, W, a_invW), w = pp - h * W;
+                        const int q = 2 * (h & 1) + (w & 1);
+                        const int IHc = (a.H - (h & 1) + 1) >> 1, IWc = (W - (w & 1) + 1) >> 1;
+                        g[u][e] = pp < P ? a.dpar[a.dpo[q] + bc[u] * IHc * IWc + (int64_t)(h >> 1) * IWc + (w >> 1)] : 0.f;
+                    }
+                }
+            } else {
+                g[u] = *reinterpret_cast<const fv*>(a.d + o[u]);
+            }
             if (a.d2) g[u] += *reinterpret_cast<const fv*>(a.d2 + o[u]);
             if (a.mask_mode == MASK_OUT8) {  // V mask bytes as 0 / 1 floats
                 unsigned mb;
@@ -962,6 +1008,9 @@ int launch_chan_stats(const float* y, int B, int C, int64_t P, float* part0, flo
 
 int launch_bwd_prep(BwdPrepArgs a, int* nslice, hipStream_t s) {
     PCX_CHECK_ARG(a.mask_mode != MASK_OUT8 || a.mask8, "bwd_prep: MASK_OUT8 needs mask8");
+    PCX_CHECK_ARG(a.dpar ? (a.H >= 1 && a.W >= 1 && (int64_t)a.H * a.W == a.P && a.P < (1 << 22) && !a.d2)
+                         : a.d != nullptr,
+                  "bwd_prep: bad upstream gradient arguments");
     const int ns = chan_slices(a.B, a.C, &a.bps);
     *nslice = ns;
     if (a.P % 4 == 0) bwd_prep_kernel<4, 2><<<dim3(a.C, ns), 256, 0, s>>>(a);

@@ -664,6 +664,10 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
     // upstream gradient of the current block's output (already ReLU-masked for the last block)
     const float* dout = c.w<float>(d.hdz);
     const float* dout2 = nullptr;  // block 0's shortcut gradient, added by the fused stem backward
+    // a stride-2 block's input gradient left in its parity-class planes (d.partmp): the previous
+    // block's BN backward prep reads them directly (no interleave pass)
+    const float* dpar = nullptr;
+    int64_t dpo[4] = {0, 0, 0, 0};
     bool masked = true;
     for (int i = 3; i >= 0; --i) {
         const DeepBlock& k = d.blk[i];
@@ -680,6 +684,11 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
             BwdPrepArgs b{};
             b.B = B; b.C = k.cout; b.P = P2;
             b.d = dout;
+            if (dpar) {
+                b.dpar = dpar;
+                for (int q2 = 0; q2 < 4; ++q2) b.dpo[q2] = dpo[q2];
+                b.H = k.Ho; b.W = k.Wo;
+            }
             if (d.residual) {
                 b.mask_mode = masked ? MASK_NONE : (k.m8 ? MASK_OUT8 : MASK_OUT);
                 b.mask_src = c.w<float>(k.out);
@@ -792,11 +801,17 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
             RC(conv_dgrad(c, 100 + i, dysc, k.cout, k.Ho, k.Wo, 1, k.stride, 0, P[q + 8], da, k.cin, k.Hi, k.Wi, 1,
                           false, dyn2, ptmp));
         }
+        dpar = nullptr;
         if (k.planar) {
-            Scope sc(&p.prof, s, "dgrad_interleave", L);
-            RC(launch_par_interleave(ptmp, da, B, k.cin, k.Hi, k.Wi, acc, s));
+            if (i > 0 && !acc) {  // consumed only by block i - 1's BN backward prep: read in place
+                dpar = ptmp;
+                for (int q2 = 0; q2 < 4; ++q2) dpo[q2] = par_off(B, k.cin, k.Hi, k.Wi, q2);
+            } else {
+                Scope sc(&p.prof, s, "dgrad_interleave", L);
+                RC(launch_par_interleave(ptmp, da, B, k.cin, k.Hi, k.Wi, acc, s));
+            }
         }
-        dout = da;
+        dout = dpar ? nullptr : da;
         dout2 = sc_in_stem ? g : nullptr;
         masked = false;
         p.buckets.mark(k.pidx, s);

@@ -386,6 +386,12 @@ struct BwdPrepArgs {
     float* p_g;               // [C][nslice] partial sums of g
     float* p_x1;              // [C][nslice] partial sums of g*xhat1
     float* p_x2;
+    // d read from the parity-class planes of a stride-2 data gradient (ConvGArgs::par_out) instead of
+    // a plain plane (no interleave pass): element (h, w) of an H x W plane lives in class
+    // q = 2 (h & 1) + (w & 1) at dpar + dpo[q] ([B][C][IHc][IWc] per class, par_off)
+    const float* dpar;
+    int64_t dpo[4];
+    int H, W;
 };
 int launch_bwd_prep(BwdPrepArgs a, int* nslice, hipStream_t s);
 int chan_slices(int B, int C, int* bps);
