@@ -725,6 +725,7 @@ __global__ __launch_bounds__(256) void maxpool3_fwd_lds_kernel(const float* __re
 template <int VEC, bool SEL>
 __global__ __launch_bounds__(256) void maxpool3_bwd_prep_kernel(const uint8_t* __restrict__ arg,
                                                                 const float* __restrict__ dout,
+                                                                const float* __restrict__ dout2,
                                                                 const float* __restrict__ y,
                                                                 const float4* __restrict__ cf, float* __restrict__ g,
                                                                 float* __restrict__ p_g, float* __restrict__ p_x, int B,
@@ -744,7 +745,7 @@ __global__ __launch_bounds__(256) void maxpool3_bwd_prep_kernel(const uint8_t* _
     for (int b = b0; b < b1; ++b) {
         const int64_t row = (int64_t)b * C + c;
         for (int i = threadIdx.x; i < OHW; i += 256) {
-            dl[i] = dout[row * OHW + i];
+            dl[i] = dout2 ? dout[row * OHW + i] + dout2[row * OHW + i] : dout[row * OHW + i];
             al[i] = arg[row * OHW + i];
             if (SEL) ysl[i] = y[row * OHW + i];
         }
@@ -1062,7 +1063,7 @@ bool maxpool3_bwd_prep_fits(int H, int W, int OH, int OW) {
 
 int launch_maxpool3_bwd_prep(const uint8_t* arg, const float* dout, const float* y, const float* ysel, const float4* cf,
                              float* g, float* p_g, float* p_x, int B, int C, int H, int W, int OH, int OW, int* nslice,
-                             hipStream_t s) {
+                             hipStream_t s, const float* dout2) {
     PCX_CHECK_ARG(OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1, "maxpool3: output %dx%d for input %dx%d", OH, OW,
                   H, W);
     PCX_CHECK_ARG(maxpool3_bwd_prep_fits(H, W, OH, OW), "maxpool3_bwd_prep: %dx%d pooled plane exceeds LDS", OH, OW);
@@ -1072,7 +1073,7 @@ int launch_maxpool3_bwd_prep(const uint8_t* arg, const float* dout, const float*
     *nslice = ns;
     const size_t lds = ((size_t)OH * OW * (ysel ? 9 : 5) + 15) / 16 * 16;
 #define PCX_MPB(V_, S_)                                                                                         \
-    maxpool3_bwd_prep_kernel<V_, S_><<<dim3(C, ns), 256, lds, s>>>(arg, dout, S_ ? ysel : y, cf, g, p_g, p_x, B, C, \
+    maxpool3_bwd_prep_kernel<V_, S_><<<dim3(C, ns), 256, lds, s>>>(arg, dout, dout2, S_ ? ysel : y, cf, g, p_g, p_x, B, C, \
                                                                    H, W, OH, OW, bps)
     if (W % 4 == 0) {
         if (ysel) PCX_MPB(4, true);

@@ -784,7 +784,8 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
         int acc = 0;
         // identity shortcut: the block input receives g directly -- for block 0 of the fused stem the
         // stem's pooled backward adds it while loading (no copy, no accumulating data gradient)
-        const bool sc_in_stem = i == 0 && d.stem_fused && d.residual && !k.sc;
+        const bool sc_in_stem = i == 0 && d.residual && !k.sc &&
+                                (d.stem_fused || maxpool3_bwd_prep_fits(d.H0, d.W0, d.H1, d.W1));
         if (d.residual && !k.sc && !sc_in_stem) {
             RC(hip_status_ok(hipMemcpyAsync(da, g, (size_t)B * k.cout * P2 * 4, hipMemcpyDeviceToDevice, s),
                              "copy shortcut grad"));
@@ -845,7 +846,7 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
         {
             Scope sc(&p.prof, s, "maxpool_bwd");
             RC(launch_maxpool3_bwd_prep(c.w<uint8_t>(d.mparg), dout, c.w<float>(d.y0), nullptr, c.w<float4>(d.cf0), dz0,
-                                        p_g, p_x, B, C0, d.H0, d.W0, d.H1, d.W1, &ns, s));
+                                        p_g, p_x, B, C0, d.H0, d.W0, d.H1, d.W1, &ns, s, dout2));
         }
         RC(bn_bwd(c, C0, ns, p_g, p_x, P[2], c.w<float4>(d.cf0), G[2], G[3], c.w<float4>(d.cfb0), (double)B * P0));
     } else {

@@ -409,9 +409,10 @@ int launch_maxpool3_bwd(const uint8_t* arg, const float* dout, float* dz, int B,
 // The BN input comes from the y plane, or (ysel != nullptr, y unused) from the pooled plane of the
 // selected taps' inputs (the fused stem, which keeps no y plane).
 bool maxpool3_bwd_prep_fits(int H, int W, int OH, int OW);
+// dout2 (optional): a second pooled gradient added to dout (block 0's identity-shortcut gradient)
 int launch_maxpool3_bwd_prep(const uint8_t* arg, const float* dout, const float* y, const float* ysel, const float4* cf, float* g,
                              float* p_g, float* p_x, int B, int C, int H, int W, int OH, int OW, int* nslice,
-                             hipStream_t s);
+                             hipStream_t s, const float* dout2 = nullptr);
 int launch_fill_cf(float4* cf, int C, float4 v, hipStream_t s);
 
 }  // namespace pcx
