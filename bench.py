@@ -125,7 +125,7 @@ def deep_kernel_costs(B, F, T, bf16=False, D=128):
     H1, W1 = (H0 - 1) // 2 + 1, (W0 - 1) // 2 + 1
     C0 = DEEP_DIMS[0]
     out["maxpool_fwd"] = (0, B * C0 * (4 * H0 * W0 + 5 * H1 * W1))            # y0 -> a0 + first-max tap
-    out["maxpool_bwd"] = (0, B * C0 * (4 * H0 * W0 * 2 + 5 * H1 * W1))        # tap, d a0, y0 -> dz0
+    out["maxpool_bwd"] = (0, B * C0 * (4 * H0 * W0 * 2 + 9 * H1 * W1))        # tap, d a0 + shortcut grad, y0 -> dz0
     if bf16 and C0 == 64 and W0 <= 256:
         # fused stem (conv.hip stem_pool_kernel / stem_wgrad_rc_kernel): y0 is recomputed, never stored;
         # the stem GEMM's FLOPs count once per recomputation
