@@ -186,9 +186,35 @@ def stalls(csv_path, out_json):
     print(json.dumps(res, indent=1, sort_keys=True))
 
 
+def label_stalls(rename_trace, csv_path, out_json, key):
+    """Per plan label: median per launch of every counter of one --pmc pass (dispatches mapped to the
+    labels of a rename trace, as `labelled`), plus the wait / active fractions of wave cycles."""
+    names = sorted({r["Counter_Name"] for r in _rows(csv_path)})
+    res = defaultdict(dict)
+    for c in names:
+        for lab, vals in labelled(rename_trace, csv_path, c).items():
+            res[lab][c] = sorted(vals)[len(vals) // 2]
+    for lab, d in res.items():
+        if d.get("SQ_WAVE_CYCLES"):
+            for c in list(d):
+                if c.startswith("SQ_WAIT") or c.startswith("SQ_ACTIVE"):
+                    d[c + "/WAVE_CYCLES"] = round(d[c] / d["SQ_WAVE_CYCLES"], 4)
+    try:
+        with open(out_json) as fi:
+            allres = json.load(fi)
+    except (OSError, ValueError):
+        allres = {}
+    allres[key] = res
+    with open(out_json, "w") as fo:
+        json.dump(allres, fo, indent=1, sort_keys=True)
+    print(json.dumps(res, indent=1, sort_keys=True))
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "--stalls":
         stalls(sys.argv[2], sys.argv[3])
+    elif sys.argv[1] == "--label-stalls":
+        label_stalls(*sys.argv[2:6])
     elif sys.argv[1] == "--labels":
         main_labelled(*sys.argv[2:6])
     else:
