@@ -1,0 +1,190 @@
+"""Algorithmic cost model of the train step:
+FLOPs and HBM bytes per kernel launch and per step for cnn_small and cnn_deep, and the MI355X
+peaks they are priced against.  Used by bench.py (roofline of the dominant kernel, step
+fractions) and by ContrastiveTrainer's perf.json."""
+
+FP32_PEAK_TFLOPS = 157.3     # MI355X vector == matrix fp32 (MI355X_MICROARCH.md)
+BF16_PEAK_TFLOPS = 2500.0    # dense bf16 MFMA (MI355X_MICROARCH.md: ~2.5 PF dense, no sparsity)
+HBM_PEAK_GBS = 8000.0        # HBM3E spec
+DEEP_DIMS = [64, 128, 256, 512]
+
+
+def small_layers(B, F, T):
+    """(label suffix, cin, cout, H, W, src bytes/sample, pooled) for the six convs of cnn_small."""
+    H1, W1 = F, T
+    H3, W3 = H1 // 2, W1 // 2
+    H5, W5 = H3 // 2, W3 // 2
+    return [(1, 1, 32, H1, W1), (2, 32, 32, H1, W1), (3, 32, 64, H3, W3), (4, 64, 64, H3, W3),
+            (5, 64, 128, H5, W5), (6, 128, 128, H5, W5)]
+
+
+def kernel_costs(B, F, T, D=128):
+    """Algorithmic FLOPs and HBM bytes of ONE launch of each profiled kernel label.
+    FLOPs: 2*MACs of the dense contraction.  Bytes: each input tensor read once, each output
+    written once, fp32 (halo / prologue re-reads are not algorithmic)."""
+    L = {l: (ci, co, h, w) for l, ci, co, h, w in small_layers(B, F, T)}
+    src_res = {1: (F, T), 2: (F, T), 3: (F, T), 4: (F // 2, T // 2), 5: (F // 2, T // 2), 6: (F // 4, T // 4)}
+    out = {}
+    for l, (ci, co, h, w) in L.items():
+        macs = B * h * w * co * ci * 9
+        sh, sw = src_res[l]
+        y_out = 4 * B * co * h * w
+        x_in = 4 * B * ci * sh * sw
+        if l == 1:
+            out["conv1_fwd_L1"] = (2 * macs, 4 * B * F * T + y_out)
+            out["wgrad_L1"] = (2 * macs, 2 * y_out + 4 * B * F * T)
+            continue
+        out[f"conv_fwd_L{l}"] = (2 * macs, x_in + y_out)
+        # dgrad: reads dz_l and y_l, reads y_{l-1} (epilogue), writes dz_{l-1}
+        out[f"conv_dgrad_L{l}"] = (2 * macs, 2 * y_out + 2 * x_in)
+        # wgrad: reads dz_l, y_l and the forward input source
+        out[f"wgrad_L{l}"] = (2 * macs, 2 * y_out + x_in)
+    # elementwise / head passes (bytes: each tensor read once, each output written once)
+    H1, W1, H3, W3, H5, W5 = F, T, F // 2, T // 2, F // 4, T // 4
+    out["bn_relu_pool_L3"] = (0, 4 * B * 32 * (H1 * W1 + H3 * W3))
+    out["bn_relu_pool_L5"] = (0, 4 * B * 64 * (H3 * W3 + H5 * W5))
+    out["head_pool_fwd"] = (4 * B * 128 * H5 * W5, 4 * B * (128 * H5 * W5 + 128 + H5 * W5))
+    out["head_pool_bwd"] = (6 * B * 128 * H5 * W5, 4 * B * (2 * 128 * H5 * W5 + 128 + H5 * W5))
+    out["proj_fwd"] = (2 * B * 128 * D, 4 * B * (128 + 2 * D))
+    out["proj_bwd"] = (4 * B * 128 * D, 4 * B * (2 * 128 + 3 * D))
+    return out
+
+
+def executed_fraction(label, T):
+    """Multiplies executed per algorithmic (direct-conv) multiply for cnn_small's kernels: the 3x3
+    forward / data-gradient convs run Winograd F(2x2,3x3) at W >= 31 (conv_wino.hip), the 3x3
+    weight gradients at even W (wgrad_wino.hip): 16 multiplies per 2x2 outputs instead of 36."""
+    widths = {2: T, 3: T // 2, 4: T // 2, 5: T // 4, 6: T // 4}
+    for pre in ("conv_fwd_L", "conv_dgrad_L"):
+        if label.startswith(pre):
+            return 4 / 9 if widths.get(int(label[len(pre):]), 0) >= 31 else 1.0
+    if label.startswith("wgrad_L") and label[7:].isdigit() and int(label[7:]) >= 2:
+        return 4 / 9 if widths[int(label[7:])] % 2 == 0 else 1.0
+    return 1.0
+
+
+def deep_convs(F, T, h=DEEP_DIMS):
+    """(fwd label, wgrad label, dgrad label or None, cin, cout, k, stride, IH, IW, OH, OW) of every
+    conv of cnn_deep, labelled as deep.hip profiles them."""
+    out = [("conv_fwd_L0", "wgrad_L0", None, 1, h[0], 7, 1, F, T, F, T)]
+    H, W, cin = (F - 1) // 2 + 1, (T - 1) // 2 + 1, h[0]
+    for i, co in enumerate(h):
+        s = 1 if i == 0 else 2
+        Ho, Wo = (H - 1) // s + 1, (W - 1) // s + 1
+        L = 2 * i + 1
+        out.append((f"conv_fwd_L{L}", f"wgrad_L{L}", f"conv_dgrad_L{L}", cin, co, 3, s, H, W, Ho, Wo))
+        out.append((f"conv_fwd_L{L + 1}", f"wgrad_L{L + 1}", f"conv_dgrad_L{L + 1}", co, co, 3, 1, Ho, Wo, Ho, Wo))
+        if s != 1 or cin != co:
+            out.append((f"shortcut_fwd_L{i}", f"wgrad_L{100 + i}", f"conv_dgrad_L{100 + i}", cin, co, 1, s, H, W,
+                        Ho, Wo))
+        H, W, cin = Ho, Wo, co
+    return out
+
+
+def deep_kernel_costs(B, F, T, bf16=False, D=128):
+    """Algorithmic FLOPs and bytes of one launch of every profiled cnn_deep label (convs: both
+    operands read once, the output written once, float32; elementwise passes: each tensor read
+    once, each output written once, float32 activations, bf16 channel-last images 2 B/element)."""
+    out = {}
+    for fl, wl, dl, ci, co, k, s, IH, IW, OH, OW in deep_convs(F, T):
+        macs = B * OH * OW * co * ci * k * k
+        x_b, y_b = 4 * B * ci * IH * IW, 4 * B * co * OH * OW
+        out[fl] = (2 * macs, x_b + y_b)
+        out[wl] = (2 * macs, x_b + y_b)
+        if dl:
+            out[dl] = (2 * macs, x_b + y_b)
+    img = 2 if bf16 else 4
+    H0, W0 = F, T
+    H1, W1 = (H0 - 1) // 2 + 1, (W0 - 1) // 2 + 1
+    C0 = DEEP_DIMS[0]
+    out["maxpool_fwd"] = (0, B * C0 * (4 * H0 * W0 + 5 * H1 * W1))            # y0 -> a0 + first-max tap
+    out["maxpool_bwd"] = (0, B * C0 * (4 * H0 * W0 * 2 + 9 * H1 * W1))        # tap, d a0 + shortcut grad, y0 -> dz0
+    if bf16 and C0 == 64 and W0 <= 256:
+        # fused stem (conv.hip stem_pool_kernel / stem_wgrad_rc_kernel): y0 is recomputed, never stored;
+        # the stem GEMM's FLOPs count once per recomputation
+        stem = 2 * B * H0 * W0 * C0 * 49
+        xb = 4 * B * H0 * W0
+        out["conv_fwd_L0"] = (stem, xb)                                        # BN0 statistics only
+        # pooled NHWC y0 at the tap (4 B) + tap (1 B) + block 0's NHWC image; no a0 plane
+        out["maxpool_fwd"] = (stem, xb + B * C0 * (5 * H1 * W1 + img * (H1 + 2) * (W1 + 2)))
+        # d a0 + block 0's shortcut gradient + tap + y0 at the tap -> dz0 in bf16
+        out["maxpool_bwd"] = (0, B * C0 * (13 * H1 * W1 + 2 * H0 * W0))
+        out["wgrad_L0"] = (2 * stem, xb + 2 * B * C0 * H0 * W0)                # bf16 dz0 + x (recompute + gradient)
+    out["bwd_prep_L0"] = (0, B * C0 * 4 * H0 * W0 * 3)
+    H, W, cin = H1, W1, C0
+    for i, co in enumerate(DEEP_DIMS):
+        st = 1 if i == 0 else 2
+        Ho, Wo = (H - 1) // st + 1, (W - 1) // st + 1
+        L, Pi, Po = 2 * i + 1, H * W, Ho * Wo
+        sc = st != 1 or cin != co
+        a_in, y = 4 * B * cin * Pi, 4 * B * co * Po
+        out[f"to_nhwc_L{L}"] = (0, a_in + img * B * cin * (H + 2) * (W + 2))
+        out[f"bn_act_L{L}"] = (0, y + img * B * co * Po)                         # y1 -> d1
+        # bf16 (residual): the outputs of blocks 0-2 leave a byte ReLU mask instead of the float32 plane
+        m8 = bf16 and i < 3
+        out[f"bn_act_L{L + 1}"] = (0, 2 * y + (y // 4 if m8 else y) + img * B * co * Po)  # y2 + residual -> out / mask (+ image)
+        out[f"chan_stats_L{L}"] = (0, y)
+        out[f"chan_stats_L{L + 1}"] = (0, y)
+        out[f"chan_stats_L{100 + i}"] = (0, y)
+        out[f"bwd_prep_L{L + 1}"] = (0, y * (4 if sc else 3) + y - (3 * y // 4 if m8 else 0))  # d, mask, y2 (, ysc) -> g
+        out[f"bwd_prep_L{L}"] = (0, (2 if bf16 else 3) * y)                      # d, y1 (-> d; bf16: sums only)
+        out[f"dy_nhwc_L{L + 1}"] = (0, 2 * y + img * B * co * Po)
+        out[f"dy_nhwc_L{L}"] = (0, 2 * y + img * B * co * Po)
+        out[f"bn_bwd_apply_L{L + 1}"] = (0, 3 * y)
+        out[f"bn_bwd_apply_L{L}"] = (0, 3 * y)
+        out[f"dgrad_interleave_L{L}"] = (0, 2 * a_in)
+        H, W, cin = Ho, Wo, co
+    C4, P4 = DEEP_DIMS[-1], H * W
+    out["head_pool_fwd"] = (4 * B * C4 * P4, 4 * B * (C4 * P4 + C4 + P4))
+    out["head_pool_bwd"] = (6 * B * C4 * P4, 4 * B * (2 * C4 * P4 + C4 + P4))
+    out["proj_fwd"] = (2 * B * C4 * D, 4 * B * (C4 + 2 * D))
+    out["proj_bwd"] = (4 * B * C4 * D, 4 * B * (2 * C4 + 3 * D))
+    return out
+
+
+def deep_step_cost(B, F, T, D=128, e=4, h=DEEP_DIMS, nparams=4968833):
+    """SURVEY 8(d)'s cnn_deep model: input read twice, every conv output written / read / re-read /
+    gradient written / read (5 passes), the same for the init max-pool output and every block
+    output; + 40 B per parameter and 12 B*D for SupCon (122.37 GB / step at B = 4096, T = 200)."""
+    flops, act = 0, e * 2 * B * F * T
+    for fl, wl, dl, ci, co, k, s, IH, IW, OH, OW in deep_convs(F, T, h):
+        macs = B * OH * OW * co * ci * k * k
+        flops += 2 * macs * (3 if dl else 2)
+        act += e * 5 * B * co * OH * OW
+    H, W = (F - 1) // 2 + 1, (T - 1) // 2 + 1
+    act += e * 5 * B * h[0] * H * W  # init max-pool output
+    for i, co in enumerate(h):
+        s = 1 if i == 0 else 2
+        H, W = (H - 1) // s + 1, (W - 1) // s + 1
+        act += e * 5 * B * co * H * W        # block output
+    flops += 4 * B * B * D + 3 * 2 * B * h[-1] * D
+    return flops, act + 40 * nparams + 12 * B * D
+
+
+def step_cost(B, F, T, D=128):
+    """Algorithmic FLOPs and bytes of one whole train step."""
+    flops = 0
+    act_bytes = 4 * 2 * B * F * T  # input read twice
+    for l, ci, co, h, w in small_layers(B, F, T):
+        macs = B * h * w * co * ci * 9
+        flops += 2 * macs * (2 if l == 1 else 3)
+        act_bytes += 4 * 5 * B * co * h * w
+    flops += 4 * B * B * D + 3 * 2 * B * 128 * D
+    params = 304225
+    return flops, act_bytes + 40 * params + 12 * B * D
+
+
+def model_step_cost(model, B, F, T):
+    """(FLOPs, bytes, peak TFLOP/s) of one train step of `model` (a PhonemeNet / PhonemeNetDeep)
+    at per-rank batch B and input [B, 1, F, T] under this cost model, or None for other models."""
+    name = type(model).__name__
+    D = getattr(model, "embedding_dim", 128)
+    if name == "PhonemeNet":
+        fl, by = step_cost(B, F, T, D)
+        return fl, by, FP32_PEAK_TFLOPS
+    if name == "PhonemeNetDeep":
+        bf16 = getattr(model, "precision", "fp32") == "bf16"
+        n = sum(p.numel() for p in model.parameters())
+        fl, by = deep_step_cost(B, F, T, D, e=2 if bf16 else 4, h=list(model.hidden_dims), nparams=n)
+        return fl, by, BF16_PEAK_TFLOPS if bf16 else FP32_PEAK_TFLOPS
+    return None

@@ -185,12 +185,16 @@ int build_deep(Plan& p) {
         plan_routed(k.cout, k.cout, k.Ho, k.Wo, &k.dma2, &k.w32_2, &k.wg2, &k.nblk2, &k.ww2, &k.wwa2);
         cin = k.cout; H = k.Ho; W = k.Wo;
     }
-    // block outputs read only as a ReLU mask (the next block reads its NHWC image): bytes.  Even widths
-    // only: with odd rows (the to_nhwc_kernel<1, ACT> form) and no float32 copy the next block's forward
-    // came out wrong (T = 200 block 2, T = 100 reduced-width block 1; measured, not yet explained), so
-    // those outputs keep their float32 plane
+    // block outputs read only as a ReLU mask (the next block reads its NHWC image): bytes, at any width.
+    // (Round 3 gated this on even widths after wrong forwards at T = 200 block 2 / T = 100 block 1 of
+    // reduced-width nets.  The cause: in those nets block i is not channel-last but block i + 1 is, and
+    // block i + 1's forward re-copied its NHWC input from block i's float32 output -- unwritten under the
+    // byte mask -- over the image block i's activation had just written.  The even-width gate only
+    // happened to exclude those cases.  The copy now runs only where nothing wrote the image (block 0
+    // without the fused stem), and the forward / backward hand nullptr, never the unwritten plane, to
+    // every consumer of a byte-masked output: the conv / shortcut GEMMs then must take the NHWC image.)
     for (int i = 0; i < 3; ++i)
-        if (d.residual && d.blk[i + 1].cn && d.blk[i].Wo % 2 == 0)
+        if (d.residual && d.blk[i + 1].cn)
             d.blk[i].m8 = p.carve("relu_mask8", (size_t)planes(B, d.blk[i].cout, d.blk[i].Ho, d.blk[i].Wo));
     d.g = p.carve("g", gmax);
     d.dyA = p.carve("dyA", gmax);
@@ -267,11 +271,19 @@ struct Ctx {
     T* w(size_t off) const { return at<T>(ws, off); }
 };
 
+// float32 output plane of block i, or nullptr when only its byte ReLU mask (and the next block's NHWC
+// image) is stored: the plane is then never written, and no consumer may be handed it
+const float* block_out(const Ctx& c, int i) {
+    const DeepBlock& k = c.d.blk[i];
+    return k.m8 ? nullptr : c.w<float>(k.out);
+}
+
 // forward conv (raw output, no bias) + train-mode statistics + BN finalise -> cf
 int conv_bn_fwd(const Ctx& c, const char* label, int layer, const float* x, int cin, int IH, int IW, int k, int stride,
                 int pad, const float* wgt, float* y, int cout, int OH, int OW, const float* gamma, const float* beta,
                 const float* bias, float* rmean, float* rvar, int64_t* nbt, int train, float4* cf, int dma_nblk = 0,
                 const void* xn = nullptr) {
+    PCX_CHECK_ARG(x || xn, "deep plan: %s of layer %d has no input (float32 plane or NHWC image)", label, layer);
     float* part = c.w<float>(c.d.stat);
     int ns = 1;
     BnFwdArgs f{};
@@ -336,6 +348,7 @@ int conv_wgrad(const Ctx& c, int layer, const float* x, int cin, int IH, int IW,
                const float* dy, int cout, int OH, int OW, float* gw, float* gb, const WgradArgs* w32 = nullptr,
                const float* bn_g = nullptr, const float* bn_y = nullptr, const float4* bn_cf = nullptr,
                const void* xn = nullptr, const void* dyn = nullptr, const WinoWgradArgs* ww = nullptr) {
+    PCX_CHECK_ARG(x || (xn && dyn), "deep plan: weight gradient of layer %d has no input (plane or NHWC image)", layer);
     if (ww) {  // stride-1 3x3, even width: Winograd weight gradient, BN backward in its staging (dy written)
         WinoWgradArgs w = *ww;
         w.B = c.p.B; w.H = OH; w.W = OW; w.cin = cin; w.cout = cout;
@@ -499,8 +512,9 @@ int deep_forward(const Plan& p, const float* const* P, float* const* bnstat, int
         const int q = k.pidx, L = 2 * i + 1;
         const void* an = k.cn ? c.w<void>(k.an) : nullptr;
         const void* d1n = k.cn ? c.w<void>(k.d1n) : nullptr;
-        // (otherwise written by the previous block's activation, or for block 0 by the fused stem pool)
-        if (k.cn && (i == 0 ? !d.stem_fused : !d.blk[i - 1].cn)) {
+        // (otherwise written by the previous block's activation -- whenever this block is channel-last,
+        // whatever the previous block's engine -- or for block 0 by the fused stem pool)
+        if (k.cn && i == 0 && !d.stem_fused) {
             Scope sc(&p.prof, s, "to_nhwc", L);
             RC(launch_to_nhwc(nhwc_args(NHWC_COPY, B, k.cin, k.Hi, k.Wi, a, c.w<void>(k.an)), s));
         }
@@ -532,6 +546,7 @@ int deep_forward(const Plan& p, const float* const* P, float* const* bnstat, int
             res = c.w<float>(k.ysc);
             rcf = c.w<float4>(k.cfsc);
         } else if (d.residual) {
+            PCX_CHECK_ARG(a, "deep plan: identity residual of block %d reads a byte-masked output", i);
             res = a;
         }
         // fused stem: block 0's identity residual a0 = relu(BN0(y0 at the tap)) from the pooled NHWC y0
@@ -558,7 +573,7 @@ int deep_forward(const Plan& p, const float* const* P, float* const* bnstat, int
                                  c.w<float>(k.out), B, k.cout, P2, s));
             }
         }
-        a = c.w<float>(k.out);
+        a = block_out(c, i);  // nullptr under the byte mask: the next block reads only its NHWC image
     }
     // head on the (already non-negative) trunk output: identity BN coefficients
     RC(launch_fill_cf(c.w<float4>(d.ident), d.h[3], make_float4(1.f, 0.f, 0.f, 1.f), s));
@@ -674,7 +689,7 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
         const int q = k.pidx, L = 2 * i + 1;
         const int64_t P2 = (int64_t)k.Ho * k.Wo;
         const double count = (double)B * P2;
-        const float* a_in = i == 0 ? c.w<float>(d.a0) : c.w<float>(d.blk[i - 1].out);
+        const float* a_in = i == 0 ? c.w<float>(d.a0) : block_out(c, i - 1);  // nullptr: byte-masked
         float* g = c.w<float>(d.g);
         float* dy2 = c.w<float>(d.dyA);
         float* dysc = c.w<float>(d.dyB);
@@ -691,7 +706,7 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
             }
             if (d.residual) {
                 b.mask_mode = masked ? MASK_NONE : (k.m8 ? MASK_OUT8 : MASK_OUT);
-                b.mask_src = c.w<float>(k.out);
+                b.mask_src = block_out(c, i);
                 b.mask8 = k.m8 ? c.w<uint8_t>(k.m8) : nullptr;
             } else {
                 b.mask_mode = MASK_BN;

@@ -161,24 +161,29 @@ class WaveformStore:
     """Mono clips resident on one device, with their integer labels.
 
     Either fixed-length clips `waves` [N, S] (synthetic stores, validation, small train sets), or
-    for a train set of >= 500 files the uncropped clips `raw` [N, L_max] with their `lengths`: the
-    reference reloads and re-crops such a set on every __getitem__ (dataset.py:57-59,113-145), so
-    `clips(indices, epoch)` draws a fresh crop / left pad per clip and epoch on the device
-    (crop_shifts).  Below 500 files the reference caches the first crop, and so does this store
-    (drawn once, at load)."""
+    for a train set of >= 500 files the uncropped clips stored ragged -- one concatenated 1-D buffer
+    `flat` with per-clip `offsets` / `lengths` (host arrays), so one long outlier clip costs its own
+    length, not N times it: the reference reloads and re-crops such a set on every __getitem__
+    (dataset.py:57-59,113-145), so `clips(indices, epoch)` draws a fresh crop / left pad per clip
+    and epoch on the device (crop_shifts) and gathers it as flat[offset + j + shift].  Below 500
+    files the reference caches the first crop, and so does this store (drawn once, at load)."""
 
     def __init__(self, waves: Optional[torch.Tensor], labels: Sequence[int], metadata: Optional[List[Dict]] = None,
-                 raw: Optional[torch.Tensor] = None, lengths: Optional[Sequence[int]] = None,
+                 flat: Optional[torch.Tensor] = None, lengths: Optional[Sequence[int]] = None,
                  max_samples: Optional[int] = None, seed: int = 0):
-        if raw is None:
+        if flat is None:
             if waves is None or waves.dim() != 2:
                 raise ValueError(f"waveforms must be [N, samples], got {None if waves is None else tuple(waves.shape)}")
             self.waves = waves.contiguous().float()
             self.max_samples = self.waves.shape[1]
         else:
             self.waves = None
-            self.raw = raw.contiguous().float()
+            self.flat = flat.contiguous().float().reshape(-1)
             self.lengths = np.asarray(lengths, np.int64)
+            self.offsets = np.concatenate([[0], np.cumsum(self.lengths)[:-1]]).astype(np.int64)
+            if int(self.lengths.sum()) != self.flat.numel():
+                raise ValueError(f"ragged store: {self.flat.numel()} samples for clip lengths summing to "
+                                 f"{int(self.lengths.sum())}")
             self.max_samples = int(max_samples)
             self.seed = int(seed)
         self.labels = [int(v) for v in labels]
@@ -191,18 +196,30 @@ class WaveformStore:
     def recrops(self) -> bool:
         return self.waves is None
 
-    def clips(self, indices: torch.Tensor, epoch: int = 0) -> torch.Tensor:
-        """[n, max_samples] clips of `indices` (a device LongTensor) for this epoch."""
+    @property
+    def device(self) -> torch.device:
+        return (self.waves if self.waves is not None else self.flat).device
+
+    def clips(self, indices, epoch: int = 0) -> torch.Tensor:
+        """[n, max_samples] clips of `indices` for this epoch.  `indices` is a host sequence of
+        clip numbers (the loaders pass the sampler's list: no device round trip) or a LongTensor."""
+        if torch.is_tensor(indices):
+            idx_np = indices.detach().cpu().numpy().astype(np.int64)
+        else:
+            idx_np = np.asarray(indices, np.int64).reshape(-1)
+        dev = self.device
         if self.waves is not None:
-            return self.waves.index_select(0, indices)
-        idx_np = indices.cpu().numpy()
-        shift = torch.as_tensor(crop_shifts(self.lengths[idx_np], self.max_samples, self.seed, epoch, idx_np),
-                                device=self.raw.device)
-        ln = torch.as_tensor(self.lengths[idx_np], device=self.raw.device)
-        src = torch.arange(self.max_samples, device=self.raw.device)[None, :] + shift[:, None]
+            return self.waves.index_select(0, torch.as_tensor(idx_np, device=dev))
+        ln_np = self.lengths[idx_np]
+        shift = torch.as_tensor(crop_shifts(ln_np, self.max_samples, self.seed, epoch, idx_np), device=dev)
+        ln = torch.as_tensor(ln_np, device=dev)
+        base = torch.as_tensor(self.offsets[idx_np], device=dev)
+        src = torch.arange(self.max_samples, device=dev)[None, :] + shift[:, None]
         valid = (src >= 0) & (src < ln[:, None])
-        rows = self.raw.index_select(0, indices)
-        out = rows.gather(1, src.clamp(0, self.raw.shape[1] - 1))
+        if self.flat.numel() == 0:
+            return torch.zeros(len(idx_np), self.max_samples, device=dev)
+        gidx = (base[:, None] + torch.minimum(src.clamp(min=0), (ln[:, None] - 1).clamp(min=0)))
+        out = self.flat[gidx.clamp(0, self.flat.numel() - 1)]
         return out * valid
 
     @staticmethod
@@ -229,11 +246,8 @@ class WaveformStore:
         every epoch draws new crops (`clips`)."""
         mono = [cls._load_mono(f, target_sr) for f in file_paths]
         if mode == "train" and len(mono) >= 500:
-            lmax = max(max_samples, max((len(m) for m in mono), default=0))
-            raw = np.zeros((len(mono), lmax), np.float32)
-            for i, m in enumerate(mono):
-                raw[i, :len(m)] = m
-            return cls(None, labels, metadata, raw=torch.from_numpy(raw).to(device),
+            flat = np.concatenate(mono).astype(np.float32) if mono else np.zeros(0, np.float32)
+            return cls(None, labels, metadata, flat=torch.from_numpy(flat).to(device),
                        lengths=[len(m) for m in mono], max_samples=max_samples, seed=seed)
         rng = random.Random(int(seed))
         out = np.zeros((len(mono), max_samples), np.float32)
@@ -270,10 +284,10 @@ class WaveformStore:
         if self.waves is not None:
             idx = torch.as_tensor(indices, dtype=torch.long, device=self.waves.device)
             return WaveformStore(self.waves.index_select(0, idx), labels, meta)
-        idx = torch.as_tensor(indices, dtype=torch.long, device=self.raw.device)
-        return WaveformStore(None, labels, meta, raw=self.raw.index_select(0, idx),
-                             lengths=self.lengths[np.asarray(indices, np.int64)], max_samples=self.max_samples,
-                             seed=self.seed)
+        parts = [self.flat[int(self.offsets[i]):int(self.offsets[i] + self.lengths[i])] for i in indices]
+        flat = torch.cat(parts) if parts else self.flat[:0]
+        return WaveformStore(None, labels, meta, flat=flat, lengths=self.lengths[np.asarray(indices, np.int64)],
+                             max_samples=self.max_samples, seed=self.seed)
 
 
 # ----------------------------------------------------------------------------- batching
@@ -315,21 +329,27 @@ class GpuContrastiveBatches:
     def __init__(self, store: WaveformStore, batch_sampler, builder: GpuViewBuilder):
         self.store, self.batch_sampler, self.builder = store, batch_sampler, builder
         self.dataset = _Sized(len(store), store.labels)
-        self.epoch = 0  # counts passes: the re-cropping store draws new crops per pass
+        self.epoch = 0  # crop epoch of the next pass (set_epoch; advances by itself as a fallback)
+
+    def set_epoch(self, epoch: int) -> None:
+        """Crop schedule of the next pass = (seed, epoch, clip), as DistributedSampler.set_epoch:
+        ContrastiveTrainer._train_epoch calls it with its current_epoch, so an extra pass (warm-up,
+        debug iteration) or a resumed run does not shift the crops."""
+        self.epoch = int(epoch)
 
     def __len__(self):
         return len(self.batch_sampler)
 
     def __iter__(self):
         store = self.store
-        dev = (store.waves if store.waves is not None else store.raw).device
+        dev = store.device
         epoch = self.epoch
         self.epoch += 1
         for idx in self.batch_sampler:
-            ix = torch.as_tensor([int(i) for i in idx], dtype=torch.long, device=dev)
-            views = self.builder(store.clips(ix, epoch), [int(i) for i in idx])
-            labels = torch.as_tensor([self.store.labels[int(i)] for i in idx], dtype=torch.long)
-            yield {"views": views, "label": labels, "index": ix}
+            idx = [int(i) for i in idx]
+            views = self.builder(store.clips(idx, epoch), idx)
+            labels = torch.as_tensor([self.store.labels[i] for i in idx], dtype=torch.long)
+            yield {"views": views, "label": labels, "index": torch.as_tensor(idx, dtype=torch.long)}
 
 
 class GpuEvalBatches:
@@ -344,9 +364,8 @@ class GpuEvalBatches:
 
     def __iter__(self):
         store = self.store
-        dev = (store.waves if store.waves is not None else store.raw).device
         for s in range(0, len(store), self.batch_size):
             idx = list(range(s, min(len(store), s + self.batch_size)))
-            views = self.builder(store.clips(torch.as_tensor(idx, dtype=torch.long, device=dev), 0), idx)
+            views = self.builder(store.clips(idx, 0), idx)
             labels = torch.as_tensor(self.store.labels[s:idx[-1] + 1], dtype=torch.long)
             yield {"views": views, "label": labels, "index": torch.as_tensor(idx)}

@@ -181,7 +181,6 @@ class GlobalSupervisedContrastiveLoss(SupervisedContrastiveLoss):
                  reduction: str = "mean", group=None):
         super().__init__(temperature, base_temperature, reduction)
         self.group = group
-        self._checked_sizes = set()
 
     def forward(self, features: torch.Tensor, labels: torch.Tensor,
                 mask: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -201,13 +200,16 @@ class GlobalSupervisedContrastiveLoss(SupervisedContrastiveLoss):
             labels = labels.reshape(-1)
             if labels.shape[0] != features.shape[0]:
                 raise ValueError("Num of labels does not match num of features")
+        # every rank must pass the same local batch size (the gathers below need it): checked on
+        # EVERY call by one 2-int collective that every rank issues, so the collectives line up
+        # whatever sizes the ranks see (a per-rank "already checked" cache would let one rank skip
+        # the collective while another enters it)
         n = features.shape[0]
-        if n not in self._checked_sizes:  # once per local batch size: no per-step host sync
-            ext = torch.tensor([n, -n], device=features.device)  # (max, -min) in one collective
-            dist.all_reduce(ext, op=dist.ReduceOp.MAX, group=self.group)
-            if ext[0].item() != -ext[1].item():
-                raise ValueError("global mode: every rank must pass the same local batch size")
-            self._checked_sizes.add(n)
+        ext = torch.tensor([n, -n], device=features.device)  # (max, -min) in one collective
+        dist.all_reduce(ext, op=dist.ReduceOp.MAX, group=self.group)
+        hi, neg_lo = ext.tolist()
+        if hi != -neg_lo:
+            raise ValueError(f"global mode: every rank must pass the same local batch size (got {-neg_lo}..{hi})")
         return _GlobalSupConFn.apply(features, labels, mask, self.temperature, self.base_temperature,
                                      self.reduction, self.group)
 

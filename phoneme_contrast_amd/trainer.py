@@ -13,9 +13,14 @@ MI355X additions (all optional, no behaviour change for a single process):
     each rank its own shard (scripts/train.py: ShardedBatchSampler).
   * FusedAdam fast path: when the optimizer is a FusedAdam the all-reduced flat buffer is passed
     straight to its single-kernel step.
+  * perf.json: per epoch the train steps' wall time, samples/s over all ranks
+    and the step's algorithmic TFLOP/s and GB/s with their fractions of the MI355X roofs
+    (phoneme_contrast_amd.costs), written next to metrics.json.
+  * loaders with `set_epoch` (GpuContrastiveBatches) get the trainer's epoch before each pass.
 """
 import json
 import logging
+import time
 from collections import defaultdict
 from pathlib import Path
 from typing import Any, Dict, Optional, Tuple
@@ -57,6 +62,7 @@ class ContrastiveTrainer:
         self.best_val_loss = float("inf")
         self.metrics_history = defaultdict(list)
         self.rank, self.world_size = ddp.world()
+        self.perf_history = []
 
     # ------------------------------------------------------------------ loop
     def train(self, num_epochs: int) -> None:
@@ -92,21 +98,29 @@ class ContrastiveTrainer:
 
     def _train_epoch(self) -> Dict[str, float]:
         self.model.train()
+        if hasattr(self.train_loader, "set_epoch"):
+            self.train_loader.set_epoch(self.current_epoch)
         total_loss, num_batches = 0.0, 0
         pbar = tqdm(self.train_loader, desc=f"Epoch {self.current_epoch + 1}",
                     disable=self.rank != 0)
+        step_s, samples, shape = 0.0, 0, None
         for batch in pbar:
             views, labels = self._prepare_batch(batch)
+            t0 = time.perf_counter()  # the train step proper (views already built): fwd, loss, bwd, step
             embeddings = self._forward_pass(views)
             loss = self.loss_fn(embeddings, labels)
             self.optimizer.zero_grad()
             loss.backward()
             self._reduce_clip_step()
-            total_loss += loss.item()
+            total_loss += loss.item()  # synchronises: the step has finished
+            step_s += time.perf_counter() - t0
+            samples += views.shape[0]
+            shape = tuple(views.shape)
             num_batches += 1
             self.global_step += 1
             if hasattr(pbar, "set_postfix"):
                 pbar.set_postfix({"loss": loss.item()})
+        self._record_perf(num_batches, samples, step_s, shape)
         if self.world_size > 1:
             # BatchNorm running statistics are per rank during the epoch (each rank's batches);
             # like DDP's broadcast_buffers, validation and checkpoints use rank 0's
@@ -226,6 +240,29 @@ class ContrastiveTrainer:
             return
         with open(self.output_dir / "metrics.json", "w") as f:
             json.dump(self.metrics_history, f, indent=2)
+        with open(self.output_dir / "perf.json", "w") as f:
+            json.dump({"world_size": self.world_size, "epochs": self.perf_history}, f, indent=2)
+
+    def _record_perf(self, steps: int, samples: int, seconds: float, shape) -> None:
+        """One perf.json entry per epoch: this rank's train-step time, samples/s
+        of all ranks (each rank runs the same number of equal-size steps), and the step's
+        algorithmic rates against the MI355X roofs for the per-rank batch shape."""
+        from .costs import HBM_PEAK_GBS, model_step_cost
+        rec = {"epoch": self.current_epoch, "steps": steps, "samples_per_rank": samples,
+               "step_seconds": round(seconds, 4)}
+        if steps and seconds > 0:
+            rec["ms_per_step"] = round(1000.0 * seconds / steps, 3)
+            rec["samples_per_s"] = round(self.world_size * samples / seconds, 1)
+            cost = model_step_cost(self.model, shape[0], shape[-2], shape[-1]) if shape and len(shape) == 4 else None
+            if cost is not None:
+                fl, by, peak = cost
+                per = seconds / steps
+                rec.update({"step_tflops": round(fl / per / 1e12, 2), "step_gbps": round(by / per / 1e9, 1),
+                            "mfma_fraction": round(fl / per / (peak * 1e12), 4),
+                            "hbm_fraction": round(by / per / (HBM_PEAK_GBS * 1e9), 4),
+                            "cost_model": "phoneme_contrast_amd/costs.py (SURVEY 8(d)); last batch shape "
+                                          f"{list(shape)}"})
+        self.perf_history.append(rec)
 
     def load_checkpoint(self, path: Path) -> None:
         # every entry is a tensor or a plain container, so the safe loader reads it (as

@@ -141,7 +141,7 @@ def main(cfg):
     logger.info("Starting training...")
     trainer.train(num_epochs=cfg.training.epochs)
     logger.info("Training complete!")
-    if world > 1:
+    if ddp.is_distributed():  # also the world-1 group PCX_DIST_FORCE_INIT=1 creates
         torch.distributed.destroy_process_group()
     return trainer
 

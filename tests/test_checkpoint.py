@@ -87,6 +87,25 @@ def test_metrics_json_layout():
                    "val_linear_accuracy": [0.5], "val_rf_accuracy": [0.25]}
 
 
+def test_perf_json_layout():
+    """perf.json: one record per epoch with samples/s and the step's roofline
+    fractions from phoneme_contrast_amd.costs (cnn_small at B = 4096, T = 200: 7.29 TFLOP, 73.7 GB)."""
+    m = model_registry.create("phoneme_cnn", {"embedding_dim": 128})
+    out = Path(tempfile.mkdtemp())
+    t = _trainer(m, torch.optim.SGD(m.parameters(), 0.1), None, {}, out)
+    t._record_perf(10, 40960, 0.5, (4096, 1, 40, 200))
+    t.current_epoch = 1
+    t._record_perf(0, 0, 0.0, None)
+    t._save_metrics()
+    got = json.loads((out / "perf.json").read_text())
+    e0 = got["epochs"][0]
+    assert got["world_size"] == 1 and len(got["epochs"]) == 2 and got["epochs"][1]["steps"] == 0
+    assert e0["ms_per_step"] == 50.0 and e0["samples_per_s"] == 81920.0
+    assert abs(e0["step_tflops"] - 7294498635776 / 0.05 / 1e12) < 0.01
+    assert abs(e0["mfma_fraction"] - 7294498635776 / 0.05 / 157.3e12) < 1e-4
+    assert 0 < e0["hbm_fraction"] < 1
+
+
 @pytest.mark.gpu
 def test_fused_adam_state_interchanges_with_torch_adam():
     """Checkpoint written with FusedAdam (GPU, one flat buffer) -> torch.optim.Adam on CPU: the

@@ -209,7 +209,9 @@ def test_large_train_store_recrops_per_epoch(tmp_path):
         _write(p, x, 16000, 2)
         paths.append(p)
     st = WaveformStore.from_files(paths, [0] * n, [{}] * n, 16000, ms, "train", torch.device("cpu"), seed=11)
-    assert st.recrops and tuple(st.raw.shape) == (n, int(lens.max()))
+    # ragged: one concatenated buffer, each clip at its own length (no [N, L_max] padding)
+    assert st.recrops and st.flat.dim() == 1 and st.flat.numel() == int(lens.sum())
+    assert list(st.offsets[:3]) == [0, lens[0], lens[0] + lens[1]]
     idx = torch.arange(n)
     c0, c1 = st.clips(idx, 0), st.clips(idx, 1)
     assert tuple(c0.shape) == (n, ms) and not torch.equal(c0, c1)
@@ -217,6 +219,10 @@ def test_large_train_store_recrops_per_epoch(tmp_path):
                                                     torch.device("cpu"), seed=11).clips(idx, 0))
     sub = torch.tensor([5, 17, 5])
     assert torch.equal(st.clips(sub, 1), c1[sub])  # a clip's draw does not depend on its batch
+    assert torch.equal(st.clips([5, 17, 5], 1), c1[sub])  # host index lists (the loaders' form)
+    part = st.subset([17, 5, 300])
+    assert part.flat.numel() == int(lens[[17, 5, 300]].sum())
+    assert torch.equal(part.flat[int(lens[17]):int(lens[17] + lens[5])], st.flat[st.offsets[5]:st.offsets[5] + lens[5]])
     sh = crop_shifts(lens, ms, 11, 1, np.arange(n))
     for i in range(n):
         mono = read_wav(paths[i])[0][0]
@@ -231,3 +237,27 @@ def test_large_train_store_recrops_per_epoch(tmp_path):
     big = np.full(20000, ms + 10)
     s = crop_shifts(big, ms, 1, 0, np.arange(20000))
     assert s.min() == 0 and s.max() == 10 and abs(s.mean() - 5) < 0.1
+
+
+def test_loader_epoch_follows_set_epoch(tmp_path):
+    """GpuContrastiveBatches draws the crops of the epoch it is told (set_epoch, as the trainer calls
+    it), not of how many passes ran: an extra pass does not shift the schedule."""
+    from phoneme_contrast_amd.data import GpuContrastiveBatches
+    n, ms = 8, 16
+    lens = np.array([30, 5, 40, 16, 17, 9, 50, 20])
+    flat = torch.arange(int(lens.sum()), dtype=torch.float32) + 1.0
+    st = WaveformStore(None, [i // 2 for i in range(n)], flat=flat, lengths=lens, max_samples=ms, seed=3)
+
+    class Ident:
+        def __call__(self, clips, idx):
+            return clips
+
+    ld = GpuContrastiveBatches(st, [[0, 1, 2, 3], [4, 5, 6, 7]], Ident())
+    ld.set_epoch(2)
+    e2 = [b["views"].clone() for b in ld]
+    list(ld)  # an extra pass (e.g. the classifier probe) ...
+    ld.set_epoch(2)
+    assert all(torch.equal(a, b["views"]) for a, b in zip(e2, ld))  # ... does not shift epoch 2
+    ld.set_epoch(3)
+    assert not all(torch.equal(a, b["views"]) for a, b in zip(e2, ld))
+    assert torch.equal(e2[0], st.clips([0, 1, 2, 3], 2))

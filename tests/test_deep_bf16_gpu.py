@@ -53,8 +53,12 @@ def _round_conv_operands(model):
             mod.forward = (lambda m: (lambda x: _Bf16Conv.apply(x, m.weight, m.bias, m.stride, m.padding)))(mod)
 
 
+# (True, 200, None) and (True, 100, [16, 32, ...]) store the odd-width outputs of blocks 2 / 1 as byte
+# ReLU masks under a channel-last next block (the round-3 failure cases); T = 201 is the real-data
+# width (32000-sample clips, reference src/datasets/dataset.py:50): 101 / 51 / 26 / 13-wide blocks
 @pytest.mark.parametrize("residual,T,dims,B", [(True, 200, None, 32), (False, 57, None, 32),
-                                               (True, 100, [16, 32, 64, 128], 32), (True, 100, FULL, 16)])
+                                               (True, 100, [16, 32, 64, 128], 32), (True, 100, FULL, 16),
+                                               (True, 201, FULL, 16), (True, 201, None, 32)])
 def test_deep_bf16_step(residual, T, dims, B):
     from oracle import torch_port as tp
     from phoneme_contrast_amd.losses import SupervisedContrastiveLoss

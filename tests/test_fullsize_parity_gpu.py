@@ -16,10 +16,17 @@ gradients are also compared with torch's own float32 evaluation of the same step
 arithmetic): cnn_deep's ReLU / max-pool kinks move float32 gradients by up to ~1e-2 of max|g| in
 any float32 evaluation (tools/wgrad_probe.py: the weight-gradient engines alone are at 1e-6 at these
 shapes), so each tensor passes within 3x the yardstick's largest error.  Every test prints its
-per-tensor max-abs and L2 errors (FULLSIZE lines).
+per-tensor max-abs and L2 errors (FULLSIZE lines) and records them, with the tolerances they were
+held to, in gpurun_out/fullsize_parity.json (PCX_FULLSIZE_JSON overrides the path; the round's copy
+is committed under profiles/).
+
+T = 201 is the real-data width (32000-sample clips, reference src/datasets/dataset.py:50): odd widths
+201 / 100 / 50 put the layer-2 weight gradient on the pixel-stream kernel (Winograd needs even W) and
+the Winograd forward / data gradient on 101-tile rows.
 """
 import gc
 import json
+import os
 
 import numpy as np
 import pytest
@@ -31,6 +38,20 @@ from oracle import torch_port as tp
 pytestmark = pytest.mark.gpu
 
 B, T = 4096, 200
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _record(name, rec):
+    path = os.environ.get("PCX_FULLSIZE_JSON", os.path.join(ROOT, "gpurun_out", "fullsize_parity.json"))
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    try:
+        with open(path) as f:
+            allrec = json.load(f)
+    except (OSError, ValueError):
+        allrec = {}
+    allrec[name] = rec
+    with open(path, "w") as f:
+        json.dump(allrec, f, indent=1, sort_keys=True)
 
 
 def _run_native(model, x, labels, masks, temperature):
@@ -91,11 +112,16 @@ def _compare(got, ref, emb_tol, name, yardstick=None):
            "grads_l2rel": {k: v[2] for k, v in errs.items()},
            "float32_yardstick_maxrel": {k: v[1] for k, v in ys.items()},
            "float32_yardstick_l2rel": {k: v[2] for k, v in ys.items()}}
-    print(f"\nFULLSIZE {name} " + json.dumps(rec, sort_keys=True))
-    assert de < emb_tol, de
-    assert dl < 1e-4, (got["loss"], ref["loss"])
     ymax = max((v[1] for v in ys.values() if v[0] == "rel"), default=0.0)
     yl2 = max((v[2] for v in ys.values() if v[0] == "rel"), default=0.0)
+    rec["tolerances"] = {"emb": emb_tol, "loss": 1e-4, "grad_maxrel": max(2e-3, 3.0 * ymax),
+                         "grad_l2rel": max(2e-3, 3.0 * yl2), "bn_fed_bias_abs": 1e-4}
+    rec["worst_grad_maxrel"] = max((v[1] for v in errs.values() if v[0] == "rel"), default=0.0)
+    rec["worst_grad_l2rel"] = max((v[2] for v in errs.values() if v[0] == "rel"), default=0.0)
+    print(f"\nFULLSIZE {name} " + json.dumps(rec, sort_keys=True))
+    _record(name, rec)
+    assert de < emb_tol, de
+    assert dl < 1e-4, (got["loss"], ref["loss"])
     bad = {}
     for k, (kind, err, l2) in errs.items():
         if kind == "abs":
@@ -108,9 +134,9 @@ def _compare(got, ref, emb_tol, name, yardstick=None):
         assert torch.allclose(got["state"][k], r, rtol=1e-5, atol=1e-6), k
 
 
-def _inputs(seed, chans):
+def _inputs(seed, chans, t=T):
     g = torch.Generator().manual_seed(seed)
-    x = torch.randn(B, 1, 40, T, generator=g)
+    x = torch.randn(B, 1, 40, t, generator=g)
     labels = torch.arange(B // 4).repeat_interleave(4)  # the sampler layout (2 clips x 2 views)
     masks = [(torch.rand(B, c, generator=g) >= 0.1).float() / 0.9 for c in chans]
     return x, labels, masks
@@ -121,19 +147,20 @@ def _free():
     torch.cuda.empty_cache()
 
 
-def test_cnn_small_b4096_matches_float64():
+@pytest.mark.parametrize("t", [200, 201])
+def test_cnn_small_b4096_matches_float64(t):
     from phoneme_contrast_amd.models import PhonemeNet
     torch.manual_seed(42)
     m = PhonemeNet({"embedding_dim": 128, "use_attention": True, "dropout_rate": 0.1})
     sd64 = {k: v.clone().double() if v.is_floating_point() else v.clone() for k, v in m.state_dict().items()}
     m = m.cuda().train()
-    x, labels, masks = _inputs(1234, (32, 64, 128))
+    x, labels, masks = _inputs(1234, (32, 64, 128), t)
     got = _run_native(m, x, labels, masks, 0.15)
     del m
     _free()
     ref = _run_oracle(sd64, x, labels, masks, 0.15)
     _free()
-    _compare(got, ref, 1e-5, "cnn_small")
+    _compare(got, ref, 1e-5, "cnn_small" if t == 200 else f"cnn_small_T{t}")
 
 
 def test_cnn_small_eval_first8_of_4096_equal_8_batch():

@@ -153,6 +153,8 @@ def test_scripts_train_main_two_synthetic_epochs():
     assert len(m["train_loss"]) == 2 and all(np.isfinite(m["train_loss"]))
     assert len(m["val_loss"]) == 2 and len(m["train_lr"]) == 2 and m["train_lr"][1] < m["train_lr"][0]
     assert (out / "checkpoints" / "checkpoint_final.pt").exists()
+    perf = json.load(open(out / "perf.json"))["epochs"]  # SURVEY section 5 record
+    assert len(perf) == 2 and all(e["samples_per_s"] > 0 and 0 < e["mfma_fraction"] < 1 for e in perf)
     # per-rank batch = classes x samples x views embeddings; 40 train classes // 8 = 5 batches
     assert len(tr.train_loader) == len(tr.train_loader.batch_sampler) >= 4
     assert tr.global_step == 2 * len(tr.train_loader)
