@@ -130,6 +130,29 @@ int launch_wgrad_wino(int pro, WinoWgradArgs a, hipStream_t s);
 // dW [cout][cin][3][3] = G^T (sum of the slices) G, float64, fixed order
 int launch_wgrad_wino_reduce(const float* part, int nslice, int cout, int cin, float* dw, hipStream_t s);
 
+// cnn_small layer-2 backward in one kernel (wgbd_wino.hip): Winograd weight gradient AND data gradient of
+// a 32 -> 32 stride-1 3x3 conv from one staging of dz, y (dy = BN backward) and y_prev (x = relu(BN_prev)),
+// with the producer's ReLU mask and BN backward sums in the data gradient's epilogue (EPI_BWD_RELU)
+struct WinoBwdArgs {
+    int B, H, W;           // 32 channels in and out; W % 4 == 0, W / 2 even
+    const float* dz;       // [B][32][H][W] gradient of this conv's BN output
+    const float* y;        // [B][32][H][W] raw conv output
+    const float4* cf_dy;   // {a, mb, mgi, mean}: dy = a (dz - mb - (y - mean) mgi)
+    const float* yp;       // [B][32][H][W] producer's raw output: x = relu(s yp + t)
+    const float4* cf_x;    // producer BN forward coefficients {s, t, mean, invstd}
+    const float* up;       // U' of the flipped weights: launch_wino_pack(w, up, 32, 32, 1)
+    float* part;           // weight-gradient partials [nslice][32][32][16] (launch_wgrad_wino_reduce)
+    float* dzp;            // out: [B][32][H][W] gradient of the producer BN's output
+    float* bn0;            // out: [32][nslice] sum dzp
+    float* bn1;            // out: [32][nslice] sum dzp * xhat_prev
+    int nseg, seg_t0[4], seg_S[4];  // column strips (tiles) of a tile row
+    int V, NIR, XCS;
+    size_t lds;
+    int ntask, per_slice, nslice;
+};
+bool wgbd_wino_geometry(int B, int H, int W, int C, WinoBwdArgs* a);
+int launch_wgbd_wino(WinoBwdArgs a, hipStream_t s);
+
 // PhonemeNetDeep 7x7 stem (Cin = 1, pad 3): direct forward + BN partials, weight gradient with the
 // BN backward of (dz, y) in its loads (conv.hip)
 struct StemArgs {

@@ -66,6 +66,13 @@ int build_small(Plan& p) {
             L.nblk = L.wino ? (int)wino_nblk(B, L.H, L.W, L.cin, L.cout)
                             : (int)std::max(conv3x3_nblk(B, L.H, L.W, L.cout), conv3x3_nblk(B, L.H, L.W, L.cin));
             L.wgw = wgrad_wino_geometry(B, L.H, L.W, L.cin, L.cout, &L.ww);
+            // layer 2 (32 -> 32 at full resolution, BN + ReLU input): both gradients in one pass
+            L.wgbd = l == 2 && !L.pooled_in && L.cin == 32 && L.cout == 32 && L.wino && getenv("PCX_NO_WGBD") == nullptr &&
+                     wgbd_wino_geometry(B, L.H, L.W, 32, &L.wb);
+            if (L.wgbd) {
+                wg = std::max(wg, (size_t)L.wb.nslice * 32 * 32 * 16);
+                stat = std::max(stat, (size_t)2 * 32 * L.wb.nslice);
+            }
             if (L.wgw) {
                 wg = std::max(wg, (size_t)L.ww.nslice * L.cout * L.cin * 16);
             } else {
@@ -324,6 +331,32 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
         const Layer& Lp = p.L[l - 1];
         // conv bias feeding a train-mode BN: exact gradient is zero (sum_b,h,w of BN-backward)
         RC(hip_status_ok(hipMemsetAsync(G[p_conv_b(l)], 0, L.cout * 4, s), "memset bias grad"));
+        if (L.wgbd) {  // ---- weight and data gradient in one pass (dy never materialised)
+            RC(launch_wino_pack(P[p_conv_w(l)], at<float>(ws, L.wud), L.cin, L.cout, 1, s));
+            WinoBwdArgs w = L.wb;
+            w.B = B; w.H = L.H; w.W = L.W;
+            w.dz = at<float>(ws, L.dz);
+            w.y = at<float>(ws, L.y);
+            w.cf_dy = at<float4>(ws, L.cfb);
+            w.yp = at<float>(ws, Lp.y);
+            w.cf_x = at<float4>(ws, Lp.cf);
+            w.up = at<float>(ws, L.wud);
+            w.part = wgp;
+            w.dzp = at<float>(ws, Lp.dz);
+            w.bn0 = part;
+            w.bn1 = part + (size_t)Lp.cout * w.nslice;
+            {
+                Scope sc(&p.prof, s, "wgbd", l);
+                RC(launch_wgbd_wino(w, s));
+            }
+            {
+                Scope sc(&p.prof, s, "wgrad_reduce", l);
+                RC(launch_wgrad_wino_reduce(wgp, w.nslice, L.cout, L.cin, G[p_conv_w(l)], s));
+            }
+            p.buckets.mark(p_conv_w(l), s);
+            RC(bwd_finalize(l - 1, w.nslice, (double)B * Lp.H * Lp.W));
+            continue;
+        }
         // ---- weight gradient
         if (L.wgw) {
             WinoWgradArgs w = L.ww;

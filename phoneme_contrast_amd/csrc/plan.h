@@ -134,6 +134,8 @@ struct Layer {  // one 3x3 conv of the trunk (L = 1..6)
     WgradArgs wg;          // weight-gradient geometry (pixel-stream kernel)
     bool wgw;              // weight gradient on the Winograd kernel (wgrad_wino.hip) instead
     WinoWgradArgs ww;
+    bool wgbd;             // weight AND data gradient in one kernel (wgbd_wino.hip: layer 2, W % 4 == 0)
+    WinoBwdArgs wb;
 };
 
 struct DeepPlan;  // deep.hip

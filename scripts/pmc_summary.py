@@ -194,11 +194,32 @@ def label_stalls(rename_trace, csv_path, out_json, key):
     for c in names:
         for lab, vals in labelled(rename_trace, csv_path, c).items():
             res[lab][c] = sorted(vals)[len(vals) // 2]
+    durs = defaultdict(list)  # per-label launch durations (ms) from the rename trace's timestamps
+    prev = None
+    for r in _rows(rename_trace):
+        lab = r["Kernel_Name"]
+        dt = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+        if lab == prev and not ("(" in lab or "<" in lab or "::" in lab):
+            durs[lab][-1] += dt
+        else:
+            durs[lab].append(dt)
+        prev = lab
     for lab, d in res.items():
         if d.get("SQ_WAVE_CYCLES"):
             for c in list(d):
                 if c.startswith("SQ_WAIT") or c.startswith("SQ_ACTIVE"):
                     d[c + "/WAVE_CYCLES"] = round(d[c] / d["SQ_WAVE_CYCLES"], 4)
+        if d.get("GRBM_GUI_ACTIVE") and "SQ_VALU_MFMA_BUSY_CYCLES" in d:
+            # MFMA busy per SIMD: 1024 SIMDs x (GRBM_GUI_ACTIVE / 8 XCDs); a value at 2^31 / 2^32 is a
+            # saturated counter (round 3 at B = 4096), not a measurement
+            v = d["SQ_VALU_MFMA_BUSY_CYCLES"]
+            d["mfma_busy_saturated"] = v >= 2.0 ** 31 - 1
+            d["mfma_busy_frac"] = round(v / (128.0 * d["GRBM_GUI_ACTIVE"]), 4)
+        if durs.get(lab):
+            dv = sorted(durs[lab])
+            d["trace_ms"] = round(dv[len(dv) // 2], 4)
+            if d.get("GRBM_GUI_ACTIVE"):
+                d["clock_ghz"] = round(d["GRBM_GUI_ACTIVE"] / 8.0 / (d["trace_ms"] * 1e6), 3)
     try:
         with open(out_json) as fi:
             allres = json.load(fi)

@@ -33,3 +33,21 @@ def test_winograd_epilogues_match_direct_engine(case):
     assert os.path.exists(BENCH), "tools/wino_bench missing: run make"
     r = subprocess.run([BENCH] + [str(v) for v in case], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, (case, r.stdout, r.stderr)
+
+
+WB = os.path.join(ROOT, "tools", "wb_bench")
+WB_CASES = [  # H, W, B, reps: the fused layer-2 backward (wgbd_wino) vs wgrad_wino + conv_wino's data gradient
+    (40, 200, 48, 1),   # cnn_small T = 200: strips of 48 + 52 tiles
+    (20, 100, 24, 1),   # T = 100: one 50-tile strip (4 data-gradient groups, the last partial)
+    (21, 56, 16, 1),    # odd H (a half tile row at the bottom), one 28-tile strip
+]
+
+
+@pytest.mark.parametrize("case", WB_CASES)
+def test_fused_layer2_backward_matches_two_kernel_path(case):
+    """dW, dz_prev and the producer BN's backward sums of the one-pass kernel agree with the two
+    kernels it replaces (both Winograd, fp32: rounding-level differences only, <= 2e-5 relative)."""
+    assert os.path.exists(WB), "tools/wb_bench missing: run make"
+    r = subprocess.run([WB] + [str(v) for v in case], capture_output=True, text=True, timeout=120)
+    print(r.stdout)
+    assert r.returncode == 0, (case, r.stdout, r.stderr)

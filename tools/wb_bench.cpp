@@ -1,0 +1,141 @@
+// Cross-check + timing of the fused layer-2 backward (wgbd_wino: Winograd weight AND data gradient in
+// one pass) against the two-kernel path it replaces (wgrad_wino writing dy, then conv_wino's data
+// gradient with the EPI_BWD_RELU epilogue), on random operands of one shape.
+//   wb_bench H W [B] [reps]
+// Prints both times and the differences: dW (max |a - b| / max |b|), dz_prev (max |a - b| / max |b|),
+// the producer-BN backward sums (relative, per channel).  Exit 2 when a difference exceeds 2e-5
+// (tests/test_wino_engine_gpu.py runs it).
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include "../phoneme_contrast_amd/csrc/kernels.h"
+#include "pcx.h"
+
+__global__ void fill(float* p, size_t n, unsigned seed, float scale, float off) {
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    for (; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        unsigned h = (unsigned)i * 2654435761u ^ seed;
+        h ^= h >> 13; h *= 0x5bd1e995; h ^= h >> 15;
+        p[i] = off + scale * ((h & 0xffffff) / 16777216.0f - 0.5f);
+    }
+}
+
+static void check(int rc, const char* what) {
+    if (rc) {
+        char msg[512];
+        pcx_last_error(msg, sizeof msg);
+        printf("%s failed: %s\n", what, msg);
+        exit(1);
+    }
+}
+
+static double maxrel(const std::vector<float>& a, const std::vector<float>& b) {
+    double m = 0.0, d = 0.0;
+    for (size_t i = 0; i < a.size(); ++i) {
+        m = std::max(m, (double)std::fabs(b[i]));
+        d = std::max(d, (double)std::fabs(a[i] - b[i]));
+    }
+    return m > 0 ? d / m : d;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 3) { printf("usage: wb_bench H W [B] [reps]\n"); return 2; }
+    const int H = atoi(argv[1]), W = atoi(argv[2]);
+    const int B = argc > 3 ? atoi(argv[3]) : 4096, reps = argc > 4 ? atoi(argv[4]) : 5;
+    const int C = 32;
+    pcx::WinoBwdArgs f{};
+    pcx::WinoWgradArgs w{};
+    pcx::WinoGeo g{};
+    if (!pcx::wgbd_wino_geometry(B, H, W, C, &f)) { printf("no wgbd geometry for %dx%d\n", H, W); return 1; }
+    if (!pcx::wgrad_wino_geometry(B, H, W, C, C, &w)) { printf("no wgrad_wino geometry\n"); return 1; }
+    if (!pcx::wino_geometry(B, H, W, C, C, &g)) { printf("no wino geometry\n"); return 1; }
+    const size_t n = (size_t)B * C * H * W, nw = (size_t)C * C * 9;
+    const int nblk = (int)pcx::wino_nblk(B, H, W, C, C);
+    float *dz, *y, *yp, *dy, *dzp1, *dzp2, *cfd, *cfx, *wt, *up, *part, *g1, *g2, *bn;
+    (void)hipMalloc(&dz, n * 4); (void)hipMalloc(&y, n * 4); (void)hipMalloc(&yp, n * 4); (void)hipMalloc(&dy, n * 4);
+    (void)hipMalloc(&dzp1, n * 4); (void)hipMalloc(&dzp2, n * 4);
+    (void)hipMalloc(&cfd, C * 16); (void)hipMalloc(&cfx, C * 16); (void)hipMalloc(&wt, nw * 4);
+    (void)hipMalloc(&up, (size_t)16 * C * C * 4);
+    const size_t np = std::max((size_t)f.nslice, (size_t)w.nslice) * C * C * 16;
+    (void)hipMalloc(&part, np * 4); (void)hipMalloc(&g1, nw * 4); (void)hipMalloc(&g2, nw * 4);
+    const size_t nbn = 2 * (size_t)C * std::max(f.nslice, nblk);
+    (void)hipMalloc(&bn, nbn * 4);
+    fill<<<4096, 256>>>(dz, n, 1, 2.f, 0.f); fill<<<4096, 256>>>(y, n, 2, 2.f, 0.f); fill<<<4096, 256>>>(yp, n, 3, 2.f, 0.f);
+    fill<<<1, 256>>>(cfd, C * 4, 4, 0.5f, 1.f); fill<<<1, 256>>>(cfx, C * 4, 5, 0.5f, 0.5f);
+    fill<<<1, 256>>>(wt, nw, 6, 0.4f, 0.f);
+    (void)hipMemset(dzp1, 0, n * 4); (void)hipMemset(dzp2, 0, n * 4);
+    check(pcx::launch_wino_pack(wt, up, C, C, 1, 0), "wino_pack");
+
+    // fused
+    f.B = B; f.H = H; f.W = W;
+    f.dz = dz; f.y = y; f.cf_dy = (const float4*)cfd; f.yp = yp; f.cf_x = (const float4*)cfx; f.up = up;
+    f.part = part; f.dzp = dzp1; f.bn0 = bn; f.bn1 = bn + (size_t)C * f.nslice;
+    auto fused = [&]() {
+        check(pcx::launch_wgbd_wino(f, 0), "wgbd_wino");
+        check(pcx::launch_wgrad_wino_reduce(part, f.nslice, C, C, g1, 0), "reduce");
+    };
+    fused();
+    (void)hipDeviceSynchronize();
+    std::vector<float> bnf(2 * (size_t)C * f.nslice);
+    (void)hipMemcpy(bnf.data(), bn, bnf.size() * 4, hipMemcpyDeviceToHost);
+    std::vector<double> sf(2 * C, 0.0), sr(2 * C, 0.0);
+    for (int c = 0; c < C; ++c)
+        for (int s = 0; s < f.nslice; ++s) {
+            sf[c] += bnf[(size_t)c * f.nslice + s];
+            sf[C + c] += bnf[(size_t)(C + c) * f.nslice + s];
+        }
+
+    // two-kernel reference path
+    w.B = B; w.H = H; w.W = W; w.cin = C; w.cout = C;
+    w.dz = dz; w.y = y; w.cf_dy = (const float4*)cfd; w.src = yp; w.cf_x = (const float4*)cfx;
+    w.part = part; w.dy_out = dy;
+    pcx::ConvArgs c{};
+    c.B = B; c.H = H; c.W = W; c.cin = C; c.cout = C;
+    c.src = dy; c.srcH = H; c.srcW = W; c.wpack = up; c.out = dzp2; c.yprev = yp; c.cf_out = (const float4*)cfx;
+    c.Hs = H; c.Ws = W; c.part0 = bn; c.part1 = bn + (size_t)C * nblk; c.nblk = nblk;
+    auto twok = [&]() {
+        check(pcx::launch_wgrad_wino(pcx::PRO_BNRELU, w, 0), "wgrad_wino");
+        check(pcx::launch_wgrad_wino_reduce(part, w.nslice, C, C, g2, 0), "reduce");
+        check(pcx::launch_conv3x3_wino(pcx::PRO_RAW, pcx::EPI_BWD_RELU, c, 0), "conv_wino dgrad");
+    };
+    twok();
+    (void)hipDeviceSynchronize();
+    std::vector<float> bnr(2 * (size_t)C * nblk);
+    (void)hipMemcpy(bnr.data(), bn, bnr.size() * 4, hipMemcpyDeviceToHost);
+    for (int ci = 0; ci < C; ++ci)
+        for (int s = 0; s < nblk; ++s) {
+            sr[ci] += bnr[(size_t)ci * nblk + s];
+            sr[C + ci] += bnr[(size_t)(C + ci) * nblk + s];
+        }
+
+    std::vector<float> h1(nw), h2(nw), d1(n), d2(n);
+    (void)hipMemcpy(h1.data(), g1, nw * 4, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(h2.data(), g2, nw * 4, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(d1.data(), dzp1, n * 4, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(d2.data(), dzp2, n * 4, hipMemcpyDeviceToHost);
+    const double ew = maxrel(h1, h2), ed = maxrel(d1, d2);
+    double eb = 0.0, mb = 0.0;
+    for (int i = 0; i < 2 * C; ++i) {
+        mb = std::max(mb, std::fabs(sr[i]));
+        eb = std::max(eb, std::fabs(sf[i] - sr[i]));
+    }
+    eb = mb > 0 ? eb / mb : eb;
+
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
+    float tf = 0.f, tr = 0.f;
+    (void)hipEventRecord(e0);
+    for (int i = 0; i < reps; ++i) fused();
+    (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
+    (void)hipEventElapsedTime(&tf, e0, e1);
+    (void)hipEventRecord(e0);
+    for (int i = 0; i < reps; ++i) twok();
+    (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
+    (void)hipEventElapsedTime(&tr, e0, e1);
+    printf("wgbd H=%d W=%d B=%d strips=%d (%d,%d) nslice=%d: fused %.3f ms, two-kernel %.3f ms; "
+           "dW rel %.2e, dz_prev rel %.2e, BN sums rel %.2e\n", H, W, B, f.nseg, f.seg_S[0], f.seg_S[1], f.nslice,
+           tf / reps, tr / reps, ew, ed, eb);
+    return (ew < 2e-5 && ed < 2e-5 && eb < 2e-5) ? 0 : 2;
+}
