@@ -39,6 +39,8 @@ def kernel_costs(B, F, T, D=128):
         out[f"conv_dgrad_L{l}"] = (2 * macs, 2 * y_out + 2 * x_in)
         # wgrad: reads dz_l, y_l and the forward input source
         out[f"wgrad_L{l}"] = (2 * macs, 2 * y_out + x_in)
+        if l == 2:  # the fused layer-2 backward (wgbd_wino.hip): both GEMMs; dz2, y2, y1 read, dz1 written
+            out["wgbd_L2"] = (4 * macs, 2 * y_out + 2 * x_in)
     # elementwise / head passes (bytes: each tensor read once, each output written once)
     H1, W1, H3, W3, H5, W5 = F, T, F // 2, T // 2, F // 4, T // 4
     out["bn_relu_pool_L3"] = (0, 4 * B * 32 * (H1 * W1 + H3 * W3))
@@ -60,6 +62,8 @@ def executed_fraction(label, T):
             return 4 / 9 if widths.get(int(label[len(pre):]), 0) >= 31 else 1.0
     if label.startswith("wgrad_L") and label[7:].isdigit() and int(label[7:]) >= 2:
         return 4 / 9 if widths[int(label[7:])] % 2 == 0 else 1.0
+    if label == "wgbd_L2":  # fused layer-2 backward: both gradients on Winograd F(2x2,3x3)
+        return 4 / 9
     return 1.0
 
 

@@ -30,7 +30,15 @@
 // turned into dy / x and stored after the row's last group.  Out-of-image items load 0 (buffer offsets
 // beyond num_records) and stage exact zeros.  Strips are 48 / 52 tiles at W = 200 (the data gradient
 // runs 16-tile groups: 7 groups per tile row, 12 % padding).
+#include <type_traits>
+
 #include "kernels.h"
+
+#if defined(WB_KO) && (WB_KO & 4)
+#define WB_KO_EPI 1
+#else
+#define WB_KO_EPI 0
+#endif
 
 namespace pcx {
 namespace {
@@ -155,7 +163,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
     double* const bsum = reinterpret_cast<double*>(xb + 2 * 4096) + 4 * (dg ? ld : 0);
     if (dg)
         for (int i = 0; i < 4; ++i) bsum[i] = 0.0;
+    // epilogue coefficients per channel: the epilogue reads the staged x = relu(s yp + t) instead of yp
+    // (no global load inside the row loop: a vmcnt wait there would also wait for the next row's staging
+    // loads), so mask = [x > 0] (exactly [s yp + t > 0]) and, where the mask is on, x = s yp + t, hence
+    // xhat = (yp - mean) invstd = x r1 + r0 with r1 = invstd / s, r0 = -(t / s + mean) invstd
+    float2* const ecf = reinterpret_cast<float2*>(xb + 2 * 4096 + 2048);
+    if (tid < CH) {
+        const float4 k = a.cf_x[tid];
+        const float r1 = k.x != 0.f ? k.w / k.x : 0.f;
+        ecf[tid] = make_float2(r1, -(k.y * r1) - k.z * k.w);
+    }
 
+    // the task loop is instantiated once per wave role (the weight-gradient and the data-gradient code
+    // then get their registers allocated separately: one loop with a runtime branch spilled); both
+    // instantiations execute the same barriers
+    auto run = [&](auto role) {
+    constexpr bool DG = decltype(role)::value;
     const int t0s = slice * a.per_slice, t1s = min(a.ntask, t0s + a.per_slice);
     for (int task = t0s; task < t1s; ++task) {
         const int b = task / a.nseg, seg = task - b * a.nseg;
@@ -243,8 +266,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
             // ring rows of this tile row: patch row i (image row 2 tr - 1 + i) in slot (2 tr + i) & 3
             const int sw = ((2 * tr + IW) & 3) * CH * XCS, su = ((2 * tr + IU) & 3) * CH * XCS;
             float rz[2] = {0.f, 0.f}, rx_[2] = {0.f, 0.f};  // this row's BN sums (data-gradient epilogue)
+            float ex[2][4];                                  // the epilogue's x values (prefetched)
             for (int g = 0; g < ng; ++g) {
-                if (!dg) {
+                if constexpr (!DG) {
+#if !(defined(WB_KO) && (WB_KO & 1))
                     // ---- weight gradient: K-steps 8 g .. 8 g + 7 (tiles 16 g .. 16 g + 15)
                     const float* w = xr + sw + c32 * XCS + 2 * g2;
                     const float* u = xr + su + c32 * XCS + 2 * g2;
@@ -264,7 +289,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
                         __builtin_amdgcn_sched_barrier(0);
                     }
                     if (s < s1) wmul(A, sx, sy, R);
+#endif
                 } else {
+#if !(defined(WB_KO) && (WB_KO & 2))
                     // ---- data gradient: tiles 16 g + t_l (clamped into the strip), K = 32 dy channels
                     const int tl = min(16 * g + t_l, S - 1);
                     const float* pw = dr + sw + n_l * XCS + 2 * tl;
@@ -307,9 +334,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
                             const float m1 = acc[1][cs][r] - acc[2][cs][r] - acc[3][cs][r];
                             *reinterpret_cast<f2*>(xo + (c * 16 + t_l) * 8 + 2 * Q) = f2{m0, m1};
                         }
+#endif
+                    // the epilogue's x values (rows 2 tr, 2 tr + 1 = ring slots of patch rows 1, 2) read
+                    // before the barrier: after the last group's barrier the next stage overwrites row 2 tr
+                    const int so1 = ((2 * tr + 1) & 3) * CH * XCS, so2 = ((2 * tr + 2) & 3) * CH * XCS;
+#pragma unroll
+                    for (int k2 = 0; k2 < 2; ++k2) {
+                        const int p = ld + 256 * k2, c = p >> 4, tile = min(16 * g + (p & 15), S - 1);
+                        const float* xp = xr + c * XCS + 2 * tile + 1;
+                        ex[k2][0] = xp[so1];
+                        ex[k2][1] = xp[so1 + 1];
+                        ex[k2][2] = xp[so2];
+                        ex[k2][3] = xp[so2 + 1];
+                    }
                 }
                 __syncthreads();  // group g's (M A) rows visible; group g - 1's exchange buffer consumed
-                if (dg) {
+                if constexpr (DG && !(WB_KO_EPI)) {
                     // ---- epilogue of group g: dx = A^T (M A) over the 4 rows, ReLU(BN_prev) mask, BN_prev sums
                     const float* xi = xb + (g & 1) * 4096;
                     const int h0 = 2 * tr;
@@ -324,25 +364,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
                         const float y00 = m0[0] + m0[2] + m1[0], y01 = m0[1] + m0[3] + m1[1];
                         const float y10 = m0[2] - m1[0] - m1[2], y11 = m0[3] - m1[1] - m1[3];
                         const int64_t o = pb + (int64_t)c * HW + h0 * W + 2 * (t0 + tile);
-                        const float2 p0 = *reinterpret_cast<const float2*>(a.yp + o);
-                        const float2 p1 = r1ok ? *reinterpret_cast<const float2*>(a.yp + o + W) : make_float2(0.f, 0.f);
-                        const float4 k = a.cf_x[c];
-                        const float yy[4] = {p0.x, p0.y, p1.x, p1.y};
+                        const float2 k = ecf[c];
                         const float gv[4] = {y00, y01, y10, y11};
                         float dz[4];
 #pragma unroll
                         for (int e = 0; e < 4; ++e) {
-                            const bool on = (e < 2 || r1ok) && fmaf(yy[e], k.x, k.y) > 0.f;
-                            dz[e] = on ? gv[e] : 0.f;
+                            const float xe = ex[k2][e];  // 0 outside the image (row H of an odd H)
+                            dz[e] = xe > 0.f ? gv[e] : 0.f;
                             rz[k2] += dz[e];
-                            rx_[k2] = fmaf(dz[e], (yy[e] - k.z) * k.w, rx_[k2]);
+                            rx_[k2] = fmaf(dz[e], fmaf(xe, k.x, k.y), rx_[k2]);
                         }
                         *reinterpret_cast<float2*>(a.dzp + o) = make_float2(dz[0], dz[1]);
                         if (r1ok) *reinterpret_cast<float2*>(a.dzp + o + W) = make_float2(dz[2], dz[3]);
                     }
                 }
             }
-            if (dg) {
+            if constexpr (DG) {
 #pragma unroll
                 for (int k2 = 0; k2 < 2; ++k2) {
                     bsum[k2] += (double)rz[k2];
@@ -354,6 +391,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
             __syncthreads();
         }
     }
+    };
+    if (dg) run(std::true_type{});
+    else run(std::false_type{});
     // ---- outputs: weight-gradient partials (as wgrad_wino: row (r & 3) + 8 (r >> 2) + 4 g2, column c32)
     if (!dg) {
         float* out = a.part + (int64_t)slice * CH * CH * 16;
@@ -412,7 +452,8 @@ bool wgbd_wino_geometry(int B, int H, int W, int C, WinoBwdArgs* a) {
     const int kmax = (2 * smax + 1 + V - 1) / V, nx = kmax + 1;
     if (nx > 16 * 2) return false;  // 16 threads x NIR = 2 items per row and channel
     const int XCS = smallest_2odd(std::max(V * kmax + 1, 2 * smax + 5));
-    const size_t lds = ((size_t)4 + 8 * CH * XCS + 2 * 4096) * 4 + 256 * 4 * 8;  // + the lanes' float64 sums
+    // rings, exchange buffer, the lanes' float64 sums, the epilogue coefficients
+    const size_t lds = ((size_t)4 + 8 * CH * XCS + 2 * 4096) * 4 + 256 * 4 * 8 + CH * 8;
     if (lds > 160 * 1024) return false;
     if ((int64_t)CH * H * W * 4 >= OOB) return false;
     if (a) {

@@ -17,10 +17,13 @@ FWD = [f"conv_fwd_L{l}" for l in range(2, 7)]
 DGRAD = [f"conv_dgrad_L{l}" for l in range(6, 1, -1)]
 # kernel family (name up to '<' / '(') -> layer labels in per-step dispatch order
 ORDER = {
-    "conv_wino_kernel": FWD + DGRAD,  # Winograd conv (every cnn_small layer at W >= 31)
+    # Winograd conv (every cnn_small layer at W >= 31); layer 2's data gradient runs inside the fused
+    # layer-2 backward (wgbd_wino_kernel, round 4) at T = 200
+    "conv_wino_kernel": FWD + DGRAD[:-1],
     "conv3x3_dma_kernel": FWD + DGRAD,
     "wgrad_s_kernel": [f"wgrad_L{l}" for l in range(6, 1, -1)],
-    "wgrad_wino_kernel": [f"wgrad_L{l}" for l in range(6, 1, -1)],  # Winograd weight gradient (W even)
+    "wgrad_wino_kernel": [f"wgrad_L{l}" for l in range(6, 2, -1)],  # Winograd weight gradient (W even)
+    "wgbd_wino_kernel": ["wgbd_L2"],
     "wgrad_wino_reduce_kernel": [f"wgrad_reduce_L{l}" for l in range(6, 1, -1)],
     "bn_relu_pool_kernel": ["bn_relu_pool_L3", "bn_relu_pool_L5"],
     "conv1_fwd_kernel": ["conv1_fwd_L1"],
