@@ -207,6 +207,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
         };
         auto goff = [&](int m, int st) { return ch * HW + (2 * st + 1 + m / NIR) * W + c0 - V + V * (j0 + 16 * (m % NIR)); };
         auto load = [&](int st) {
+#if defined(WB_KO) && (WB_KO & 8)  // analysis builds only (tools/wb_ko.sh): no staging loads
+            for (int m = 0; m < NIT; ++m) dzv[m] = yv[m] = xv[m] = vecf<V>(0.f);
+            return;
+#endif
             const unsigned ok = rowmask(st);
 #pragma unroll
             for (int m = 0; m < NIT; ++m) {

@@ -11,7 +11,7 @@ BASELINE size.  Reference: /root/reference/src/models/phoneme_cnn.py:98-126 (cnn
 
 Tolerances (stated contract): embeddings 1e-5 abs, loss 1e-4 abs, gradients
 2e-3 x max|g| per tensor (biases feeding a train-mode BN: 1e-4 abs, their exact gradient is 0),
-running statistics 1e-5 rel.  cnn_deep fp32 embeddings 5e-5 (as the full-width B = 4/5 test).  Both
+running statistics 1e-5 rel (cnn_deep fp32 embeddings too: 4.5e-6 measured, round 4).  Both
 models' gradients are also compared with torch's own float32 evaluation of the same step (the
 reference's arithmetic): cnn_small's layer-1 gradients are 33 M-term sums at the end of a 6-layer
 backward (~1e-3 of max|g| in any float32 evaluation), and cnn_deep's ReLU / max-pool kinks move
@@ -209,4 +209,5 @@ def test_cnn_deep_fp32_b4096_matches_float64():
     with torch.backends.cudnn.flags(enabled=False):  # torch's own float32 im2col + rocBLAS convs
         f32 = _run_oracle(sd64, x, labels, masks, 0.15, torch.float32)
     _free()
-    _compare(got, ref, 5e-5, "cnn_deep_fp32", yardstick=f32)
+    # embeddings at the 1e-5 contract (round 4: measured 4.5e-6; round 3 held them to 5e-5)
+    _compare(got, ref, 1e-5, "cnn_deep_fp32", yardstick=f32)
