@@ -32,7 +32,8 @@ def kernel_costs(B, F, T, D=128):
         x_in = 4 * B * ci * sh * sw
         if l == 1:
             out["conv1_fwd_L1"] = (2 * macs, 4 * B * F * T + y_out)
-            out["wgrad_L1"] = (2 * macs, 2 * y_out + 4 * B * F * T)
+            # (round 4: y1 is recomputed from the input window, not read: dz1 + x)
+            out["wgrad_L1"] = (2 * macs, y_out + 4 * B * F * T)
             continue
         out[f"conv_fwd_L{l}"] = (2 * macs, x_in + y_out)
         # dgrad: reads dz_l and y_l, reads y_{l-1} (epilogue), writes dz_{l-1}

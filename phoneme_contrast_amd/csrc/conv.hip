@@ -17,6 +17,8 @@ void tile_shape(int cout, int* wm, int* wn) {
     else { *wm = 2; *wn = 2; }
 }
 
+typedef const __attribute__((address_space(4))) float* cfloat4p;  // constant space: scalar loads
+
 // ------------------------------------------------------------------ Cin = 1 first conv
 constexpr int C1_CPW = 8;  // output channels per wave
 
@@ -181,8 +183,11 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Args a) {
 // ------------------------------------------------------------------ weight gradient, Cin = 1
 // dW[n][tap] = sum dy[n] x(shifted), dy = BN backward of (dz, y).  Same quad walk as the forward:
 // wave w owns channels 8w .. 8w + 7 (+ 32k), lanes consecutive pixel quads (16-byte dz / y loads);
-// HBM-read-bound (dz and y are read once).  Partials per slice.
-template <bool FULL>
+// HBM-read-bound.  Partials per slice.  RC (round 4): y is not read but recomputed from the input
+// window the gradient needs anyway, with conv1_fwd_kernel's weights and FMA order (the same float
+// bits): 9 FMAs per output instead of 4 bytes of HBM -- dz alone is streamed (4.2 instead of 8.4 GB
+// per B = 4096 step).
+template <bool FULL, bool RC>
 __global__ __launch_bounds__(256) void wgrad1_kernel(Wgrad1Args a) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -195,6 +200,14 @@ __global__ __launch_bounds__(256) void wgrad1_kernel(Wgrad1Args a) {
     for (int cg = wave * C1_CPW; cg < a.cout; cg += 4 * C1_CPW) {
         float acc[C1_CPW][9];
         float A1[C1_CPW], A2[C1_CPW], A3[C1_CPW];
+        float wt[RC ? C1_CPW : 1][9];  // wave-uniform: constant-space loads into scalar registers
+        if constexpr (RC) {
+            const cfloat4p wp = (cfloat4p)a.w;
+#pragma unroll
+            for (int j = 0; j < C1_CPW; ++j)
+#pragma unroll
+                for (int t = 0; t < 9; ++t) wt[j][t] = wp[(cg + j) * 9 + t];
+        }
 #pragma unroll
         for (int j = 0; j < C1_CPW; ++j) {
             const float4 k = a.cf_dy[cg + j];  // dy = a (dz - mb - (y - mean) mgi)
@@ -215,16 +228,28 @@ __global__ __launch_bounds__(256) void wgrad1_kernel(Wgrad1Args a) {
             for (int j = 0; j < C1_CPW; ++j) {
                 float dz[4], yy[4];
                 if (FULL) {
-                    const float4 u = ld4(a.dz + o + (int64_t)j * HW), v = ld4(a.y + o + (int64_t)j * HW);
+                    const float4 u = ld4(a.dz + o + (int64_t)j * HW);
                     dz[0] = u.x; dz[1] = u.y; dz[2] = u.z; dz[3] = u.w;
-                    yy[0] = v.x; yy[1] = v.y; yy[2] = v.z; yy[3] = v.w;
+                    if constexpr (!RC) {
+                        const float4 v = ld4(a.y + o + (int64_t)j * HW);
+                        yy[0] = v.x; yy[1] = v.y; yy[2] = v.z; yy[3] = v.w;
+                    }
+                }
+                if constexpr (RC) {  // conv1_fwd_kernel's arithmetic, term for term
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        float v = 0.f;
+#pragma unroll
+                        for (int tp = 0; tp < 9; ++tp) v = fmaf(wt[j][tp], xr[tp / 3][e + tp % 3], v);
+                        yy[e] = v;
+                    }
                 }
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     if (!FULL) {
                         const bool ok = w0 + e < a.W;
                         dz[e] = ok ? a.dz[o + (int64_t)j * HW + e] : 0.f;
-                        yy[e] = ok ? a.y[o + (int64_t)j * HW + e] : 0.f;
+                        if constexpr (!RC) yy[e] = ok ? a.y[o + (int64_t)j * HW + e] : 0.f;
                     }
                     float dy = fmaf(A1[j], dz[e], fmaf(A2[j], yy[e], A3[j]));
                     if (!FULL && w0 + e >= a.W) dy = 0.f;
@@ -259,7 +284,6 @@ __global__ __launch_bounds__(256) void wgrad1_kernel(Wgrad1Args a) {
 constexpr int ST_K = 7, ST_T = 49, ST_WCPW = 2;
 
 __device__ __forceinline__ float bf16r(float v) { return (float)(__bf16)v; }
-typedef const __attribute__((address_space(4))) float* cfloat4p;  // constant space: scalar loads
 
 __host__ __device__ constexpr int st_rw(int W) { return ((W + 8) + 3) & ~3; }  // LDS row: 4 | W | >= 4
 
@@ -1713,10 +1737,15 @@ int launch_conv1_fwd(Conv1Args a, hipStream_t s) {
 int launch_wgrad1(Wgrad1Args a, hipStream_t s) {
     PCX_CHECK_ARG(a.cout % (4 * C1_CPW) == 0, "wgrad1: cout must be a multiple of 32");
     PCX_CHECK_ARG((int64_t)a.B * a.H < ((int64_t)1 << 31), "wgrad1: too many rows");
-    if (a.W % 4 == 0)
-        wgrad1_kernel<true><<<a.nslice, 256, 0, s>>>(a);
-    else
-        wgrad1_kernel<false><<<a.nslice, 256, 0, s>>>(a);
+    PCX_CHECK_ARG(a.y || a.w, "wgrad1: needs the conv output y or the weights to recompute it");
+    const bool rc = a.y == nullptr;
+    if (a.W % 4 == 0) {
+        if (rc) wgrad1_kernel<true, true><<<a.nslice, 256, 0, s>>>(a);
+        else wgrad1_kernel<true, false><<<a.nslice, 256, 0, s>>>(a);
+    } else {
+        if (rc) wgrad1_kernel<false, true><<<a.nslice, 256, 0, s>>>(a);
+        else wgrad1_kernel<false, false><<<a.nslice, 256, 0, s>>>(a);
+    }
     PCX_LAUNCH_CHECK("wgrad1_kernel");
     return PCX_OK;
 }

@@ -30,6 +30,7 @@
 //    contiguous run per K-chunk: dwordx4 DMA, conflict-free ds_read_b128 A operands;
 //  * epilogue: the 16 lanes of a row hold 16 consecutive tiles, so output rows are stored (and the
 //    producer's y / pooled windows loaded) as 128- / 256-byte runs.
+#include <cstdlib>
 #include <type_traits>
 
 #include "conv_epilogue.h"
@@ -80,6 +81,14 @@ constexpr int WSW = 36, WSP = 160;
 __device__ __forceinline__ void bdma(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned lds_byte_addr) {
     const unsigned m0 = __builtin_amdgcn_readfirstlane(lds_byte_addr);
     asm volatile("s_nop 0\n\tbuffer_load_dword %0, %1, 0 offen lds" :: "v"(voff), "s"(r), "{m0}"(m0) : "memory");
+}
+
+// LDS DMA of 16 bytes per lane (the source may be any 4-byte aligned address: measured,
+// profiles/r4_probe_dma_align.txt); LDS destination = M0 + 16 * lane.  Past num_records the range
+// check is per dword (profiles/r4_probe_dma_oob.txt).
+__device__ __forceinline__ void bdma4(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned lds_byte_addr) {
+    const unsigned m0 = __builtin_amdgcn_readfirstlane(lds_byte_addr);
+    asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" :: "v"(voff), "s"(r), "{m0}"(m0) : "memory");
 }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t wrsrc(const float* base, int bytes) {
@@ -389,8 +398,16 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
 // Persistent: each workgroup walks units u = it * G + (XCD-contiguous slot); unit = (64-tile block tb
 // of one sample, 32-channel output group cg).  The first K-chunk of the next unit is copied while the
 // last chunk of the current one is multiplied and during its epilogue.
-template <int PRO, int EPI, int CK, bool V4>
+// X4 (round 4): the operand slot is copied by 16-byte DMAs -- 5 per chunk of 8 channels instead of 24
+// dword copies; a slot row is 40 floats (segment B starts on a 16-byte granule), the 4-byte-aligned
+// sources of the granules straddle the image's left / right edges, and the out-of-image columns they
+// bring in (the neighbouring rows' values) are zeroed by selects in the border waves, for every prologue.
+// Needs 4 readable bytes before a.src (ConvArgs::src_guard: the plans carve a guard at the workspace start).
+template <int PRO, int EPI, int CK, bool V4, bool X4>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv_wino_kernel(ConvArgs a, WinoGeo g) {
+    static_assert(!X4 || CK == 8, "16-byte staging covers whole 8-channel chunks");
+    constexpr int WROW = X4 ? 40 : WSW;       // slot row width (floats)
+    constexpr int NCP = X4 ? 5 : 3;           // copy offsets per lane
     constexpr int WSLOT = CK * WSP + 32;      // floats of one wave's slot (+ the last plane's overflow)
     constexpr int INF = 4 * WSLOT;            // input floats per buffer
     constexpr int BUFF = INF + CK * 512;      // + transformed weights of the chunk
@@ -430,11 +447,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     // wave's loads land in issue order); the last plane runs into the slot's 32-float tail.  Lane
     // offsets depend on the unit only (the channel is the buffer base); out-of-image positions get
     // an out-of-range offset, which copies a 0.  (No exec masking next to in-flight MFMAs.)
-    unsigned voff[3];
+    unsigned voff[NCP];
     auto plan_copies = [&](const Unit& x) {
-        const int segw = 2 * min(16, g.TC - x.tc_a) + 2;
+        const int len_a = min(16, g.TC - x.tc_a);
+        const int segw = 2 * len_a + 2;
         const int rb0 = 2 * x.tr_a - 1, rb1 = 2 * x.tr_a + 1;
         const int cb0 = 2 * x.tc_a - 1, cb1 = -segw - 1;
+        if constexpr (X4) {
+            // granule gi = 64 j + lane of the chunk: plane gi / 40, row (gi % 40) / 10, slot column 4 (gi % 10);
+            // offsets relative to a.src + (b cin + c0) HW - 1 (the granule of image column -1 starts in range)
+            const int SB = (segw + 3) & ~3, segwB = 2 * (16 - len_a) + 2;
+#pragma unroll
+            for (int j = 0; j < NCP; ++j) {
+                const int gi = 64 * j + lane, pl = gi / 40, gg = gi - pl * 40, r = gg / 10, sc = 4 * (gg - r * 10);
+                const bool sB = sc >= SB;
+                const int grow = r + (sB ? rb1 : rb0), gcol = sB ? sc - SB - 1 : cb0 + sc;
+                const bool ok = (unsigned)grow < (unsigned)a.H && (sB ? (len_a < 16 && sc - SB < segwB) : sc < segw);
+                voff[j] = ok ? 4u * (unsigned)(pl * HW + grow * a.W + gcol + 1) : 0x80000000u;
+            }
+            return;
+        }
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
             const int pos = 64 * p + lane;
@@ -454,7 +486,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
 #endif
         const float* sb = a.src + ((int64_t)x.b * a.cin + c0) * HW;
         const unsigned sl = lds0 + 4u * (unsigned)(buf * BUFF + wave * WSLOT);
-        const int cpp = CK / np;
+        if constexpr (X4) {  // 5 granule copies per chunk: parts of 3 + 2
+            const __amdgpu_buffer_rsrc_t r = wrsrc(sb - 1, 4 * (CK * HW + 1));
+            const int j0 = part == 0 ? 0 : 3, j1 = np == 1 ? NCP : (part == 0 ? 3 : NCP);
+#pragma unroll
+            for (int j = 0; j < NCP; ++j)
+                if (j >= j0 && j < j1) bdma4(r, voff[j], sl + 1024u * (unsigned)j);
+        }
+        const int cpp = X4 ? 0 : CK / np;
 #pragma unroll
         for (int ci = 0; ci < cpp; ++ci) {
             const int cl = part * cpp + ci;
@@ -489,21 +528,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
         const bool seg1 = n >= len_a;
         const int tr = seg1 ? cur.tr_a + 1 : cur.tr_a, tc = seg1 ? n - len_a : cur.tc_a + n;
         const bool tvalid = cur.tw + n < g.NTS;
-        const int pbase = wave * WSLOT + kq * WSP + (seg1 ? 2 * n + 2 : 2 * n);
+        // (X4: segment B starts at the granule after segment A's segw columns)
+        const int bshift = X4 ? (((2 * len_a + 2 + 3) & ~3) - (2 * len_a + 2)) : 0;
+        const int pbase = wave * WSLOT + kq * WSP + (seg1 ? 2 * n + 2 + bshift : 2 * n);
         // BN+ReLU operands: out-of-image patch rows / columns must be 0 after the prologue (the copy
         // wrote raw 0s there); a factor per patch row / column, applied only in waves that touch the
         // image border
         float fr0 = 1.f, fr2 = 1.f, fr3 = 1.f, fc0 = 1.f, fc2 = 1.f, fc3 = 1.f;
         bool border = false;
-        if (PRO != PRO_RAW) {
+        if (PRO != PRO_RAW || X4) {
             fr0 = tr > 0 ? 1.f : 0.f;
             fr2 = 2 * tr + 1 < a.H ? 1.f : 0.f;
             fr3 = 2 * tr + 2 < a.H ? 1.f : 0.f;
             fc0 = tc > 0 ? 1.f : 0.f;
             fc2 = 2 * tc + 1 < a.W ? 1.f : 0.f;
             fc3 = 2 * tc + 2 < a.W ? 1.f : 0.f;
-            border = __builtin_amdgcn_readfirstlane(
-                         (int)(__ballot((fr0 * fr2 * fr3 * fc0 * fc2 * fc3) == 0.f) != 0)) != 0;
+            // (X4 under PRO_RAW: out-of-image rows are zero-copied; only the columns need zeroing)
+            const float f = (PRO == PRO_RAW ? 1.f : fr0 * fr2 * fr3) * fc0 * fc2 * fc3;
+            border = __builtin_amdgcn_readfirstlane((int)(__ballot(f == 0.f) != 0)) != 0;
         }
         f32x4 acc[16][2];  // the unit's first K-step starts the sums from 0 (no zeroing pass)
         auto kloop = [&](auto btag) {
@@ -518,8 +560,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
                 const float* pp = bi + pbase + 4 * s * WSP;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const f2 u0 = *reinterpret_cast<const f2*>(pp + r * WSW);
-                    const f2 u1 = *reinterpret_cast<const f2*>(pp + r * WSW + 2);
+                    const f2 u0 = *reinterpret_cast<const f2*>(pp + r * WROW);
+                    const f2 u1 = *reinterpret_cast<const f2*>(pp + r * WROW + 2);
                     d[r][0] = u0.x; d[r][1] = u0.y; d[r][2] = u1.x; d[r][3] = u1.y;
                 }
                 f32x4 av[2][4];
@@ -534,7 +576,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
                     for (int r = 0; r < 4; ++r)
 #pragma unroll
                         for (int c = 0; c < 4; ++c) d[r][c] = fmaxf(fmaf(d[r][c], st.x, st.y), 0.f);
-                    if constexpr (BRD) {
+                    if constexpr (BRD && !X4) {
 #pragma unroll
                         for (int c = 0; c < 4; ++c) {
                             d[0][c] *= fr0;
@@ -547,6 +589,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
                             d[r][2] *= fc2;
                             d[r][3] *= fc3;
                         }
+                    }
+                }
+                if constexpr (BRD && X4) {
+                    // the 16-byte copies bring the neighbouring rows' values into the out-of-image columns
+                    // (and, under BN + ReLU, relu(t) into the zero-copied rows): selects, not products (the
+                    // value before a tensor's first plane is the workspace's unwritten slack)
+                    if constexpr (PRO != PRO_RAW) {
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) {
+                            d[0][c] = fr0 != 0.f ? d[0][c] : 0.f;
+                            d[2][c] = fr2 != 0.f ? d[2][c] : 0.f;
+                            d[3][c] = fr3 != 0.f ? d[3][c] : 0.f;
+                        }
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        d[r][0] = fc0 != 0.f ? d[r][0] : 0.f;
+                        d[r][2] = fc2 != 0.f ? d[r][2] : 0.f;
+                        d[r][3] = fc3 != 0.f ? d[r][3] : 0.f;
                     }
                 }
                 // V = B^T d B (rows first, then columns): 32 additions
@@ -735,20 +796,28 @@ int launch_conv3x3_wino(int pro, int epi, ConvArgs a, hipStream_t s) {
     dim3 grid((unsigned)nwg);
     // pooled data gradient with 16-byte source rows
     const bool v4 = epi == EPI_BWD_POOL && (a.Ws & 3) == 0 && !(a.H & 1) && !(a.W & 1);
-#define PCX_WINO_CASE(P_, E_, CK_, V4_)                                                                 \
-    if (pro == P_ && epi == E_ && ck == CK_ && v4 == V4_) {                                             \
-        (void)hipFuncSetAttribute((const void*)conv_wino_kernel<P_, E_, CK_, V4_>,                      \
+    // 16-byte operand copies where the caller guarantees 4 readable bytes before src (PCX_WINO_X4=0: dword copies)
+    static const bool x4_env = getenv("PCX_WINO_X4") == nullptr || atoi(getenv("PCX_WINO_X4")) != 0;
+    // (not the pooled data gradient: its window registers already spill at 8-14 VGPRs; the two more
+    // copy offsets of X4 made that 31-34)
+    // measured at B = 4096 (profiles/r4_x4_time.txt): BN + ReLU forward and the data gradients gain
+    // 3-6 %, the raw-input forward (L3 / L5: 32 -> 64, 64 -> 128) nothing or -2.5 %: dword copies there
+    const bool x4 = ck == 8 && a.src_guard && x4_env && epi != EPI_BWD_POOL && !(pro == PRO_RAW && epi == EPI_FWD);
+#define PCX_WINO_CASE(P_, E_, CK_, V4_, X4_)                                                            \
+    if (pro == P_ && epi == E_ && ck == CK_ && v4 == V4_ && x4 == X4_) {                                \
+        (void)hipFuncSetAttribute((const void*)conv_wino_kernel<P_, E_, CK_, V4_, X4_>,                 \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);               \
-        conv_wino_kernel<P_, E_, CK_, V4_><<<grid, 256, smem, s>>>(a, g);                               \
+        conv_wino_kernel<P_, E_, CK_, V4_, X4_><<<grid, 256, smem, s>>>(a, g);                          \
         PCX_LAUNCH_CHECK("conv_wino_kernel");                                                           \
         return PCX_OK;                                                                                  \
     }
-#define PCX_WINO_CK(P_, E_, V4_) PCX_WINO_CASE(P_, E_, 8, V4_) PCX_WINO_CASE(P_, E_, 4, V4_)
+#define PCX_WINO_CK(P_, E_, V4_) PCX_WINO_CASE(P_, E_, 8, V4_, false) PCX_WINO_CASE(P_, E_, 4, V4_, false) \
+    PCX_WINO_CASE(P_, E_, 8, V4_, true)
     PCX_WINO_CK(PRO_RAW, EPI_FWD, false)
     PCX_WINO_CK(PRO_BNRELU, EPI_FWD, false)
     PCX_WINO_CK(PRO_RAW, EPI_BWD_RELU, false)
-    PCX_WINO_CK(PRO_RAW, EPI_BWD_POOL, false)
-    PCX_WINO_CK(PRO_RAW, EPI_BWD_POOL, true)
+    PCX_WINO_CASE(PRO_RAW, EPI_BWD_POOL, 8, false, false) PCX_WINO_CASE(PRO_RAW, EPI_BWD_POOL, 4, false, false)
+    PCX_WINO_CASE(PRO_RAW, EPI_BWD_POOL, 8, true, false) PCX_WINO_CASE(PRO_RAW, EPI_BWD_POOL, 4, true, false)
     PCX_WINO_CK(PRO_RAW, EPI_BWD_STORE, false)
 #undef PCX_WINO_CK
 #undef PCX_WINO_CASE

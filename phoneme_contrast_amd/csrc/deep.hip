@@ -296,6 +296,7 @@ int conv_bn_fwd(const Ctx& c, const char* label, int layer, const float* x, int 
         ConvArgs a{};
         a.B = c.p.B; a.H = OH; a.W = OW; a.cin = cin; a.cout = cout;
         a.src = x;
+        a.src_guard = 1;  // workspace tensor
         a.srcH = IH; a.srcW = IW;
         a.wpack = wp;
         a.out = y;
@@ -422,6 +423,7 @@ int conv_dgrad(const Ctx& c, int layer, const float* dy, int cout, int OH, int O
         ConvArgs a{};
         a.B = c.p.B; a.H = IH; a.W = IW; a.cin = cout; a.cout = cin;
         a.src = dy;
+        a.src_guard = 1;  // workspace tensor
         a.srcH = OH; a.srcW = OW;
         a.wpack = wp;
         a.out = dx;

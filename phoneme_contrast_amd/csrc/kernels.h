@@ -44,6 +44,7 @@ struct ConvArgs {
     int nblk;
     int NR, RS;           // staged rows / LDS row stride (host-computed)
     int accumulate;       // EPI_BWD_STORE: add into out instead of overwriting
+    int src_guard;        // 1: at least 4 readable bytes precede src (conv_wino's 16-byte staging copies)
 };
 
 size_t conv3x3_nblk(int B, int H, int W, int cout);
@@ -200,7 +201,8 @@ int launch_stem_wgrad(StemArgs a, int bf16, hipStream_t s);
 struct Wgrad1Args {
     int B, H, W, cout;
     const float* dz;
-    const float* y;
+    const float* y;       // the conv's output, or nullptr with w set: recomputed from x (bit-identical)
+    const float* w;       // [cout][9] conv weights (y == nullptr)
     const float4* cf_dy;
     const float* x;
     float* part;          // [nslice][cout][9]

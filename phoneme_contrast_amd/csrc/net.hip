@@ -196,6 +196,7 @@ int small_forward(const Plan& p, const float* const* P, float* const* bnstat, in
         c.part1 = part + (size_t)L.cout * L.nblk;
         c.partn = part + (size_t)2 * L.cout * L.nblk;
         c.nblk = L.wino ? L.nblk : (int)conv3x3_nblk(B, L.H, L.W, L.cout);
+        c.src_guard = 1;  // workspace tensors (and the input never reaches a 3x3 conv)
         int pro = PRO_BNRELU;
         if (L.pooled_in) {  // block tail materialised once; the conv and its wgrad read it raw
             Scope sc(&p.prof, s, "bn_relu_pool", l);
@@ -416,6 +417,7 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
             c.src2 = at<float>(ws, L.y);
             c.cf_in = at<float4>(ws, L.cfb);
             c.src = at<float>(ws, p.dyb);  // dy = BN backward of (dz, y), materialised by the weight gradient
+            c.src_guard = 1;
             c.srcH = L.H; c.srcW = L.W;
             c.wpack = at<float>(ws, L.wud);
             c.out = dzp;
@@ -442,7 +444,8 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
         Wgrad1Args w{};
         w.B = B; w.H = L.H; w.W = L.W; w.cout = L.cout;
         w.dz = at<float>(ws, L.dz);
-        w.y = at<float>(ws, L.y);
+        w.y = nullptr;  // y1 recomputed from the input window (bit-identical to conv1_fwd's): dz1 alone streamed
+        w.w = P[p_conv_w(1)];
         w.cf_dy = at<float4>(ws, L.cfb);
         w.x = x;
         w.part = wgp;
@@ -475,7 +478,7 @@ extern "C" void* pcx_net_create(const pcx_net_config* cfg, int64_t B, int64_t F,
     Plan* p = new Plan();
     p->cfg = *cfg;
     p->B = (int)B; p->F = (int)F; p->T = (int)T; p->D = cfg->embedding_dim;
-    p->total = 0;
+    p->total = 256;  // guard: every region has >= 256 readable workspace bytes in front of it (conv_wino X4)
     int rc = PCX_EINVAL;
     if (cfg->kind == PCX_NET_CNN_SMALL && cfg->conv_bf16)
         set_error("pcx_net_create: conv_bf16 is a PhonemeNetDeep option (cnn_small is float32)");

@@ -32,8 +32,11 @@ int main(int argc, char** argv) {
     if (epi != 0) pro = 0;
     const int Hs = epi == 2 ? 2 * H : H, Ws = epi == 2 ? 2 * W : W;
     size_t nx = (size_t)B * cin * H * W, ny = (size_t)B * cout * Hs * Ws, nw = (size_t)cout * cin * 9;
-    float *x, *w, *wp, *wu, *yp, *o1, *o2, *cfi, *cfo, *part, *drop;
-    (void)hipMalloc(&x, nx * 4); (void)hipMalloc(&w, nw * 4); (void)hipMalloc(&wp, nw * 4);
+    float *x, *xg, *w, *wp, *wu, *yp, *o1, *o2, *cfi, *cfo, *part, *drop;
+    // x behind a 64-float guard of NaNs: the Winograd conv's 16-byte staging reads the float before a
+    // plane (ConvArgs::src_guard) and must select it away, never multiply it in
+    (void)hipMalloc(&xg, (nx + 64) * 4); x = xg + 64; (void)hipMemset(xg, 0xff, 64 * 4);
+    (void)hipMalloc(&w, nw * 4); (void)hipMalloc(&wp, nw * 4);
     (void)hipMalloc(&wu, nw / 9 * 16 * 4); (void)hipMalloc(&yp, ny * 4);
     (void)hipMalloc(&o1, ny * 4); (void)hipMalloc(&o2, ny * 4);
     (void)hipMalloc(&cfi, cin * 16); (void)hipMalloc(&cfo, cout * 16); (void)hipMalloc(&drop, (size_t)B * cout * 4);
@@ -52,7 +55,7 @@ int main(int argc, char** argv) {
     a.srcH = H; a.srcW = W; a.yprev = yp; a.cf_out = (const float4*)cfo; a.drop_out = drop; a.Hs = Hs; a.Ws = Ws;
     pcx::ConvArgs d = a, q = a;
     d.wpack = wp; d.out = o1; d.nblk = (int)nbd; d.part0 = part; d.part1 = part + cout * nbd; d.partn = part + 2 * cout * nbd;
-    q.wpack = wu; q.out = o2; q.nblk = (int)nbw; q.part0 = part + (2 * cout * nbm + nbm);
+    q.wpack = wu; q.out = o2; q.nblk = (int)nbw; q.part0 = part + (2 * cout * nbm + nbm); q.src_guard = 1;
     q.part1 = q.part0 + cout * nbw; q.partn = q.part0 + 2 * cout * nbw;
     float msd = timeit(pcx::launch_conv3x3_dma, pro, epi, d, reps);
     float msw = timeit(pcx::launch_conv3x3_wino, pro, epi, q, reps);
