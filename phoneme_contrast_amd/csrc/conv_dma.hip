@@ -342,7 +342,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_occ(WM)
 template <int VEC>
 __global__ __launch_bounds__(256) void bn_relu_pool_kernel(const float* __restrict__ y, const float4* __restrict__ cf,
                                                            const float* __restrict__ drop, float* __restrict__ x,
-                                                           int nplanes, int C, int Hs, int Ws, int Hp, int Wp, int ppb) {
+                                                           int nplanes, int C, int Hs, int Ws, int Hp, int Wp, int ppb,
+                                                           float* __restrict__ ysel, uint8_t* __restrict__ parg) {
     const int Wq = (Wp + 3) / 4, nqp = Hp * Wq;
     const int pbase = blockIdx.x * ppb;
     const int tot = min(ppb, nplanes - pbase) * nqp;
@@ -375,18 +376,38 @@ __global__ __launch_bounds__(256) void bn_relu_pool_kernel(const float* __restri
                 v[e] = ok ? s1[e] : 0.f;
             }
         }
-        float out[4];
+        float out[4], ya[4];
+        unsigned ag = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const float m = fmaxf(fmaxf(fmaf(u[2 * j], k.x, k.y), fmaf(u[2 * j + 1], k.x, k.y)),
-                                  fmaxf(fmaf(v[2 * j], k.x, k.y), fmaf(v[2 * j + 1], k.x, k.y)));
-            out[j] = d * fmaxf(m, 0.f);
+            // first maximum of relu(BN) in window scan order (torch max_pool2d; the data gradient's rule)
+            const float q0 = fmaxf(fmaf(u[2 * j], k.x, k.y), 0.f), q1 = fmaxf(fmaf(u[2 * j + 1], k.x, k.y), 0.f);
+            const float q2 = fmaxf(fmaf(v[2 * j], k.x, k.y), 0.f), q3 = fmaxf(fmaf(v[2 * j + 1], k.x, k.y), 0.f);
+            float best = q0, yy = u[2 * j];
+            unsigned arg = 0;
+            if (q1 > best) { best = q1; arg = 1; yy = u[2 * j + 1]; }
+            if (q2 > best) { best = q2; arg = 2; yy = v[2 * j]; }
+            if (q3 > best) { best = q3; arg = 3; yy = v[2 * j + 1]; }
+            out[j] = d * best;
+            ya[j] = yy;
+            ag |= arg << (8 * j);
         }
-        float* dst = x + ((int64_t)bc * Hp + hp) * Wp + 4 * q;
+        const int64_t po = ((int64_t)bc * Hp + hp) * Wp + 4 * q;
+        float* dst = x + po;
         if ((Wp & 3) == 0) {
             st4(dst, make_float4(out[0], out[1], out[2], out[3]));
+            if (ysel) {
+                st4(ysel + po, make_float4(ya[0], ya[1], ya[2], ya[3]));
+                *reinterpret_cast<unsigned*>(parg + po) = ag;
+            }
         } else {
-            for (int j = 0; j < 4 && 4 * q + j < Wp; ++j) dst[j] = out[j];
+            for (int j = 0; j < 4 && 4 * q + j < Wp; ++j) {
+                dst[j] = out[j];
+                if (ysel) {
+                    ysel[po + j] = ya[j];
+                    parg[po + j] = (uint8_t)(ag >> (8 * j));
+                }
+            }
         }
     }
 }
@@ -477,18 +498,22 @@ int launch_conv3x3_dma(int pro, int epi, ConvArgs a, hipStream_t s) {
 }
 
 int launch_bn_relu_pool(const float* y, const float4* cf, const float* drop, float* x, int B, int C,
-                        int Hs, int Ws, hipStream_t s) {
+                        int Hs, int Ws, hipStream_t s, float* ysel, uint8_t* parg) {
+    PCX_CHECK_ARG((ysel == nullptr) == (parg == nullptr), "bn_relu_pool: ysel and parg go together");
     const int Hp = Hs / 2, Wp = Ws / 2;
     PCX_CHECK_ARG((int64_t)B * C < ((int64_t)1 << 31), "bn_relu_pool: too many planes");
     const int nplanes = B * C, nqp = Hp * ((Wp + 3) / 4);
     const int ppb = std::max(1, 1024 / std::max(1, nqp));  // ~1024 quads per block
     const int blocks = ceil_div(nplanes, ppb);
     if (Ws % 4 == 0)
-        bn_relu_pool_kernel<4><<<blocks, 256, 0, s>>>(y, cf, drop, x, nplanes, C, Hs, Ws, Hp, Wp, ppb);
+        bn_relu_pool_kernel<4><<<blocks, 256, 0, s>>>(y, cf, drop, x, nplanes, C, Hs, Ws, Hp, Wp, ppb, ysel,
+                                                     parg);
     else if (Ws % 2 == 0)
-        bn_relu_pool_kernel<2><<<blocks, 256, 0, s>>>(y, cf, drop, x, nplanes, C, Hs, Ws, Hp, Wp, ppb);
+        bn_relu_pool_kernel<2><<<blocks, 256, 0, s>>>(y, cf, drop, x, nplanes, C, Hs, Ws, Hp, Wp, ppb, ysel,
+                                                     parg);
     else
-        bn_relu_pool_kernel<1><<<blocks, 256, 0, s>>>(y, cf, drop, x, nplanes, C, Hs, Ws, Hp, Wp, ppb);
+        bn_relu_pool_kernel<1><<<blocks, 256, 0, s>>>(y, cf, drop, x, nplanes, C, Hs, Ws, Hp, Wp, ppb, ysel,
+                                                     parg);
     PCX_LAUNCH_CHECK("bn_relu_pool_kernel");
     return PCX_OK;
 }

@@ -286,6 +286,87 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
                 sz[j] = s_z;
                 sx[j] = s_x;
             }
+        } else if (EPI == EPI_BWD_POOLSEL) {
+            // the pooled data gradient from the forward's recorded selection: y at each window's selected
+            // element and its index (bn_relu_pool_kernel), read at the conv's (pooled) resolution -- a
+            // quarter of the full-resolution window reads; dz written at Hs x Ws as EPI_BWD_POOL does
+            const int HWs = a.Hs * a.Ws;
+            const int pixc = tvalid ? pix0 : 0;
+            const int row1 = ok[2] ? a.W : 0;
+            const float* ysb = a.ysel + ((int64_t)b * a.cout + n0) * HW + pixc;
+            const uint8_t* pab = a.parg + ((int64_t)b * a.cout + n0) * HW + pixc;
+            float* ob = a.out + ((int64_t)b * a.cout + n0) * HWs + (2 * h0) * a.Ws + 2 * w0;
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+                // four channels' loads together (one round trip per batch; registers)
+                float ys[4][4], dv[4];
+                unsigned ag[4];
+                float4 cf[4];
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    const int j = 4 * half + jj;
+                    const int co = 16 * (j >> 2) + 4 * kq + (j & 3);
+                    cf[jj] = a.cf_out[n0 + co];
+                    dv[jj] = a.drop_out ? a.drop_out[(int64_t)b * a.cout + n0 + co] : 1.f;
+                    const float* yp = ysb + (int64_t)co * HW;
+                    const uint8_t* pp = pab + (int64_t)co * HW;
+                    if (vec) {
+                        const float2 p0 = ld2(yp), p1 = ld2(yp + row1);
+                        ys[jj][0] = p0.x; ys[jj][1] = p0.y; ys[jj][2] = p1.x; ys[jj][3] = p1.y;
+                        ag[jj] = (unsigned)*reinterpret_cast<const uint16_t*>(pp) |
+                                 ((unsigned)*reinterpret_cast<const uint16_t*>(pp + row1) << 16);
+                    } else {
+                        ag[jj] = 0;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            ys[jj][e] = yp[ok[e] ? poff[e] : 0];
+                            ag[jj] |= (unsigned)pp[ok[e] ? poff[e] : 0] << (8 * e);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    const int j = 4 * half + jj;
+                    const int co = 16 * (j >> 2) + 4 * kq + (j & 3);
+                    float* op = ob + (int64_t)co * HWs;
+                    const float4 k = cf[jj];
+                    float dzw[4][4];
+                    float s_z = 0.f, s_x = 0.f;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int r0 = 2 * (e >> 1), c0 = 2 * (e & 1);
+                        const float ya = ys[jj][e];
+                        const unsigned arg = (ag[jj] >> (8 * e)) & 3u;
+                        // the window's maximum of relu(BN) is positive iff the selected element's BN output is
+                        const float dd = (ok[e] && fmaf(ya, k.x, k.y) > 0.f) ? y[j][e] * dv[jj] : 0.f;
+                        dzw[r0][c0] = arg == 0 ? dd : 0.f;
+                        dzw[r0][c0 + 1] = arg == 1 ? dd : 0.f;
+                        dzw[r0 + 1][c0] = arg == 2 ? dd : 0.f;
+                        dzw[r0 + 1][c0 + 1] = arg == 3 ? dd : 0.f;
+                        s_z += dd;
+                        s_x = fmaf(dd, (ya - k.z) * k.w, s_x);
+                    }
+                    if (V4) {
+                        if (tvalid)
+#pragma unroll
+                            for (int r = 0; r < 4; ++r)
+                                st4(op + r * a.Ws, make_float4(dzw[r][0], dzw[r][1], dzw[r][2], dzw[r][3]));
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            if (ok[e]) {
+                                const int r0 = 2 * (e >> 1), c0 = 2 * (e & 1);
+                                float* q = op + r0 * a.Ws + c0;
+                                q[0] = dzw[r0][c0];
+                                q[1] = dzw[r0][c0 + 1];
+                                q[a.Ws] = dzw[r0 + 1][c0];
+                                q[a.Ws + 1] = dzw[r0 + 1][c0 + 1];
+                            }
+                    }
+                    sz[j] = s_z;
+                    sx[j] = s_x;
+                }
+            }
         } else {  // EPI_BWD_POOL: the conv runs at the pooled resolution; dz lives at Hs x Ws
             const int HWs = a.Hs * a.Ws;
             constexpr int PB = V4 ? 1 : 2;  // channels per batch of window loads (registers)
@@ -782,9 +863,10 @@ int launch_conv3x3_wino(int pro, int epi, ConvArgs a, hipStream_t s) {
     PCX_CHECK_ARG(a.nblk == a.B * g.BPS, "conv3x3_wino: partial buffer sized for %d tiles, need %d", a.nblk,
                   a.B * g.BPS);
     PCX_CHECK_ARG(pro == PRO_RAW || pro == PRO_BNRELU, "conv3x3_wino: prologue %d", pro);
-    if (epi == EPI_BWD_POOL)
+    if (epi == EPI_BWD_POOL || epi == EPI_BWD_POOLSEL)
         PCX_CHECK_ARG(a.Hs >= 2 * a.H && a.Ws >= 2 * a.W, "conv3x3_wino: pooled source %dx%d for %dx%d", a.Hs, a.Ws,
                       a.H, a.W);
+    PCX_CHECK_ARG(epi != EPI_BWD_POOLSEL || (a.ysel && a.parg), "conv3x3_wino: EPI_BWD_POOLSEL needs ysel and parg");
     const int ck = wino_ck(a.cin);
     const size_t buff = (size_t)4 * (ck * WSP + 32) + (size_t)ck * 512;
     const size_t smem = (2 * buff + 2 * (size_t)a.cin + 512) * 4;
@@ -795,7 +877,7 @@ int launch_conv3x3_wino(int pro, int epi, ConvArgs a, hipStream_t s) {
     if (nwg >= 8) nwg &= ~(int64_t)7;
     dim3 grid((unsigned)nwg);
     // pooled data gradient with 16-byte source rows
-    const bool v4 = epi == EPI_BWD_POOL && (a.Ws & 3) == 0 && !(a.H & 1) && !(a.W & 1);
+    const bool v4 = (epi == EPI_BWD_POOL || epi == EPI_BWD_POOLSEL) && (a.Ws & 3) == 0 && !(a.H & 1) && !(a.W & 1);
     // 16-byte operand copies where the caller guarantees 4 readable bytes before src (PCX_WINO_X4=0: dword copies)
     static const bool x4_env = getenv("PCX_WINO_X4") == nullptr || atoi(getenv("PCX_WINO_X4")) != 0;
     // (not the pooled data gradient: its window registers already spill at 8-14 VGPRs; the two more
@@ -818,6 +900,8 @@ int launch_conv3x3_wino(int pro, int epi, ConvArgs a, hipStream_t s) {
     PCX_WINO_CK(PRO_RAW, EPI_BWD_RELU, false)
     PCX_WINO_CASE(PRO_RAW, EPI_BWD_POOL, 8, false, false) PCX_WINO_CASE(PRO_RAW, EPI_BWD_POOL, 4, false, false)
     PCX_WINO_CASE(PRO_RAW, EPI_BWD_POOL, 8, true, false) PCX_WINO_CASE(PRO_RAW, EPI_BWD_POOL, 4, true, false)
+    PCX_WINO_CK(PRO_RAW, EPI_BWD_POOLSEL, false)
+    PCX_WINO_CK(PRO_RAW, EPI_BWD_POOLSEL, true)
     PCX_WINO_CK(PRO_RAW, EPI_BWD_STORE, false)
 #undef PCX_WINO_CK
 #undef PCX_WINO_CASE

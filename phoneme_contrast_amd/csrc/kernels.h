@@ -17,6 +17,8 @@ enum Epilogue {
     EPI_BWD_RELU = 1,   // dz = acc * [yprev*s+t > 0]; store dz; sums of dz and dz*xhat
     EPI_BWD_POOL = 2,   // route acc (pooled res) through dropout, 2x2 argmax, ReLU to 2x res
     EPI_BWD_STORE = 3,  // dx = acc (or dx += acc with ConvArgs::accumulate); no statistics
+    EPI_BWD_POOLSEL = 4,  // EPI_BWD_POOL from the forward's recorded window selection (ysel / parg at the
+                          // pooled resolution: no full-resolution window reads; conv_wino only)
 };
 
 // 3x3 / stride 1 / pad 1 convolution as an implicit GEMM on v_mfma_f32_32x32x2_f32.
@@ -45,6 +47,8 @@ struct ConvArgs {
     int NR, RS;           // staged rows / LDS row stride (host-computed)
     int accumulate;       // EPI_BWD_STORE: add into out instead of overwriting
     int src_guard;        // 1: at least 4 readable bytes precede src (conv_wino's 16-byte staging copies)
+    const float* ysel;    // EPI_BWD_POOLSEL: y at each 2x2 window's selected element [B][cout][H][W] (pooled res)
+    const uint8_t* parg;  // EPI_BWD_POOLSEL: the selected element (0..3, row-major) of each window
 };
 
 size_t conv3x3_nblk(int B, int H, int W, int cout);
@@ -65,8 +69,10 @@ size_t wino_nblk(int B, int H, int W, int cin, int cout);
 int launch_wino_pack(const float* w, float* u, int M, int K, int flip, hipStream_t s);
 int launch_conv3x3_wino(int pro, int epi, ConvArgs a, hipStream_t s);
 // materialised block tail x = drop * maxpool2(relu(y*s + t)) (feeds PRO_RAW convs)
+// ysel / parg (optional, both or neither): y at each window's first maximum of relu(y s + t) (torch's
+// max_pool2d rule) and its index, for the EPI_BWD_POOLSEL data gradient
 int launch_bn_relu_pool(const float* y, const float4* cf, const float* drop, float* x, int B, int C,
-                        int Hs, int Ws, hipStream_t s);
+                        int Hs, int Ws, hipStream_t s, float* ysel = nullptr, uint8_t* parg = nullptr);
 
 // Cin = 1 convolution (first layer), 3x3 pad 1, with BN statistics.
 struct Conv1Args {

@@ -63,6 +63,12 @@ int build_small(Plan& p) {
             L.wu = p.carve("wu", (size_t)16 * L.cin * L.cout * 4);
             L.wud = p.carve("wud", (size_t)16 * L.cin * L.cout * 4);
             // the data gradient's tile blocks are the forward's (same H x W), so one nblk serves both
+            if (L.pooled_in && L.wino && getenv("PCX_NO_POOLSEL") == nullptr) {
+                snprintf(nm, sizeof nm, "ysel%d", l);
+                L.ysel = p.carve(nm, (size_t)B * L.cin * L.H * L.W * 4);
+                snprintf(nm, sizeof nm, "parg%d", l);
+                L.parg = p.carve(nm, (size_t)B * L.cin * L.H * L.W);
+            }
             L.nblk = L.wino ? (int)wino_nblk(B, L.H, L.W, L.cin, L.cout)
                             : (int)std::max(conv3x3_nblk(B, L.H, L.W, L.cout), conv3x3_nblk(B, L.H, L.W, L.cin));
             L.wgw = wgrad_wino_geometry(B, L.H, L.W, L.cin, L.cout, &L.ww);
@@ -201,7 +207,8 @@ int small_forward(const Plan& p, const float* const* P, float* const* bnstat, in
         if (L.pooled_in) {  // block tail materialised once; the conv and its wgrad read it raw
             Scope sc(&p.prof, s, "bn_relu_pool", l);
             RC(launch_bn_relu_pool(c.src, c.cf_in, c.drop_in, at<float>(ws, L.xp), B, L.cin, L.srcH,
-                                   L.srcW, s));
+                                   L.srcW, s, L.ysel ? at<float>(ws, L.ysel) : nullptr,
+                                   L.parg ? at<uint8_t>(ws, L.parg) : nullptr));
             c.src = at<float>(ws, L.xp);
             c.srcH = L.H; c.srcW = L.W;
             pro = PRO_RAW;
@@ -431,7 +438,12 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
             c.nblk = nblk;
             {
                 Scope sc(&p.prof, s, "conv_dgrad", l);
-                const int epi = L.pooled_in ? EPI_BWD_POOL : EPI_BWD_RELU;
+                // pooled input with a recorded selection: the epilogue reads it at the pooled resolution
+                const int epi = !L.pooled_in ? EPI_BWD_RELU : L.ysel ? EPI_BWD_POOLSEL : EPI_BWD_POOL;
+                if (epi == EPI_BWD_POOLSEL) {
+                    c.ysel = at<float>(ws, L.ysel);
+                    c.parg = at<uint8_t>(ws, L.parg);
+                }
                 RC(L.wino ? launch_conv3x3_wino(PRO_RAW, epi, c, s) : launch_conv3x3_dma(PRO_RAW, epi, c, s));
             }
             RC(bwd_finalize(l - 1, nblk, (double)B * Lp.H * Lp.W));

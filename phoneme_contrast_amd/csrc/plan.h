@@ -128,6 +128,8 @@ struct Layer {  // one 3x3 conv of the trunk (L = 1..6)
     int drop_idx;          // dropout layer feeding its input (pooled_in) or -1
     size_t y, dz, cf, cfb, wu, wud;  // workspace offsets (wu / wud: Winograd weights, forward / data gradient)
     size_t xp;             // pooled_in: materialised input drop * maxpool2(relu(bn(y_prev)))
+    size_t ysel, parg;     // pooled_in + wino: each window's selected y_prev (f32) and its index (u8), recorded
+                           // by the forward's pool for the data gradient's EPI_BWD_POOLSEL epilogue
     int nblk;              // forward statistics tiles
     bool wino;             // Winograd conv (W >= 31); else the direct LDS-DMA conv (wu / wud then hold
                            // the [9][cin][cout] / flipped [9][cout][cin] packings)

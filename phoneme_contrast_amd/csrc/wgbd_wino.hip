@@ -26,7 +26,7 @@
 // strip's columns plus a one-column halo on either side (position p <-> image column 2 t0 - 1 + p): the
 // data gradient's 4 x 4 dy patches and the weight gradient's x patches are two aligned ds_read_b64 per
 // row; the weight gradient's 2 x 2 dy values are the middle pair of the same reads.  The next tile row's
-// two rows of dz, y, y_prev are loaded into registers at the start of the row (a row of MFMAs to land),
+// two rows of dz, y, y_prev are loaded into registers over the row's groups (spread: no issue burst),
 // turned into dy / x and stored after the row's last group.  Out-of-image items load 0 (buffer offsets
 // beyond num_records) and stage exact zeros.  Strips are 48 / 52 tiles at W = 200 (the data gradient
 // runs 16-tile groups: 7 groups per tile row, 12 % padding).
@@ -208,7 +208,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
             return colok & (((unsigned)r0 < (unsigned)H ? ~R1 : 0u) | ((unsigned)r1 < (unsigned)H ? R1 : 0u));
         };
         auto goff = [&](int m, int st) { return ch * HW + (2 * st + 1 + m / NIR) * W + c0 - V + V * (j0 + 16 * (m % NIR)); };
-        auto load = [&](int st) {
+        // items of stage st loaded at group gi of ngr (all of them for ngr = 0): the next tile row's loads
+        // are spread over the current row's groups (a burst of 3 NIT loads per wave at the row start stalls
+        // the issuing waves of every SIMD on the texture unit, MFMA pipes idle)
+        auto load = [&](int st, int gi, int ngr) {
 #if defined(WB_KO) && (WB_KO & 8)  // analysis builds only (tools/wb_ko.sh): no staging loads
             for (int m = 0; m < NIT; ++m) dzv[m] = yv[m] = xv[m] = vecf<V>(0.f);
             return;
@@ -216,6 +219,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
             const unsigned ok = rowmask(st);
 #pragma unroll
             for (int m = 0; m < NIT; ++m) {
+                if (ngr && (m * ngr) / NIT != gi) continue;
                 const int o = (ok >> m) & 1 ? 4 * goff(m, st) : OOB;
                 dzv[m] = bload<V>(rdz, o);
                 yv[m] = bload<V>(ry, o);
@@ -260,20 +264,20 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
         };
 
         // task prologue: stage -1 (rows -1, 0) and stage 0 (rows 1, 2)
-        load(-1);
+        load(-1, 0, 0);
         store(-1);
-        load(0);
+        load(0, 0, 0);
         store(0);
         __syncthreads();
 
         for (int tr = 0; tr < TR; ++tr) {
             const bool pre = tr + 1 < TR;
-            if (pre) load(tr + 1);
             // ring rows of this tile row: patch row i (image row 2 tr - 1 + i) in slot (2 tr + i) & 3
             const int sw = ((2 * tr + IW) & 3) * CH * XCS, su = ((2 * tr + IU) & 3) * CH * XCS;
             float rz[2] = {0.f, 0.f}, rx_[2] = {0.f, 0.f};  // this row's BN sums (data-gradient epilogue)
             float ex[2][4];                                  // the epilogue's x values (prefetched)
             for (int g = 0; g < ng; ++g) {
+                if (pre) load(tr + 1, g, ng);
                 if constexpr (!DG) {
 #if !(defined(WB_KO) && (WB_KO & 1))
                     // ---- weight gradient: K-steps 8 g .. 8 g + 7 (tiles 16 g .. 16 g + 15)

@@ -130,6 +130,7 @@ template <int PRO, int V>
 __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int co0, int ci0, int slice) {
     const int tid = threadIdx.x, lane = tid & 63, c32 = lane & 31, g = lane >> 5;
     const int Q = __builtin_amdgcn_readfirstlane(tid >> 6);
+    constexpr int NPT = V == 4 ? 2 : 4;  // parts of the next tile row's loads (V = 4: 4 parts spill)
     const int XCS = a.XCS, DCS = a.DCS;
     float* const xl = smem + 4;                   // [4 ring slots][32][XCS]
     float* const dyl = xl + 4 * 32 * XCS;         // [2 rows][32][DCS]
@@ -198,13 +199,16 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
         };
         auto dgo = [&](int i) { return dgb + (i / NIR) * W + 8 * V * (i % NIR); };
         auto xgo = [&](int i) { return xgb + (i / NIR) * W + 8 * V * (i % NIR); };
-        auto load_dy = [&](int st) {
+        // part: only the items m with m NPT / NIT == part (-1: all items)
+        auto load_dy = [&](int st, int part) {
             unsigned dm, xm;
             masks(st, dm, xm);
-            const int db = 2 * st * W + c0;
+            int db = 2 * st * W + c0 + dgb;
+            asm volatile("" : "+v"(db));  // opaque: per-item offsets formed at the load, not kept live
 #pragma unroll
             for (int m = 0; m < NIT; ++m) {
-                const int o = (dm >> m) & 1 ? 4 * (dgo(m) + db) : OOB;
+                if (part >= 0 && m * NPT / NIT != part) continue;
+                const int o = (dm >> m) & 1 ? 4 * (dgo(m) - dgb + db) : OOB;
                 dzv[m] = bload<V>(rdz, o);
                 yv[m] = bload<V>(ry, o);
             }
@@ -220,12 +224,14 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
                 for (int e = 0; e < V; ++e) dzv[m][e] = fma1(A1, dzv[m][e], fma1(A2, yv[m][e], a3));
             }
         };
-        auto load_x = [&](int st) {
+        auto load_x = [&](int st, int part) {
             unsigned dm, xm;
             masks(st, dm, xm);
-            const int xb = (2 * st + 1) * W + c0;
+            int xb = (2 * st + 1) * W + c0 + xgb;
+            asm volatile("" : "+v"(xb));
 #pragma unroll
-            for (int m = 0; m < NIT; ++m) xv[m] = bload<V>(rx, (xm >> m) & 1 ? 4 * (xgo(m) + xb) : OOB);
+            for (int m = 0; m < NIT; ++m)
+                if (part < 0 || m * NPT / NIT == part) xv[m] = bload<V>(rx, (xm >> m) & 1 ? 4 * (xgo(m) - xgb + xb) : OOB);
         };
         auto store_x = [&](int st, const vecf<V> (&xr)[NIT]) {
             unsigned dm, xm;
@@ -272,8 +278,8 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
 
         // task prologue: stages -1 and 0 (x rows -1 .. 2, dy rows 0, 1) loaded together: one round trip
         {
-            load_dy(0);
-            load_x(0);
+            load_dy(0, -1);
+            load_x(0, -1);
             vecf<V> xa[NIT];  // stage -1: x rows -1 (zeros: the ring slot holds the previous task's rows), 0
             unsigned dm, xm;
             masks(-1, dm, xm);
@@ -303,15 +309,22 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
         const int Ks = a.Ksteps;
         for (int tr = 0; tr < TR; ++tr) {
             const bool pre = tr + 1 < TR;
-            // the next tile row's dz / y / x rows now (a whole row of MFMAs to land), dy formed after
-            if (pre) {
-                load_dy(tr + 1);
-                load_x(tr + 1);
-            }
             // x rows 2 tr - 1 + i of this tile row live in ring slot (2 tr + i) & 3
             const float* xw = xl + ((2 * tr + IW) & 3) * 32 * XCS + c32 * XCS + 2 * g;
             const float* xu = xl + ((2 * tr + IU) & 3) * 32 * XCS + c32 * XCS + 2 * g;
-            ksteps(xw, xu, 0, Ks);
+            // the next tile row's dz / y / x rows loaded over this row's K-steps in NPT parts (a
+            // burst of 3 NIT loads at the row start stalls the issuing waves on the texture unit, MFMA
+            // pipes idle); dy formed after the last part
+#pragma unroll
+            for (int pt = 0; pt < NPT; ++pt) {
+                __builtin_amdgcn_sched_barrier(0);  // (no hoisting of later parts' loads: registers)
+                if (pre) {
+                    load_dy(tr + 1, pt);
+                    load_x(tr + 1, pt);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                ksteps(xw, xu, Ks * pt / NPT, Ks * (pt + 1) / NPT);
+            }
             if (pre) form_dy(tr + 1);
             __syncthreads();  // the dy rows and the two oldest x rows are free
             if (pre) store(tr + 1);

@@ -1,7 +1,8 @@
 """Cross-check of the Winograd F(2x2,3x3) conv's fused epilogues (csrc/conv_wino.hip) against the
 direct LDS-DMA conv (csrc/conv_dma.hip) on the same operands, at the cnn_small layer shapes:
 forward with the producer's BN+ReLU prologue and the BN (sum, M2) partials, the data gradient
-through ReLU + BN-backward sums, through MaxPool2 + Dropout2d (16-byte and scalar window paths),
+through ReLU + BN-backward sums, through MaxPool2 + Dropout2d (16-byte and scalar window paths; and from the selection the
+forward's pool recorded, EPI_BWD_POOLSEL),
 and plain store.  tools/wino_bench (built by `make`) runs both engines and exits 2 when the outputs
 differ by more than 1e-5 of max|out| or the per-channel partial sums by more than 1e-4 (fp32
 rounding of two exact-arithmetic conv algorithms).  The direct engine is pinned to the reference by
@@ -22,6 +23,9 @@ CASES = [  # H, W, cin, cout, B, reps, epilogue, prologue
     (40, 200, 32, 32, 48, 1, 1, 0),    # L2 data gradient through ReLU
     (20, 100, 64, 32, 48, 1, 2, 0),    # L3 data gradient through MaxPool2 (16-byte windows)
     (10, 50, 128, 64, 48, 1, 2, 0),    # L5 data gradient through MaxPool2
+    (20, 100, 64, 32, 48, 1, 4, 0),    # L3 through MaxPool2 from the forward's recorded selection
+    (10, 50, 128, 64, 48, 1, 4, 0),    # L5 likewise
+    (20, 101, 64, 32, 24, 1, 4, 0),    # odd pooled width: scalar windows and stores
     (40, 201, 32, 32, 24, 1, 0, 1),    # T = 201: odd width, scalar stores
     (40, 201, 32, 32, 24, 1, 1, 0),
     (20, 100, 64, 64, 24, 1, 3, 0),    # plain store (cnn_deep's stride-1 data gradients)

@@ -1,6 +1,8 @@
 // Standalone timing + cross-check of the Winograd conv (conv_wino.hip) against the direct LDS-DMA
 // conv (conv_dma.hip) on one layer shape and epilogue (analysis aid).
-//   wino_bench H W cin cout [B] [reps] [epi] [pro]     epi: 0 fwd, 1 bwd relu, 2 bwd pool, 3 store
+//   wino_bench H W cin cout [B] [reps] [epi] [pro]     epi: 0 fwd, 1 bwd relu, 2 bwd pool, 3 store,
+//                                                      4 bwd pool from the recorded selection (Winograd
+//                                                      EPI_BWD_POOLSEL vs the direct engine's EPI_BWD_POOL)
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -30,6 +32,8 @@ int main(int argc, char** argv) {
     int B = argc > 5 ? atoi(argv[5]) : 4096, reps = argc > 6 ? atoi(argv[6]) : 5;
     int epi = argc > 7 ? atoi(argv[7]) : 0, pro = argc > 8 ? atoi(argv[8]) : 1;
     if (epi != 0) pro = 0;
+    const bool sel = epi == 4;
+    if (sel) epi = 2;  // the direct engine's epilogue; the Winograd one reads ysel / parg instead
     const int Hs = epi == 2 ? 2 * H : H, Ws = epi == 2 ? 2 * W : W;
     size_t nx = (size_t)B * cin * H * W, ny = (size_t)B * cout * Hs * Ws, nw = (size_t)cout * cin * 9;
     float *x, *xg, *w, *wp, *wu, *yp, *o1, *o2, *cfi, *cfo, *part, *drop;
@@ -57,10 +61,23 @@ int main(int argc, char** argv) {
     d.wpack = wp; d.out = o1; d.nblk = (int)nbd; d.part0 = part; d.part1 = part + cout * nbd; d.partn = part + 2 * cout * nbd;
     q.wpack = wu; q.out = o2; q.nblk = (int)nbw; q.part0 = part + (2 * cout * nbm + nbm); q.src_guard = 1;
     q.part1 = q.part0 + cout * nbw; q.partn = q.part0 + 2 * cout * nbw;
+    int qepi = epi;
+    if (sel) {  // the forward's pool records each window's selected y and its index
+        float *xp, *ys;
+        uint8_t* pa;
+        const size_t np = (size_t)B * cout * H * W;
+        (void)hipMalloc(&xp, np * 4); (void)hipMalloc(&ys, np * 4); (void)hipMalloc(&pa, np);
+        if (pcx::launch_bn_relu_pool(yp, (const float4*)cfo, drop, xp, B, cout, Hs, Ws, 0, ys, pa)) {
+            printf("bn_relu_pool failed\n");
+            return 1;
+        }
+        q.ysel = ys; q.parg = pa; qepi = pcx::EPI_BWD_POOLSEL;
+        printf("wino EPI_BWD_POOL %.3f ms; ", timeit(pcx::launch_conv3x3_wino, pro, epi, q, reps));
+    }
     float msd = timeit(pcx::launch_conv3x3_dma, pro, epi, d, reps);
-    float msw = timeit(pcx::launch_conv3x3_wino, pro, epi, q, reps);
+    float msw = timeit(pcx::launch_conv3x3_wino, pro, qepi, q, reps);
     (void)hipMemset(o1, 0, ny * 4); (void)hipMemset(o2, 0, ny * 4);
-    pcx::launch_conv3x3_dma(pro, epi, d, 0); pcx::launch_conv3x3_wino(pro, epi, q, 0);
+    pcx::launch_conv3x3_dma(pro, epi, d, 0); pcx::launch_conv3x3_wino(pro, qepi, q, 0);
     (void)hipDeviceSynchronize();
     std::vector<float> h1(ny), h2(ny);
     (void)hipMemcpy(h1.data(), o1, ny * 4, hipMemcpyDeviceToHost); (void)hipMemcpy(h2.data(), o2, ny * 4, hipMemcpyDeviceToHost);
@@ -81,8 +98,8 @@ int main(int argc, char** argv) {
         }
     }
     double fl = 2.0 * B * H * W * cin * cout * 9;
-    printf("H%d W%d %d->%d epi%d pro%d: direct %.3f ms (%.2f of fp32 roof)  wino %.3f ms (%.2f alg.)  |d out| %.2e of %.2e  |d sum0| %.2e of %.2e\n",
-           H, W, cin, cout, epi, pro, msd, fl / msd / 1e9 / 157.3, msw, fl / msw / 1e9 / 157.3, emax, gmax, smax, sref);
+    printf("H%d W%d %d->%d epi%d%s pro%d: direct %.3f ms (%.2f of fp32 roof)  wino %.3f ms (%.2f alg.)  |d out| %.2e of %.2e  |d sum0| %.2e of %.2e\n",
+           H, W, cin, cout, epi, sel ? "sel" : "", pro, msd, fl / msd / 1e9 / 157.3, msw, fl / msw / 1e9 / 157.3, emax, gmax, smax, sref);
     // exit status: 2 when the outputs or the summed statistics partials disagree beyond fp32 noise
     const bool bad = emax > 1e-5 * gmax + 1e-6 || smax > 1e-4 * sref + 1e-3;
     return bad ? 2 : 0;
