@@ -31,6 +31,11 @@ from phoneme_contrast_amd.costs import (BF16_PEAK_TFLOPS, DEEP_DIMS, FP32_PEAK_T
 METRIC = "MFCC-samples/sec per train step (cnn_small, batch 4096) at 1/2/4/8 MI355X"
 
 
+def sig(x, n=4):
+    """x to n significant digits (a contended or tiny launch must not round to 0)."""
+    return float(f"{x:.{n}g}")
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -274,12 +279,12 @@ def main():
         ai = fl / by
         if ai > peak * 1e12 / (HBM_PEAK_GBS * 1e9):
             ach = fl / avg_s / 1e12
-            roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": peak,
-                    "unit": "TFLOP/s", "frac": round(ach / peak, 4)}
+            roof = {"kernel": dom, "bound": "mfma", "achieved": sig(ach), "peak": peak,
+                    "unit": "TFLOP/s", "frac": sig(ach / peak)}
         else:
             ach = by / avg_s / 1e9
-            roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4)}
+            roof = {"kernel": dom, "bound": "hbm", "achieved": sig(ach), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": sig(ach / HBM_PEAK_GBS)}
         roof["traffic"] = load_pmc(args.model, args.precision if deep else "fp32", dom)
         roof["algorithmic_flops_per_launch"] = fl
         roof["algorithmic_bytes_per_launch"] = by
@@ -290,7 +295,7 @@ def main():
             # cnn_small's 3x3 convs run Winograd F(2x2,3x3): 4/9 of the direct multiplies are executed
             xf = executed_fraction(dom, T)
             roof["executed_flops_per_launch"] = int(fl * xf)
-            roof["executed_frac"] = round(roof["frac"] * xf, 4)
+            roof["executed_frac"] = sig(roof["frac"] * xf)
         for lab, rec in kernels.items():  # per-kernel achieved rates for every costed label
             if lab in costs:
                 f_, b_ = costs[lab]

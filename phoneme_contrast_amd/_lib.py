@@ -10,7 +10,9 @@ import threading
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpcx.so")
+# PCX_LIB_PATH: an alternative build of the same library (same-box A/B timing of kernel variants,
+# scripts/ab_bench.sh); unset, the in-tree library
+LIB_PATH = os.environ.get("PCX_LIB_PATH") or os.path.join(_HERE, "libpcx.so")
 
 PCX_OK = 0
 PCX_EINVAL = -1

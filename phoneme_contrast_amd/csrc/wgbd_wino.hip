@@ -277,7 +277,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
             float rz[2] = {0.f, 0.f}, rx_[2] = {0.f, 0.f};  // this row's BN sums (data-gradient epilogue)
             float ex[2][4];                                  // the epilogue's x values (prefetched)
             for (int g = 0; g < ng; ++g) {
-                if (pre) load(tr + 1, g, ng);
+#ifndef WB_LOADPOS
+#define WB_LOADPOS 0
+#endif
+                // the next tile row's staging loads: spread over the groups, at the group start (analysis
+                // builds: WB_LOADPOS 1 = data-gradient waves after the group's MFMAs, 2 = all items at once,
+                // weight-gradient waves at group 0, data-gradient waves after group 1's MFMAs)
+                if (pre && (WB_LOADPOS == 0 || (WB_LOADPOS == 1 && !DG))) load(tr + 1, g, ng);
+                if (pre && WB_LOADPOS == 2 && !DG && g == 0) load(tr + 1, 0, 0);
                 if constexpr (!DG) {
 #if !(defined(WB_KO) && (WB_KO & 1))
                     // ---- weight gradient: K-steps 8 g .. 8 g + 7 (tiles 16 g .. 16 g + 15)
@@ -345,6 +352,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
                             *reinterpret_cast<f2*>(xo + (c * 16 + t_l) * 8 + 2 * Q) = f2{m0, m1};
                         }
 #endif
+                    if (pre && WB_LOADPOS == 1) load(tr + 1, g, ng);
+                    if (pre && WB_LOADPOS == 2 && g == min(1, ng - 1)) load(tr + 1, 0, 0);
                     // the epilogue's x values (rows 2 tr, 2 tr + 1 = ring slots of patch rows 1, 2) read
                     // before the barrier: after the last group's barrier the next stage overwrites row 2 tr
                     const int so1 = ((2 * tr + 1) & 3) * CH * XCS, so2 = ((2 * tr + 2) & 3) * CH * XCS;
