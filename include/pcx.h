@@ -143,6 +143,9 @@ int pcx_net_backward(const void* plan, const float* const* params, const float* 
  * recorded events, returns the number of distinct kernel labels and fills '\n'-separated labels,
  * total milliseconds and launch counts per label, then clears. */
 int pcx_net_profile(void* plan, int enable);
+/* Restrict the recording to one kernel label (e.g. "wgbd_L2"; NULL or "": every label): a timed
+ * region then carries one event pair per launch of that kernel instead of one per launch. */
+int pcx_net_profile_only(void* plan, const char* label);
 int pcx_net_profile_read(void* plan, char* labels, size_t labels_len, float* total_ms,
                          int* counts, int max_entries);
 

@@ -72,6 +72,7 @@ SIGNATURES = {
     "pcx_net_backward": (c_int, [c_void_p, _pp, c_void_p, _pp, c_void_p, c_void_p, _pp, c_void_p,
                                  c_size, c_void_p]),
     "pcx_net_profile": (c_int, [c_void_p, c_int]),
+    "pcx_net_profile_only": (c_int, [c_void_p, ctypes.c_char_p]),
     "pcx_net_grad_buckets": (c_int, [c_void_p, c_int, _pi]),
     "pcx_net_bucket_wait": (c_int, [c_void_p, c_int, c_void_p]),
     "pcx_net_grad_stages": (c_int, [c_void_p, _pi, c_int]),

@@ -613,6 +613,13 @@ extern "C" int pcx_net_profile(void* plan, int enable) {
     return PCX_OK;
 }
 
+extern "C" int pcx_net_profile_only(void* plan, const char* label) {
+    using namespace pcx;
+    PCX_CHECK_ARG(plan, "pcx_net_profile_only: NULL plan");
+    static_cast<Plan*>(plan)->prof.only = label ? label : "";
+    return PCX_OK;
+}
+
 extern "C" int pcx_net_profile_read(void* plan, char* labels, size_t labels_len, float* total_ms,
                                     int* counts, int max_entries) {
     using namespace pcx;

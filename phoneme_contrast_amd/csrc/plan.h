@@ -21,6 +21,7 @@ struct Region {
 // on the stream they run on, inside its timed region.
 struct Profiler {
     bool on = false;
+    std::string only;  // record this label alone (empty: every label)
     std::vector<hipEvent_t> pool;
     size_t used = 0;
     std::vector<std::string> labels;
@@ -82,13 +83,13 @@ struct Scope {
             r.push(label.c_str());
             tx = true;
         }
-        if (!p->on) return;
+        if (!p->on || (!p->only.empty() && label != p->only)) return;
         a = p->get();
         if (a) (void)hipEventRecord(a, s);
     }
     ~Scope() {
         if (tx) Roctx::get().pop();
-        if (!p->on || !a) return;
+        if (!a) return;
         hipEvent_t b = p->get();
         if (!b) return;
         (void)hipEventRecord(b, s);

@@ -142,17 +142,23 @@ class _NativeNet(BaseModel):
             p = _Plan(self._net_config(), B, F, T)
             if getattr(self, "_profiling", False):
                 _lib.check(_lib.lib().pcx_net_profile(p.handle, 1), "pcx_net_profile")
+                only = getattr(self, "_profile_only", None)
+                _lib.check(_lib.lib().pcx_net_profile_only(p.handle, only.encode() if only else None),
+                           "pcx_net_profile_only")
             if p.nparams != len(list(self.parameters())):
                 raise RuntimeError("native plan / module parameter count mismatch")
             self._plans[key] = p
         return p
 
-    def kernel_profile(self, enable: bool = True):
-        """Start (or stop) per-launch HIP-event timing of the native kernels (all cached plans)."""
+    def kernel_profile(self, enable: bool = True, only: Optional[str] = None):
+        """Start (or stop) per-launch HIP-event timing of the native kernels (all cached plans);
+        only: record that kernel label alone (one event pair per launch of it)."""
         lib = _lib.lib()
         self._profiling = bool(enable)
+        self._profile_only = only
         for p in self._plans.values():
             _lib.check(lib.pcx_net_profile(p.handle, 1 if enable else 0), "pcx_net_profile")
+            _lib.check(lib.pcx_net_profile_only(p.handle, only.encode() if only else None), "pcx_net_profile_only")
 
     def kernel_profile_read(self):
         """{kernel label: (total_ms, launches)} since kernel_profile(True); waits for the events."""
