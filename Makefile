@@ -44,7 +44,26 @@ build/wgbd_wino.o: CXXFLAGS += -fno-slp-vectorize
 $(LIB): $(OBJ)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJ)
 
-clean:
-	rm -rf build $(LIB) $(TOOLS)
+# host-side sanitizer build (no GPU): every source compiled host-only with ASan + UBSan, linked with the
+# plan-builder check tools/plan_check.cpp (tests/test_plan_asan.py runs it)
+ASAN_FLAGS = -O1 -g -std=c++17 --offload-arch=$(ARCH) -fPIC -Iinclude -Xarch_host -fsanitize=address \
+             -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer -Xarch_host -fno-sanitize-recover=all
+ASAN_OBJ = $(patsubst phoneme_contrast_amd/csrc/%.hip,build_asan/%.o,$(SRC))
 
-.PHONY: all clean
+build_asan/%.o: phoneme_contrast_amd/csrc/%.hip $(HDR)
+	@mkdir -p build_asan
+	$(HIPCC) $(ASAN_FLAGS) -c $< -o $@
+
+build_asan/plan_check.o: tools/plan_check.cpp include/pcx.h
+	@mkdir -p build_asan
+	$(HIPCC) $(ASAN_FLAGS) -c $< -o $@
+
+tools/plan_check_asan: build_asan/plan_check.o $(ASAN_OBJ)
+	$(HIPCC) -fsanitize=address,undefined build_asan/plan_check.o $(ASAN_OBJ) -o $@
+
+asan: tools/plan_check_asan
+
+clean:
+	rm -rf build build_asan $(LIB) $(TOOLS) tools/plan_check_asan
+
+.PHONY: all asan clean
