@@ -18,6 +18,7 @@
 //    pixel-major ([k][channels], 16-byte runs) and read K-contiguous by ds_read_b64_tr_b16.
 // Operand rounding (bf16 round-to-nearest-even of the float32 value) and float32 accumulation are
 // those of convg_bf16; only the summation order differs.
+#include "conv_epilogue.h"
 #include "kernels.h"
 
 namespace pcx {
@@ -364,6 +365,62 @@ __global__ __launch_bounds__(256) void convn_kernel(ConvGArgs a) {
                 }
             }
     }
+    if (MODE == 0 && a.st_part0 != nullptr) {
+        // BN forward partials of the tile (replaces the statistics pass over out): per (wave, channel)
+        // Chan statistics of its 64 pixels about the channel's first pixel in the wave (K, v_readlane),
+        // reduced over the lanes with the transposed butterfly, then the two pixel halves merged
+        __syncthreads();  // every wave is done with the operand stages: the LDS holds the exchange
+        float* red = reinterpret_cast<float*>(smem);
+        const int64_t nw0 = n0 + wc * 32 * WN;
+        const int cnt_w = (int)max((int64_t)0, min((int64_t)(32 * WN), N - nw0));
+        bool valid[WN];
+#pragma unroll
+        for (int ni = 0; ni < WN; ++ni) valid[ni] = nw0 + ni * 32 + l32 < N;
+#pragma unroll
+        for (int mi = 0; mi < WM; ++mi) {
+            float kv[16], s1[16], s2[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float k0 = readlane_f(acc[mi][0][r], 0), k1 = readlane_f(acc[mi][0][r], 32);
+                kv[r] = h ? k1 : k0;
+                s1[r] = 0.f;
+                s2[r] = 0.f;
+#pragma unroll
+                for (int ni = 0; ni < WN; ++ni)
+                    if (valid[ni]) {
+                        const float d = acc[mi][ni][r] - kv[r];
+                        s1[r] += d;
+                        s2[r] = fmaf(d, d, s2[r]);
+                    }
+            }
+            const float t1 = xsum16(s1, l32), t2 = xsum16(s2, l32), K = xsel16(kv, l32);
+            if (!(l32 & 1)) {
+                const float n = (float)cnt_w;
+                float* d = red + (wc * BM + wr * 32 * WM + mi * 32 + acc_row(l32 >> 1, h)) * 3;
+                d[0] = n;
+                d[1] = cnt_w ? K + t1 / n : 0.f;
+                d[2] = cnt_w ? fmaxf(t2 - t1 * t1 / n, 0.f) : 0.f;
+            }
+        }
+        __syncthreads();
+        if (tid < BM && m0 + tid < M) {
+            float n = 0.f, mean = 0.f, m2 = 0.f;
+#pragma unroll
+            for (int w = 0; w < 2; ++w) {
+                const float* d = red + (w * BM + tid) * 3;
+                if (d[0] > 0.f) {
+                    const float nt = n + d[0], delta = d[1] - mean;
+                    mean += delta * d[0] / nt;
+                    m2 += d[2] + delta * delta * n * d[0] / nt;
+                    n = nt;
+                }
+            }
+            const int64_t ntile = (N + BN - 1) / BN;
+            a.st_part0[(m0 + tid) * ntile + tn] = n * mean;
+            a.st_part1[(m0 + tid) * ntile + tn] = m2;
+            if (tid == 0 && tm == 0) a.st_partn[tn] = n;
+        }
+    }
 }
 
 // ------------------------------------------------------------------ weight gradient
@@ -576,6 +633,8 @@ int launch_to_nhwc(NhwcArgs a, hipStream_t s) {
 // 14 % faster than 32 on the 256-channel layers) where the channel count allows
 static int convn_kc(int ck) { return ck % 64 == 0 ? 64 : 32; }
 
+int64_t convn_stat_tiles(const ConvGArgs& a) { return ceil_div((int64_t)a.B * a.OH * a.OW, 128); }
+
 bool convn_fits(const ConvGArgs& a) {
     if (a.KH != a.KW || (a.KH != 1 && a.KH != 3) || a.pad > 1 || a.pad < 0) return false;
     if (a.mode == 2) return a.cin % 8 == 0 && a.cout % 8 == 0;
@@ -631,6 +690,8 @@ int launch_convn(const ConvGArgs& a, hipStream_t s) {
     }
     const int wm = M >= 128 ? 2 : 1;
     constexpr int wn = 2;  // (128 x 256 tiles measured slower: 2 blocks per CU instead of 4)
+    PCX_CHECK_ARG(!a.st_part0 || (a.mode == 0 && a.st_part1 && a.st_partn && convn_stat_tiles(a) == ceil_div(N, 64 * wn)),
+                  "convn: forward statistics need mode 0 and all three partial arrays");
     const int64_t nblocks = ceil_div(M, 64 * wm) * ceil_div(N, 64 * wn);
     PCX_CHECK_ARG(nblocks < ((int64_t)1 << 31), "convn: grid too large");
     dim3 grid((unsigned)(8 * xcd_per(nblocks)));

@@ -175,6 +175,9 @@ int build_deep(Plan& p) {
         if (k.planar) partmax = std::max(partmax, (size_t)planes(B, k.cin, k.Hi, k.Wi) * 4);
         k.an = k.d1n = k.m8 = 0;
         if (k.cn) {
+            // the channel-last forward writes BN partials per 128-pixel tile (conv1, conv2, shortcut)
+            const size_t nt = (size_t)ceil_div((int64_t)B * k.Ho * k.Wo, 128);
+            stat = std::max(stat, (size_t)2 * k.cout * nt + nt);
             k.an = p.carve("nhwc_a", nhwc_bytes(B, k.cin, k.Hi, k.Wi));
             k.d1n = p.carve("nhwc_d1", nhwc_bytes(B, k.cout, k.Ho, k.Wo));
             dynmax = std::max(dynmax, nhwc_bytes(B, k.cout, k.Ho, k.Wo));
@@ -322,10 +325,19 @@ int conv_bn_fwd(const Ctx& c, const char* label, int layer, const float* x, int 
         a.bf16 = c.d.bf16;
         a.wpack = c.w<void>(c.d.wpk16);
         a.xn = xn;
+        if (train && a.bf16 && xn) {  // the channel-last engine writes the BN partials in its epilogue
+            ns = (int)convn_stat_tiles(a);
+            a.st_part0 = part;
+            a.st_part1 = part + (size_t)cout * ns;
+            a.st_partn = part + (size_t)2 * cout * ns;
+            f.part0 = a.st_part0;
+            f.part1 = a.st_part1;
+            f.partn = a.st_partn;
+        }
         Scope sc(&c.p.prof, c.s, label, layer);
         RC(launch_convg(a, c.s));
     }
-    if (train && !dma_nblk) {
+    if (train && !dma_nblk && !(c.d.bf16 && xn)) {
         Scope sc(&c.p.prof, c.s, "chan_stats", strcmp(label, "shortcut_fwd") == 0 ? 100 + layer : layer);
         int bps;
         const int nsl = chan_slices(c.p.B, cout, &bps);

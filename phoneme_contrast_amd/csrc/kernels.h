@@ -345,6 +345,12 @@ struct ConvGArgs {
     const float* bn_g;
     const float* bn_y;
     const float4* bn_cf;
+    // mode 0 on the channel-last engine (optional): the BN forward partials of out in the epilogue --
+    // per 128-pixel tile tn and channel c: st_part0[c][ntile] = sum, st_part1 = M2 about the tile mean,
+    // st_partn[tn] = valid pixels; ntile = ceil(B OH OW / 128) (launch_bn_fwd_finalize's layout)
+    float* st_part0;
+    float* st_part1;
+    float* st_partn;
     // bf16 only: zero-padded channel-last bf16 images [B][H + 2][W + 2][C] of x (modes 0, 2) and dy
     // (modes 1, 2) written by launch_to_nhwc; when set, the channel-last engine (convn.hip) runs
     const void* xn;
@@ -390,6 +396,7 @@ struct NhwcArgs {
 size_t nhwc_bytes(int B, int C, int H, int W);
 int launch_to_nhwc(NhwcArgs a, hipStream_t s);
 bool convn_fits(const ConvGArgs& a);
+int64_t convn_stat_tiles(const ConvGArgs& a);  // mode 0: the st_part* tile count
 int launch_convn(const ConvGArgs& a, hipStream_t s);
 size_t convg_bf16_wpack_bytes(int mode, int cin, int cout, int k);
 size_t convg_wpack_bytes(int mode, int cin, int cout, int k);  // fp32 packed weights (wpack)
