@@ -365,6 +365,68 @@ __global__ __launch_bounds__(256) void convn_kernel(ConvGArgs a) {
                 }
             }
     }
+    if (MODE == 1 && a.ep_pg != nullptr) {
+        // backward partials of the BN + ReLU (+ Dropout2d) that produced this conv's input (replaces
+        // the bwd_prep pass over dx): producer values loaded for all of a row block first, per-row
+        // sums over the lanes by the transposed butterfly, the two pixel halves added
+        __syncthreads();  // operand stages consumed
+        float* red = reinterpret_cast<float*>(smem);                   // [2 (wc)][BM][2]
+        float4* cfl = reinterpret_cast<float4*>(red + 4 * BM);        // [BM]
+        if (tid < BM) cfl[tid] = a.ep_cf[min(m0 + tid, M - 1)];
+        __syncthreads();
+        const int64_t IHWe = (int64_t)a.IH * a.IW;
+        int64_t yb[WN], db[WN];
+        bool valid[WN];
+#pragma unroll
+        for (int ni = 0; ni < WN; ++ni) {
+            const int64_t col = n0 + wc * 32 * WN + ni * 32 + l32;
+            valid[ni] = col < N;
+            const int64_t cc = valid[ni] ? col : N - 1, b = cc / IHWe;
+            yb[ni] = b * a.cin * IHWe + (cc - b * IHWe);
+            db[ni] = b * a.cin;
+        }
+#pragma unroll
+        for (int mi = 0; mi < WM; ++mi) {
+            float yv[WN][16], dv[WN][16];
+#pragma unroll
+            for (int ni = 0; ni < WN; ++ni)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int64_t rc = min(m0 + wr * 32 * WM + mi * 32 + acc_row(r, h), M - 1);
+                    yv[ni][r] = a.ep_y[yb[ni] + rc * IHWe];
+                    dv[ni][r] = a.ep_drop ? a.ep_drop[db[ni] + rc] : 1.f;
+                }
+            float sg[16], sx[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int rl = wr * 32 * WM + mi * 32 + acc_row(r, h);
+                const float4 k = cfl[rl];
+                const bool rok = m0 + rl < M;
+                float tg = 0.f, tx = 0.f;
+#pragma unroll
+                for (int ni = 0; ni < WN; ++ni) {
+                    const float y = yv[ni][r];
+                    const float g = (valid[ni] && rok && fmaf(y, k.x, k.y) > 0.f) ? acc[mi][ni][r] * dv[ni][r] : 0.f;
+                    tg += g;
+                    tx = fmaf(g, (y - k.z) * k.w, tx);
+                }
+                sg[r] = tg;
+                sx[r] = tx;
+            }
+            const float tg = xsum16(sg, l32), tx = xsum16(sx, l32);
+            if (!(l32 & 1)) {
+                float* d = red + (wc * BM + wr * 32 * WM + mi * 32 + acc_row(l32 >> 1, h)) * 2;
+                d[0] = tg;
+                d[1] = tx;
+            }
+        }
+        __syncthreads();
+        if (tid < BM && m0 + tid < M) {
+            const int64_t ntile = (N + BN - 1) / BN;
+            a.ep_pg[(m0 + tid) * ntile + tn] = red[tid * 2] + red[(BM + tid) * 2];
+            a.ep_px[(m0 + tid) * ntile + tn] = red[tid * 2 + 1] + red[(BM + tid) * 2 + 1];
+        }
+    }
     if (MODE == 0 && a.st_part0 != nullptr) {
         // BN forward partials of the tile (replaces the statistics pass over out): per (wave, channel)
         // Chan statistics of its 64 pixels about the channel's first pixel in the wave (K, v_readlane),
@@ -633,7 +695,9 @@ int launch_to_nhwc(NhwcArgs a, hipStream_t s) {
 // 14 % faster than 32 on the 256-channel layers) where the channel count allows
 static int convn_kc(int ck) { return ck % 64 == 0 ? 64 : 32; }
 
-int64_t convn_stat_tiles(const ConvGArgs& a) { return ceil_div((int64_t)a.B * a.OH * a.OW, 128); }
+int64_t convn_stat_tiles(const ConvGArgs& a) {
+    return ceil_div((int64_t)a.B * (a.mode == 1 ? (int64_t)a.IH * a.IW : (int64_t)a.OH * a.OW), 128);
+}
 
 bool convn_fits(const ConvGArgs& a) {
     if (a.KH != a.KW || (a.KH != 1 && a.KH != 3) || a.pad > 1 || a.pad < 0) return false;
@@ -692,6 +756,9 @@ int launch_convn(const ConvGArgs& a, hipStream_t s) {
     constexpr int wn = 2;  // (128 x 256 tiles measured slower: 2 blocks per CU instead of 4)
     PCX_CHECK_ARG(!a.st_part0 || (a.mode == 0 && a.st_part1 && a.st_partn && convn_stat_tiles(a) == ceil_div(N, 64 * wn)),
                   "convn: forward statistics need mode 0 and all three partial arrays");
+    PCX_CHECK_ARG(!a.ep_pg || (a.mode == 1 && a.ep_px && a.ep_y && a.ep_cf && !a.accumulate &&
+                               convn_stat_tiles(a) == ceil_div(N, 64 * wn)),
+                  "convn: data-gradient BN sums need mode 1 (stride 1, no accumulate), y, cf and both partial arrays");
     const int64_t nblocks = ceil_div(M, 64 * wm) * ceil_div(N, 64 * wn);
     PCX_CHECK_ARG(nblocks < ((int64_t)1 << 31), "convn: grid too large");
     dim3 grid((unsigned)(8 * xcd_per(nblocks)));

@@ -426,7 +426,7 @@ int conv_wgrad(const Ctx& c, int layer, const float* x, int cin, int IH, int IW,
 
 int conv_dgrad(const Ctx& c, int layer, const float* dy, int cout, int OH, int OW, int k, int stride, int pad,
                const float* wgt, float* dx, int cin, int IH, int IW, int accumulate, bool dma = false,
-               const void* dyn = nullptr, float* par_out = nullptr) {
+               const void* dyn = nullptr, float* par_out = nullptr, const ConvGArgs* ep = nullptr) {
     if (dma) {  // stride-1 3x3: the LDS-DMA conv on flipped weights, plain store / accumulate
         float* wp = c.w<float>(c.d.wpk);
         const bool wino = wino_geometry(c.p.B, IH, IW, cout, cin, nullptr);
@@ -455,6 +455,9 @@ int conv_dgrad(const Ctx& c, int layer, const float* dy, int cout, int OH, int O
     a.wpack = c.w<void>(c.d.wpk16);
     a.dyn = dyn;
     a.par_out = par_out;
+    if (ep) {  // the producer BN's backward sums in the channel-last engine's epilogue
+        a.ep_y = ep->ep_y; a.ep_cf = ep->ep_cf; a.ep_drop = ep->ep_drop; a.ep_pg = ep->ep_pg; a.ep_px = ep->ep_px;
+    }
     Scope sc(&c.p.prof, c.s, "conv_dgrad", layer);
     return launch_convg(a, c.s);
 }
@@ -771,9 +774,24 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
                       G[q + 5], k.w32_2 ? &k.wg2 : nullptr, g, c.w<float>(k.y2), c.w<float4>(k.cfb2), d1n, dyn1,
                       k.ww2 ? &k.wwa2 : nullptr));
         float* dd = c.w<float>(d.dd);
-        RC(conv_dgrad(c, L + 1, dy2, k.cout, k.Ho, k.Wo, 3, 1, 1, P[q + 4], dd, k.cout, k.Ho, k.Wo, 0, k.dma2, dyn1));
+        // channel-last: conv2's data gradient also reduces BN1's backward sums (no bwd_prep pass over dd)
+        const bool ep_sums = k.cn && getenv("PCX_NO_EPSUMS") == nullptr;
+        ConvGArgs ep{};
+        if (ep_sums) {
+            ns = ceil_div((int64_t)B * P2, 128);
+            ep.ep_y = c.w<float>(k.y1);
+            ep.ep_cf = c.w<float4>(k.cf1);
+            ep.ep_drop = d.residual ? dmask[i] : nullptr;
+            ep.ep_pg = part;
+            ep.ep_px = part + (size_t)k.cout * ns;
+        }
+        RC(conv_dgrad(c, L + 1, dy2, k.cout, k.Ho, k.Wo, 3, 1, 1, P[q + 4], dd, k.cout, k.Ho, k.Wo, 0, k.dma2, dyn1,
+                      nullptr, ep_sums ? &ep : nullptr));
         // ---- through Dropout2d / ReLU / BN1
-        {
+        if (ep_sums) {
+            RC(bn_bwd(c, k.cout, ns, ep.ep_pg, ep.ep_px, P[q + 2], c.w<float4>(k.cf1), G[q + 2], G[q + 3],
+                      c.w<float4>(k.cfb1), count));
+        } else {
             BwdPrepArgs b{};
             b.B = B; b.C = k.cout; b.P = P2;
             b.d = dd;

@@ -351,6 +351,15 @@ struct ConvGArgs {
     float* st_part0;
     float* st_part1;
     float* st_partn;
+    // mode 1 (stride 1) on the channel-last engine (optional): the backward partials of the BN + ReLU
+    // (+ Dropout2d) feeding this conv's input, from out = dx in the epilogue (bwd_prep's MASK_BN sums):
+    // g = dx ep_drop[b,c] [ep_y s + t > 0] (ep_cf = {s, t, mean, invstd}), per 128-pixel tile
+    // ep_pg[c][ntile] = sum g, ep_px[c][ntile] = sum g (ep_y - mean) invstd; ntile = ceil(B IH IW / 128)
+    const float* ep_y;
+    const float4* ep_cf;
+    const float* ep_drop;
+    float* ep_pg;
+    float* ep_px;
     // bf16 only: zero-padded channel-last bf16 images [B][H + 2][W + 2][C] of x (modes 0, 2) and dy
     // (modes 1, 2) written by launch_to_nhwc; when set, the channel-last engine (convn.hip) runs
     const void* xn;
@@ -396,7 +405,7 @@ struct NhwcArgs {
 size_t nhwc_bytes(int B, int C, int H, int W);
 int launch_to_nhwc(NhwcArgs a, hipStream_t s);
 bool convn_fits(const ConvGArgs& a);
-int64_t convn_stat_tiles(const ConvGArgs& a);  // mode 0: the st_part* tile count
+int64_t convn_stat_tiles(const ConvGArgs& a);  // mode 0: the st_part* tile count; mode 1: ep_p*
 int launch_convn(const ConvGArgs& a, hipStream_t s);
 size_t convg_bf16_wpack_bytes(int mode, int cin, int cout, int k);
 size_t convg_wpack_bytes(int mode, int cin, int cout, int k);  // fp32 packed weights (wpack)
