@@ -126,13 +126,23 @@ bool head_reg_fits(const HeadPoolArgs& a) { return a.C == HR_C && a.P % 4 == 0 &
 __global__ __launch_bounds__(512) void head_pool_fwd_reg_kernel(HeadPoolArgs a) {
     __shared__ __attribute__((aligned(16))) float part[8][HR_PMAX];  // per-wave partial logits
     __shared__ __attribute__((aligned(16))) float att[HR_PMAX];
-    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // (uniform: coefficient loads are scalar)
     const int c0 = wave * HR_CPW, P = a.P;
     const float* yb = a.y + ((int64_t)b * HR_C + c0) * P;
     float4 xv[HR_CPW][HR_KP];
     float4 lg[HR_KP];
 #pragma unroll
     for (int k = 0; k < HR_KP; ++k) lg[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    // every y load of the sample first (clamped in bounds, zeroed after): one memory round trip per
+    // sample -- computing each channel right after its load had the compiler wait for every load
+#pragma unroll
+    for (int c = 0; c < HR_CPW; ++c)
+#pragma unroll
+        for (int k = 0; k < HR_KP; ++k) {
+            const int p = 4 * lane + 256 * k;
+            xv[c][k] = ld4(yb + (int64_t)c * P + (p < P ? p : 0));
+        }
 #pragma unroll
     for (int c = 0; c < HR_CPW; ++c) {
         const float4 cf = a.cf[c0 + c];
@@ -141,11 +151,9 @@ __global__ __launch_bounds__(512) void head_pool_fwd_reg_kernel(HeadPoolArgs a) 
 #pragma unroll
         for (int k = 0; k < HR_KP; ++k) {
             const int p = 4 * lane + 256 * k;
-            float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (p < P) {
-                const float4 y = ld4(yb + (int64_t)c * P + p);
-                x = make_float4(xval(y.x, cf, d), xval(y.y, cf, d), xval(y.z, cf, d), xval(y.w, cf, d));
-            }
+            const float4 y = xv[c][k];
+            const float4 x = p < P ? make_float4(xval(y.x, cf, d), xval(y.y, cf, d), xval(y.z, cf, d), xval(y.w, cf, d))
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
             xv[c][k] = x;
             lg[k].x = fmaf(wa, x.x, lg[k].x);
             lg[k].y = fmaf(wa, x.y, lg[k].y);
@@ -198,7 +206,8 @@ __global__ __launch_bounds__(512) void head_pool_bwd_reg_kernel(HeadPoolArgs a) 
     __shared__ __attribute__((aligned(16))) float att[HR_PMAX];
     __shared__ __attribute__((aligned(16))) float dl[HR_PMAX];
     __shared__ float red[8];
-    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int c0 = wave * HR_CPW, P = a.P;
     const float invp = 1.f / (float)P;
     const float* yb = a.y + ((int64_t)b * HR_C + c0) * P;
@@ -208,7 +217,7 @@ __global__ __launch_bounds__(512) void head_pool_bwd_reg_kernel(HeadPoolArgs a) 
 #pragma unroll
         for (int k = 0; k < HR_KP; ++k) {
             const int p = 4 * lane + 256 * k;
-            yv[c][k] = p < P ? ld4(yb + (int64_t)c * P + p) : make_float4(0.f, 0.f, 0.f, 0.f);
+            yv[c][k] = ld4(yb + (int64_t)c * P + (p < P ? p : 0));  // (lanes past P: never used)
         }
     if (a.wa) {  // dl[p] = att (1 - att) sum_c dpooled[c] / P x[c][p]
         float4 sp[HR_KP];
