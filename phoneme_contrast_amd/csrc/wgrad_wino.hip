@@ -130,7 +130,7 @@ template <int PRO, int V>
 __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int co0, int ci0, int slice) {
     const int tid = threadIdx.x, lane = tid & 63, c32 = lane & 31, g = lane >> 5;
     const int Q = __builtin_amdgcn_readfirstlane(tid >> 6);
-    constexpr int NPT = 2;  // parts of the next tile row's loads (V = 4: 4 parts spill)
+    constexpr int NPT = V == 4 ? 2 : 4;  // parts of the next tile row's loads (V = 4: 4 parts spill)
     const int XCS = a.XCS, DCS = a.DCS;
     float* const xl = smem + 4;                   // [4 ring slots][32][XCS]
     float* const dyl = xl + 4 * 32 * XCS;         // [2 rows][32][DCS]
@@ -169,21 +169,17 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
     const int t0s = slice * a.per_slice, t1s = min(a.ntask, t0s + a.per_slice);
     vecf<V> dzv[NIT], yv[NIT], xv[NIT];
 
-    // the task (sample, strip) being staged: its buffer resources and per-task column validity
-    int c0 = 0;
-    __amdgpu_buffer_rsrc_t rdz, ry, rdo, rx;
-    unsigned dcol = 0, xcol = 0;
-    auto set_task = [&](int task) {
+    for (int task = t0s; task < t1s; ++task) {
         const int b = task / a.nseg;
         const int t0 = (task - b * a.nseg) * a.S;
-        c0 = 2 * t0;
-        rdz = rsrc(a.dz + ((int64_t)b * a.cout + co0) * HW, (int64_t)32 * HW * 4);
-        ry = rsrc(a.y + ((int64_t)b * a.cout + co0) * HW, (int64_t)32 * HW * 4);
-        rdo = rsrc(write_dy ? a.dy_out + ((int64_t)b * a.cout + co0) * HW : a.dz, write_dy ? (int64_t)32 * HW * 4 : 0);
-        rx = rsrc(a.src + ((int64_t)b * a.cin + ci0) * HW, (int64_t)32 * HW * 4);
-        // (whole vectors: V divides W and 2 t0)
-        dcol = 0;
-        xcol = 0;
+        const int c0 = 2 * t0;
+        const __amdgpu_buffer_rsrc_t rdz = rsrc(a.dz + ((int64_t)b * a.cout + co0) * HW, (int64_t)32 * HW * 4);
+        const __amdgpu_buffer_rsrc_t ry = rsrc(a.y + ((int64_t)b * a.cout + co0) * HW, (int64_t)32 * HW * 4);
+        const __amdgpu_buffer_rsrc_t rdo =
+            rsrc(write_dy ? a.dy_out + ((int64_t)b * a.cout + co0) * HW : a.dz, write_dy ? (int64_t)32 * HW * 4 : 0);
+        const __amdgpu_buffer_rsrc_t rx = rsrc(a.src + ((int64_t)b * a.cin + ci0) * HW, (int64_t)32 * HW * 4);
+        // per-task column validity of the items (whole vectors: V divides W and 2 t0)
+        unsigned dcol = 0, xcol = 0;
 #pragma unroll
         for (int i = 0; i < NIT; ++i) {
             const int kc = V * (j0 + 8 * (i % NIR));
@@ -192,164 +188,139 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
         }
         dcol &= dex;
         xcol &= xex;
-    };
 
-    // stage st (= -1 .. TR - 1): dy rows 2 st, 2 st + 1 and x rows 2 st + 1, 2 st + 2
-    constexpr unsigned R1 = ((1u << NIR) - 1) << NIR;  // items of the stage's second row
-    auto masks = [&](int st, unsigned& dm, unsigned& xm) {
-        const bool d0 = 2 * st >= 0, d1 = 2 * st + 1 >= 0 && 2 * st + 1 < H;
-        const bool x0 = 2 * st + 1 >= 0 && 2 * st + 1 < H, x1 = 2 * st + 2 < H;
-        dm = dcol & ((d0 ? ~R1 : 0u) | (d1 ? R1 : 0u));
-        xm = xcol & ((x0 ? ~R1 : 0u) | (x1 ? R1 : 0u));
-    };
-    auto dgo = [&](int i) { return dgb + (i / NIR) * W + 8 * V * (i % NIR); };
-    auto xgo = [&](int i) { return xgb + (i / NIR) * W + 8 * V * (i % NIR); };
-    // part: only the items m with m NPT / NIT == part (-1: all items)
-    auto load_dy = [&](int st, int part) {
-        unsigned dm, xm;
-        masks(st, dm, xm);
-        int db = 2 * st * W + c0 + dgb;
-        asm volatile("" : "+v"(db));  // opaque: per-item offsets formed at the load, not kept live
+        // stage st (= -1 .. TR - 1): dy rows 2 st, 2 st + 1 and x rows 2 st + 1, 2 st + 2
+        constexpr unsigned R1 = ((1u << NIR) - 1) << NIR;  // items of the stage's second row
+        auto masks = [&](int st, unsigned& dm, unsigned& xm) {
+            const bool d0 = 2 * st >= 0, d1 = 2 * st + 1 >= 0 && 2 * st + 1 < H;
+            const bool x0 = 2 * st + 1 >= 0 && 2 * st + 1 < H, x1 = 2 * st + 2 < H;
+            dm = dcol & ((d0 ? ~R1 : 0u) | (d1 ? R1 : 0u));
+            xm = xcol & ((x0 ? ~R1 : 0u) | (x1 ? R1 : 0u));
+        };
+        auto dgo = [&](int i) { return dgb + (i / NIR) * W + 8 * V * (i % NIR); };
+        auto xgo = [&](int i) { return xgb + (i / NIR) * W + 8 * V * (i % NIR); };
+        // part: only the items m with m NPT / NIT == part (-1: all items)
+        auto load_dy = [&](int st, int part) {
+            unsigned dm, xm;
+            masks(st, dm, xm);
+            int db = 2 * st * W + c0 + dgb;
+            asm volatile("" : "+v"(db));  // opaque: per-item offsets formed at the load, not kept live
 #pragma unroll
-        for (int m = 0; m < NIT; ++m) {
-            if (part >= 0 && m * NPT / NIT != part) continue;
-            const int o = (dm >> m) & 1 ? 4 * (dgo(m) - dgb + db) : OOB;
-            dzv[m] = bload<V>(rdz, o);
-            yv[m] = bload<V>(ry, o);
-        }
-    };
-    // dy = A1 dz + A2 y + A3 (exact 0 outside the image) into dzv
-    auto form_dy = [&](int st) {
-        unsigned dm, xm;
-        masks(st, dm, xm);
-#pragma unroll
-        for (int m = 0; m < NIT; ++m) {
-            const float a3 = (dm >> m) & 1 ? A3 : 0.f;
-#pragma unroll
-            for (int e = 0; e < V; ++e) dzv[m][e] = fma1(A1, dzv[m][e], fma1(A2, yv[m][e], a3));
-        }
-    };
-    auto load_x = [&](int st, int part) {
-        unsigned dm, xm;
-        masks(st, dm, xm);
-        int xb = (2 * st + 1) * W + c0 + xgb;
-        asm volatile("" : "+v"(xb));
-#pragma unroll
-        for (int m = 0; m < NIT; ++m)
-            if (part < 0 || m * NPT / NIT == part) xv[m] = bload<V>(rx, (xm >> m) & 1 ? 4 * (xgo(m) - xgb + xb) : OOB);
-    };
-    auto store_x = [&](int st, const vecf<V> (&xr)[NIT]) {
-        unsigned dm, xm;
-        masks(st, dm, xm);
-        // x rows 2 st + 1, 2 st + 2 -> ring slots (2 st + 2) & 3, (2 st + 3) & 3
-        const int sl0 = ((2 * st + 2) & 3) * 32 * XCS, sl1 = ((2 * st + 3) & 3) * 32 * XCS;
-#pragma unroll
-        for (int m = 0; m < NIT; ++m) {
-            if (!((xex >> m) & 1)) continue;
-            // (stage -1's first row is image row -1: zeros, never loaded)
-            vecf<V> v = st == -1 && m < NIR ? vecf<V>(0.f) : xr[m];
-            if (PRO == PRO_BNRELU) {
-                const float tt = (xm >> m) & 1 ? xt : 0.f;
-#pragma unroll
-                for (int e = 0; e < V; ++e) v[e] = fmaxf(fmaf(v[e], xs, tt), 0.f);
+            for (int m = 0; m < NIT; ++m) {
+                if (part >= 0 && m * NPT / NIT != part) continue;
+                const int o = (dm >> m) & 1 ? 4 * (dgo(m) - dgb + db) : OOB;
+                dzv[m] = bload<V>(rdz, o);
+                yv[m] = bload<V>(ry, o);
             }
-            float* d = xl + (m / NIR ? sl1 : sl0) + xlb + 8 * V * (m % NIR);
-            if constexpr (V == 4) {
-                d[0] = v[0];
-                *reinterpret_cast<f2*>(d + 1) = f2{v[1], v[2]};
-                d[3] = v[3];
-            } else {
-                d[0] = v[0];
-                d[1] = v[1];
+        };
+        // dy = A1 dz + A2 y + A3 (exact 0 outside the image) into dzv
+        auto form_dy = [&](int st) {
+            unsigned dm, xm;
+            masks(st, dm, xm);
+#pragma unroll
+            for (int m = 0; m < NIT; ++m) {
+                const float a3 = (dm >> m) & 1 ? A3 : 0.f;
+#pragma unroll
+                for (int e = 0; e < V; ++e) dzv[m][e] = fma1(A1, dzv[m][e], fma1(A2, yv[m][e], a3));
             }
-        }
-    };
-
-    auto store = [&](int st) {
-        unsigned dm, xm;
-        masks(st, dm, xm);
-        const int db = 2 * st * W + c0;
+        };
+        auto load_x = [&](int st, int part) {
+            unsigned dm, xm;
+            masks(st, dm, xm);
+            int xb = (2 * st + 1) * W + c0 + xgb;
+            asm volatile("" : "+v"(xb));
 #pragma unroll
-        for (int m = 0; m < NIT; ++m) {
-            if (!((dex >> m) & 1)) continue;
-            const bool ok = (dm >> m) & 1;
-            const vecf<V> v = dzv[m];
-            float* d = dyl + dlb + (m / NIR) * 32 * DCS + 8 * V * (m % NIR);
-            *reinterpret_cast<f2*>(d) = f2{v[0], v[1]};
-            if constexpr (V == 4) *reinterpret_cast<f2*>(d + 2) = f2{v[2], v[3]};
-            if (write_dy) bstore<V>(rdo, ok ? 4 * (dgo(m) + db) : OOB, v);
-        }
-        store_x(st, xv);
-    };
-
-    // task prologue: stages -1 and 0 (x rows -1 .. 2, dy rows 0, 1).  Stage -1's first row (image row -1)
-    // is always outside the image: only its second row (x row 0) is loaded, into xa.
-    vecf<V> xa[NIT];  // (items m < NIR unused)
-    auto load_xa = [&](int part) {
-        unsigned dm, xm;
-        masks(-1, dm, xm);
-        const int xb = -W + c0;
+            for (int m = 0; m < NIT; ++m)
+                if (part < 0 || m * NPT / NIT == part) xv[m] = bload<V>(rx, (xm >> m) & 1 ? 4 * (xgo(m) - xgb + xb) : OOB);
+        };
+        auto store_x = [&](int st, const vecf<V> (&xr)[NIT]) {
+            unsigned dm, xm;
+            masks(st, dm, xm);
+            // x rows 2 st + 1, 2 st + 2 -> ring slots (2 st + 2) & 3, (2 st + 3) & 3
+            const int sl0 = ((2 * st + 2) & 3) * 32 * XCS, sl1 = ((2 * st + 3) & 3) * 32 * XCS;
 #pragma unroll
-        for (int m = NIR; m < NIT; ++m)
-            if (part < 0 || m * NPT / NIT == part) xa[m] = bload<V>(rx, (xm >> m) & 1 ? 4 * (xgo(m) + xb) : OOB);
-    };
-    auto prologue_store = [&]() {
-        store_x(-1, xa);
-        form_dy(0);
-        store(0);
-    };
-    // XP (V = 2: the 5-row tasks of the 10 x 50 layers): the next task's prologue is loaded over the
-    // current task's last tile row instead of as one round trip at the task start (V = 4: registers)
-    constexpr bool XP = V == 2;
+            for (int m = 0; m < NIT; ++m) {
+                if (!((xex >> m) & 1)) continue;
+                vecf<V> v = xr[m];
+                if (PRO == PRO_BNRELU) {
+                    const float tt = (xm >> m) & 1 ? xt : 0.f;
+#pragma unroll
+                    for (int e = 0; e < V; ++e) v[e] = fmaxf(fmaf(v[e], xs, tt), 0.f);
+                }
+                float* d = xl + (m / NIR ? sl1 : sl0) + xlb + 8 * V * (m % NIR);
+                if constexpr (V == 4) {
+                    d[0] = v[0];
+                    *reinterpret_cast<f2*>(d + 1) = f2{v[1], v[2]};
+                    d[3] = v[3];
+                } else {
+                    d[0] = v[0];
+                    d[1] = v[1];
+                }
+            }
+        };
 
-    // wave constants of row Q: e = w + sx u from x rows (w, u) of the tile row's four; the dy row
-    // combination pr = r0 + sy r1 (Q 0: r0, 1: r0 + r1, 2: r0 - r1, 3: r1 via r0 := row 1, sy = 0)
-    const int IW = Q == 0 ? 0 : Q == 2 ? 2 : 1, IU = Q == 0 ? 2 : Q == 2 ? 1 : Q == 1 ? 2 : 3;
-    const float sx = Q == 1 ? 1.f : -1.f;
-    const float sy = Q == 1 ? 1.f : Q == 2 ? -1.f : 0.f;
-    const float* const dr0 = dyl + (Q == 3 ? 32 * DCS : 0) + c32 * DCS + 2 * g;
-    const float* const dr1 = dyl + 32 * DCS + c32 * DCS + 2 * g;
-    auto ksteps = [&](const float* xw, const float* xu, int s0, int s1) {
-        const int n = s1 - s0;
-        const float* w = xw + 4 * s0;
-        const float* u = xu + 4 * s0;
-        const float* q0 = dr0 + 4 * s0;
-        const float* q1 = dr1 + 4 * s0;
-        kloop(w, u, q0, q1, sx, sy, acc, n);
-    };
-    const int Ks = a.Ksteps;
+        auto store = [&](int st) {
+            unsigned dm, xm;
+            masks(st, dm, xm);
+            const int db = 2 * st * W + c0;
+#pragma unroll
+            for (int m = 0; m < NIT; ++m) {
+                if (!((dex >> m) & 1)) continue;
+                const bool ok = (dm >> m) & 1;
+                const vecf<V> v = dzv[m];
+                float* d = dyl + dlb + (m / NIR) * 32 * DCS + 8 * V * (m % NIR);
+                *reinterpret_cast<f2*>(d) = f2{v[0], v[1]};
+                if constexpr (V == 4) *reinterpret_cast<f2*>(d + 2) = f2{v[2], v[3]};
+                if (write_dy) bstore<V>(rdo, ok ? 4 * (dgo(m) + db) : OOB, v);
+            }
+            store_x(st, xv);
+        };
 
-    for (int task = t0s; task < t1s; ++task) {
-        const bool hasn = task + 1 < t1s;
-        if (task == t0s || !XP) {  // prologue as one round trip (loaded together)
-            set_task(task);
+        // task prologue: stages -1 and 0 (x rows -1 .. 2, dy rows 0, 1) loaded together: one round trip
+        {
             load_dy(0, -1);
             load_x(0, -1);
-            load_xa(-1);
-            prologue_store();
-            __syncthreads();
+            vecf<V> xa[NIT];  // stage -1: x rows -1 (zeros: the ring slot holds the previous task's rows), 0
+            unsigned dm, xm;
+            masks(-1, dm, xm);
+            const int xb = -W + c0;
+#pragma unroll
+            for (int m = 0; m < NIT; ++m) xa[m] = bload<V>(rx, (xm >> m) & 1 ? 4 * (xgo(m) + xb) : OOB);
+            store_x(-1, xa);
+            form_dy(0);
+            store(0);
         }
+        __syncthreads();
+        // wave constants of row Q: e = w + sx u from x rows (w, u) of the tile row's four; the dy row
+        // combination pr = r0 + sy r1 (Q 0: r0, 1: r0 + r1, 2: r0 - r1, 3: r1 via r0 := row 1, sy = 0)
+        const int IW = Q == 0 ? 0 : Q == 2 ? 2 : 1, IU = Q == 0 ? 2 : Q == 2 ? 1 : Q == 1 ? 2 : 3;
+        const float sx = Q == 1 ? 1.f : -1.f;
+        const float sy = Q == 1 ? 1.f : Q == 2 ? -1.f : 0.f;
+        const float* const dr0 = dyl + (Q == 3 ? 32 * DCS : 0) + c32 * DCS + 2 * g;
+        const float* const dr1 = dyl + 32 * DCS + c32 * DCS + 2 * g;
+        auto ksteps = [&](const float* xw, const float* xu, int s0, int s1) {
+            const int n = s1 - s0;
+            const float* w = xw + 4 * s0;
+            const float* u = xu + 4 * s0;
+            const float* q0 = dr0 + 4 * s0;
+            const float* q1 = dr1 + 4 * s0;
+            kloop(w, u, q0, q1, sx, sy, acc, n);
+        };
+        const int Ks = a.Ksteps;
         for (int tr = 0; tr < TR; ++tr) {
             const bool pre = tr + 1 < TR;
-            const bool nextp = XP && !pre && hasn;
-            // (the last row's K-steps read only LDS: the staging state moves to the next task now)
-            if (nextp) set_task(task + 1);
             // x rows 2 tr - 1 + i of this tile row live in ring slot (2 tr + i) & 3
             const float* xw = xl + ((2 * tr + IW) & 3) * 32 * XCS + c32 * XCS + 2 * g;
             const float* xu = xl + ((2 * tr + IU) & 3) * 32 * XCS + c32 * XCS + 2 * g;
-            // the next tile row's dz / y / x rows (or the next task's prologue) loaded over this row's
-            // K-steps in NPT parts (a burst of 3 NIT loads at the row start stalls the issuing waves on
-            // the texture unit, MFMA pipes idle); dy formed after the last part
+            // the next tile row's dz / y / x rows loaded over this row's K-steps in NPT parts (a
+            // burst of 3 NIT loads at the row start stalls the issuing waves on the texture unit, MFMA
+            // pipes idle); dy formed after the last part
 #pragma unroll
             for (int pt = 0; pt < NPT; ++pt) {
                 __builtin_amdgcn_sched_barrier(0);  // (no hoisting of later parts' loads: registers)
                 if (pre) {
                     load_dy(tr + 1, pt);
                     load_x(tr + 1, pt);
-                } else if (nextp) {
-                    load_dy(0, pt);
-                    load_x(0, pt);
-                    load_xa(pt);
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 ksteps(xw, xu, Ks * pt / NPT, Ks * (pt + 1) / NPT);
@@ -357,7 +328,6 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
             if (pre) form_dy(tr + 1);
             __syncthreads();  // the dy rows and the two oldest x rows are free
             if (pre) store(tr + 1);
-            else if (nextp) prologue_store();
             __syncthreads();
         }
     }
