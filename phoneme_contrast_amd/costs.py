@@ -36,16 +36,21 @@ def kernel_costs(B, F, T, D=128):
             out["wgrad_L1"] = (2 * macs, y_out + 4 * B * F * T)
             continue
         out[f"conv_fwd_L{l}"] = (2 * macs, x_in + y_out)
-        # dgrad: reads dz_l and y_l, reads y_{l-1} (epilogue), writes dz_{l-1}
-        out[f"conv_dgrad_L{l}"] = (2 * macs, 2 * y_out + 2 * x_in)
+        # dgrad: reads dy_l (materialised by the weight gradient), the producer's values for its ReLU /
+        # BN-backward epilogue -- y_{l-1} at full resolution, or behind a MaxPool2 the forward's recorded
+        # selection (y at the selected element + its index: 5 bytes per pooled input, EPI_BWD_POOLSEL) --
+        # and writes dz_{l-1} at full resolution
+        prod = 5 * B * ci * h * w if (sh, sw) != (h, w) else x_in
+        out[f"conv_dgrad_L{l}"] = (2 * macs, y_out + prod + x_in)
         # wgrad: reads dz_l, y_l and the forward input source
         out[f"wgrad_L{l}"] = (2 * macs, 2 * y_out + x_in)
         if l == 2:  # the fused layer-2 backward (wgbd_wino.hip): both GEMMs; dz2, y2, y1 read, dz1 written
             out["wgbd_L2"] = (4 * macs, 2 * y_out + 2 * x_in)
     # elementwise / head passes (bytes: each tensor read once, each output written once)
     H1, W1, H3, W3, H5, W5 = F, T, F // 2, T // 2, F // 4, T // 4
-    out["bn_relu_pool_L3"] = (0, 4 * B * 32 * (H1 * W1 + H3 * W3))
-    out["bn_relu_pool_L5"] = (0, 4 * B * 64 * (H3 * W3 + H5 * W5))
+    # (+ the recorded selection for the pooled data gradient: y at the selected element, its index)
+    out["bn_relu_pool_L3"] = (0, B * 32 * (4 * H1 * W1 + 9 * H3 * W3))
+    out["bn_relu_pool_L5"] = (0, B * 64 * (4 * H3 * W3 + 9 * H5 * W5))
     out["head_pool_fwd"] = (4 * B * 128 * H5 * W5, 4 * B * (128 * H5 * W5 + 128 + H5 * W5))
     out["head_pool_bwd"] = (6 * B * 128 * H5 * W5, 4 * B * (2 * 128 * H5 * W5 + 128 + H5 * W5))
     out["proj_fwd"] = (2 * B * 128 * D, 4 * B * (128 + 2 * D))
