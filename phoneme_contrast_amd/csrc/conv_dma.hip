@@ -400,6 +400,16 @@ __global__ __launch_bounds__(256) void bn_relu_pool_kernel(const float* __restri
                 st4(ysel + po, make_float4(ya[0], ya[1], ya[2], ya[3]));
                 *reinterpret_cast<unsigned*>(parg + po) = ag;
             }
+        } else if ((Wp & 1) == 0) {  // 8-byte aligned pairs (the quad's second pair may lie past the row)
+#pragma unroll
+            for (int j = 0; j < 4; j += 2)
+                if (4 * q + j < Wp) {
+                    *reinterpret_cast<float2*>(dst + j) = make_float2(out[j], out[j + 1]);
+                    if (ysel) {
+                        *reinterpret_cast<float2*>(ysel + po + j) = make_float2(ya[j], ya[j + 1]);
+                        *reinterpret_cast<uint16_t*>(parg + po + j) = (uint16_t)(ag >> (8 * j));
+                    }
+                }
         } else {
             for (int j = 0; j < 4 && 4 * q + j < Wp; ++j) {
                 dst[j] = out[j];
