@@ -278,11 +278,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
             float ex[2][4];                                  // the epilogue's x values (prefetched)
             for (int g = 0; g < ng; ++g) {
 #ifndef WB_LOADPOS
-#define WB_LOADPOS 0
+#define WB_LOADPOS 1
 #endif
-                // the next tile row's staging loads: spread over the groups, at the group start (analysis
-                // builds: WB_LOADPOS 1 = data-gradient waves after the group's MFMAs, 2 = all items at once,
-                // weight-gradient waves at group 0, data-gradient waves after group 1's MFMAs)
+                // the next tile row's staging loads, spread over the groups: the weight-gradient waves at the
+                // group start, the data-gradient waves after the group's MFMAs (WB_LOADPOS 1; same-box A/B
+                // 7.38-7.41 -> 7.29-7.33 ms against all waves at the group start, 0; 2 = all items at once,
+                // weight-gradient waves at group 0, data-gradient waves after group 1's MFMAs: slower)
                 if (pre && (WB_LOADPOS == 0 || (WB_LOADPOS == 1 && !DG))) load(tr + 1, g, ng);
                 if (pre && WB_LOADPOS == 2 && !DG && g == 0) load(tr + 1, 0, 0);
                 if constexpr (!DG) {
