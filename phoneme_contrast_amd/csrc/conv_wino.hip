@@ -286,7 +286,8 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
                 sz[j] = s_z;
                 sx[j] = s_x;
             }
-        } else if (EPI == EPI_BWD_POOLSEL) {
+        } else if (EPI == EPI_BWD_POOLSEL || EPI == EPI_BWD_POOLSELP) {
+            constexpr bool PO = EPI == EPI_BWD_POOLSELP;
             // the pooled data gradient from the forward's recorded selection: y at each window's selected
             // element and its index (bn_relu_pool_kernel), read at the conv's (pooled) resolution -- a
             // quarter of the full-resolution window reads; dz written at Hs x Ws as EPI_BWD_POOL does
@@ -330,23 +331,38 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
                     const int co = 16 * (j >> 2) + 4 * kq + (j & 3);
                     float* op = ob + (int64_t)co * HWs;
                     const float4 k = cf[jj];
-                    float dzw[4][4];
+                    float dzw[4][4], dde[4];
                     float s_z = 0.f, s_x = 0.f;
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         const int r0 = 2 * (e >> 1), c0 = 2 * (e & 1);
                         const float ya = ys[jj][e];
-                        const unsigned arg = (ag[jj] >> (8 * e)) & 3u;
                         // the window's maximum of relu(BN) is positive iff the selected element's BN output is
                         const float dd = (ok[e] && fmaf(ya, k.x, k.y) > 0.f) ? y[j][e] * dv[jj] : 0.f;
-                        dzw[r0][c0] = arg == 0 ? dd : 0.f;
-                        dzw[r0][c0 + 1] = arg == 1 ? dd : 0.f;
-                        dzw[r0 + 1][c0] = arg == 2 ? dd : 0.f;
-                        dzw[r0 + 1][c0 + 1] = arg == 3 ? dd : 0.f;
+                        dde[e] = dd;
+                        if constexpr (!PO) {
+                            const unsigned arg = (ag[jj] >> (8 * e)) & 3u;
+                            dzw[r0][c0] = arg == 0 ? dd : 0.f;
+                            dzw[r0][c0 + 1] = arg == 1 ? dd : 0.f;
+                            dzw[r0 + 1][c0] = arg == 2 ? dd : 0.f;
+                            dzw[r0 + 1][c0 + 1] = arg == 3 ? dd : 0.f;
+                        }
                         s_z += dd;
                         s_x = fmaf(dd, (ya - k.z) * k.w, s_x);
                     }
-                    if (V4) {
+                    if constexpr (PO) {
+                        // EPI_BWD_POOLSELP: the consumer rebuilds the windows from parg -- the routed
+                        // gradient at the pooled resolution only (a quarter of the full-resolution writes)
+                        float* pq = a.dpool + ((int64_t)b * a.cout + n0 + co) * HW + pix0;
+                        if (vec) {
+                            if (ok[0]) st2(pq, dde[0], dde[1]);
+                            if (ok[2]) st2(pq + a.W, dde[2], dde[3]);
+                        } else {
+#pragma unroll
+                            for (int e = 0; e < 4; ++e)
+                                if (ok[e]) pq[poff[e]] = dde[e];
+                        }
+                    } else if constexpr (V4) {
                         if (tvalid)
 #pragma unroll
                             for (int r = 0; r < 4; ++r)
@@ -866,7 +882,9 @@ int launch_conv3x3_wino(int pro, int epi, ConvArgs a, hipStream_t s) {
     if (epi == EPI_BWD_POOL || epi == EPI_BWD_POOLSEL)
         PCX_CHECK_ARG(a.Hs >= 2 * a.H && a.Ws >= 2 * a.W, "conv3x3_wino: pooled source %dx%d for %dx%d", a.Hs, a.Ws,
                       a.H, a.W);
-    PCX_CHECK_ARG(epi != EPI_BWD_POOLSEL || (a.ysel && a.parg), "conv3x3_wino: EPI_BWD_POOLSEL needs ysel and parg");
+    PCX_CHECK_ARG((epi != EPI_BWD_POOLSEL && epi != EPI_BWD_POOLSELP) || (a.ysel && a.parg),
+                  "conv3x3_wino: EPI_BWD_POOLSEL needs ysel and parg");
+    PCX_CHECK_ARG(epi != EPI_BWD_POOLSELP || a.dpool, "conv3x3_wino: EPI_BWD_POOLSELP needs dpool");
     const int ck = wino_ck(a.cin);
     const size_t buff = (size_t)4 * (ck * WSP + 32) + (size_t)ck * 512;
     const size_t smem = (2 * buff + 2 * (size_t)a.cin + 512) * 4;
@@ -902,6 +920,8 @@ int launch_conv3x3_wino(int pro, int epi, ConvArgs a, hipStream_t s) {
     PCX_WINO_CASE(PRO_RAW, EPI_BWD_POOL, 8, true, false) PCX_WINO_CASE(PRO_RAW, EPI_BWD_POOL, 4, true, false)
     PCX_WINO_CK(PRO_RAW, EPI_BWD_POOLSEL, false)
     PCX_WINO_CK(PRO_RAW, EPI_BWD_POOLSEL, true)
+    PCX_WINO_CASE(PRO_RAW, EPI_BWD_POOLSELP, 8, false, false) PCX_WINO_CASE(PRO_RAW, EPI_BWD_POOLSELP, 8, false, true)
+    PCX_WINO_CASE(PRO_RAW, EPI_BWD_POOLSELP, 4, false, false)
     PCX_WINO_CK(PRO_RAW, EPI_BWD_STORE, false)
 #undef PCX_WINO_CK
 #undef PCX_WINO_CASE

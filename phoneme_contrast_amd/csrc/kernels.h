@@ -19,6 +19,8 @@ enum Epilogue {
     EPI_BWD_STORE = 3,  // dx = acc (or dx += acc with ConvArgs::accumulate); no statistics
     EPI_BWD_POOLSEL = 4,  // EPI_BWD_POOL from the forward's recorded window selection (ysel / parg at the
                           // pooled resolution: no full-resolution window reads; conv_wino only)
+    EPI_BWD_POOLSELP = 5, // EPI_BWD_POOLSEL writing the routed gradient at the pooled resolution (dpool):
+                          // the consumer (wgbd_wino) rebuilds dz's 2x2 windows from parg
 };
 
 // 3x3 / stride 1 / pad 1 convolution as an implicit GEMM on v_mfma_f32_32x32x2_f32.
@@ -49,6 +51,7 @@ struct ConvArgs {
     int src_guard;        // 1: at least 4 readable bytes precede src (conv_wino's 16-byte staging copies)
     const float* ysel;    // EPI_BWD_POOLSEL: y at each 2x2 window's selected element [B][cout][H][W] (pooled res)
     const uint8_t* parg;  // EPI_BWD_POOLSEL: the selected element (0..3, row-major) of each window
+    float* dpool;         // EPI_BWD_POOLSELP: the routed gradient at the pooled resolution [B][cout][H][W]
 };
 
 size_t conv3x3_nblk(int B, int H, int W, int cout);
@@ -143,6 +146,9 @@ int launch_wgrad_wino_reduce(const float* part, int nslice, int cout, int cin, f
 struct WinoBwdArgs {
     int B, H, W;           // 32 channels in and out; W % 4 == 0, W / 2 even
     const float* dz;       // [B][32][H][W] gradient of this conv's BN output
+    const float* dzpool;   // (instead of dz, optional) behind a 2x2 MaxPool: the routed gradient at the
+    const uint8_t* parg;   //   pooled resolution [B][32][H/2][W/2] and the window selection (conv_wino's
+                           //   EPI_BWD_POOLSELP / bn_relu_pool); dz is rebuilt while staging
     const float* y;        // [B][32][H][W] raw conv output
     const float4* cf_dy;   // {a, mb, mgi, mean}: dy = a (dz - mb - (y - mean) mgi)
     const float* yp;       // [B][32][H][W] producer's raw output: x = relu(s yp + t)

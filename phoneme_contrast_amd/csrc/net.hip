@@ -92,6 +92,12 @@ int build_small(Plan& p) {
         }
         stat = std::max(stat, (size_t)2 * L.cout * L.nblk + L.nblk);
     }
+    {  // layer 2's fused backward reads layer 3's pooled data gradient + selection (a quarter of dz2's bytes)
+        Layer &L2 = p.L[2], &L3 = p.L[3];
+        L2.pd = L2.wgbd && L3.pooled_in && L3.ysel && L3.wino && !(L2.H & 1) && L2.W % 4 == 0 &&
+                L3.H == L2.H / 2 && L3.W == L2.W / 2 && getenv("PCX_NO_POOLDZ") == nullptr;
+        for (int i = 0; L2.pd && i < L2.wb.nseg; ++i) L2.pd = !(L2.wb.seg_t0[i] & 1);
+    }
     // first-layer weight gradient slices
     {
         int64_t nrows = (int64_t)B * H1;
@@ -344,6 +350,11 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
             WinoBwdArgs w = L.wb;
             w.B = B; w.H = L.H; w.W = L.W;
             w.dz = at<float>(ws, L.dz);
+            if (L.pd) {  // layer 3's data gradient left dz2 pooled (EPI_BWD_POOLSELP): rebuilt while staging
+                w.dz = nullptr;
+                w.dzpool = at<float>(ws, L.dz);
+                w.parg = at<uint8_t>(ws, p.L[3].parg);
+            }
             w.y = at<float>(ws, L.y);
             w.cf_dy = at<float4>(ws, L.cfb);
             w.yp = at<float>(ws, Lp.y);
@@ -439,10 +450,14 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
             {
                 Scope sc(&p.prof, s, "conv_dgrad", l);
                 // pooled input with a recorded selection: the epilogue reads it at the pooled resolution
-                const int epi = !L.pooled_in ? EPI_BWD_RELU : L.ysel ? EPI_BWD_POOLSEL : EPI_BWD_POOL;
+                int epi = !L.pooled_in ? EPI_BWD_RELU : L.ysel ? EPI_BWD_POOLSEL : EPI_BWD_POOL;
                 if (epi == EPI_BWD_POOLSEL) {
                     c.ysel = at<float>(ws, L.ysel);
                     c.parg = at<uint8_t>(ws, L.parg);
+                    if (l == 3 && Lp.pd) {  // the fused layer-2 backward rebuilds dz2's windows itself
+                        epi = EPI_BWD_POOLSELP;
+                        c.dpool = dzp;
+                    }
                 }
                 RC(L.wino ? launch_conv3x3_wino(PRO_RAW, epi, c, s) : launch_conv3x3_dma(PRO_RAW, epi, c, s));
             }

@@ -139,6 +139,7 @@ struct Layer {  // one 3x3 conv of the trunk (L = 1..6)
     WinoWgradArgs ww;
     bool wgbd;             // weight AND data gradient in one kernel (wgbd_wino.hip: layer 2, W % 4 == 0)
     WinoBwdArgs wb;
+    bool pd;               // wgbd: dz read as layer 3's pooled gradient + window selection (EPI_BWD_POOLSELP)
 };
 
 struct DeepPlan;  // deep.hip

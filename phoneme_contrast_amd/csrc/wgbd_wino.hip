@@ -110,7 +110,8 @@ __device__ __forceinline__ void wmul(const WOps& o, float sx, float sy, f32x16 (
 
 // XCT: the ring's channel stride as a compile-time constant (LDS offsets become instruction immediates:
 // ~20 address VALU per 16-tile group less), or 0 for a runtime stride
-template <int V, int NIR, int XCT>
+// PD: dz rebuilt from the pooled gradient and the window selection (WinoBwdArgs::dzpool / parg)
+template <int V, int NIR, int XCT, bool PD>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void wgbd_wino_kernel(WinoBwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int NIT = 2 * NIR;  // staged items per thread and stage (two rows)
@@ -132,6 +133,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
     const float4 kx = a.cf_x[ch];
     const float xs = kx.x, xt = kx.y;
     vecf<V> dzv[NIT], yv[NIT], xv[NIT];
+    static_assert(!PD || V == 4, "pooled dz: 4-column items (two pooled columns)");
+    vecf<2> dpv[NIT];     // PD: the items' two pooled gradients
+    unsigned pav[NIT];    // PD: their two selection bytes
 
     // ---- Winograd row constants (both GEMMs combine the same patch rows: B^T row Q)
     const int IW = Q == 0 ? 0 : Q == 2 ? 2 : 1, IU = Q == 0 ? 2 : Q == 2 ? 1 : Q == 1 ? 2 : 3;
@@ -188,7 +192,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
         const int c0 = 2 * t0;
         const int ng = (S + 15) >> 4, Ks = S >> 1;
         const int64_t pb = (int64_t)b * CH * HW;
-        const __amdgpu_buffer_rsrc_t rdz = rsrc(a.dz + pb, (int64_t)CH * HW * 4);
+        const int Wp = W >> 1, HWp = (H >> 1) * Wp;
+        const int64_t pbp = (int64_t)b * CH * HWp;
+        const __amdgpu_buffer_rsrc_t rdz = PD ? rsrc(a.dzpool + pbp, (int64_t)CH * HWp * 4) : rsrc(a.dz + pb, (int64_t)CH * HW * 4);
+        const __amdgpu_buffer_rsrc_t rpa = rsrc(reinterpret_cast<const float*>(PD ? a.parg + pbp : nullptr),
+                                                PD ? (int64_t)CH * HWp : 0);
         const __amdgpu_buffer_rsrc_t ry = rsrc(a.y + pb, (int64_t)CH * HW * 4);
         const __amdgpu_buffer_rsrc_t rx = rsrc(a.yp + pb, (int64_t)CH * HW * 4);
         // item columns: c0 - V + V k .. + V - 1 (all in or all out: V divides W and c0); LDS position V k - V + 1
@@ -208,6 +216,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
             return colok & (((unsigned)r0 < (unsigned)H ? ~R1 : 0u) | ((unsigned)r1 < (unsigned)H ? R1 : 0u));
         };
         auto goff = [&](int m, int st) { return ch * HW + (2 * st + 1 + m / NIR) * W + c0 - V + V * (j0 + 16 * (m % NIR)); };
+        // PD: the item's pooled offset: row (2 st + 1 + r) / 2 = st + r (r = m / NIR), columns
+        // (c0 - V + V k) / 2 .. + 1 for k = j0 + 16 (m % NIR)
+        auto poff_ = [&](int m, int st, int pbase) { return pbase + (st + m / NIR) * Wp + (V / 2) * 16 * (m % NIR); };
         // items of stage st loaded at group gi of ngr (all of them for ngr = 0): the next tile row's loads
         // are spread over the current row's groups (a burst of 3 NIT loads per wave at the row start stalls
         // the issuing waves of every SIMD on the texture unit, MFMA pipes idle)
@@ -217,11 +228,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
             return;
 #endif
             const unsigned ok = rowmask(st);
+            int pbase = ch * HWp + ((c0 - V + V * j0) >> 1);
+            if constexpr (PD) asm volatile("" : "+v"(pbase));  // opaque: offsets formed at the loads
 #pragma unroll
             for (int m = 0; m < NIT; ++m) {
                 if (ngr && (m * ngr) / NIT != gi) continue;
                 const int o = (ok >> m) & 1 ? 4 * goff(m, st) : OOB;
-                dzv[m] = bload<V>(rdz, o);
+                if constexpr (PD) {
+                    const int op = (ok >> m) & 1 ? poff_(m, st, pbase) : OOB / 4;
+                    dpv[m] = bload<2>(rdz, 4 * op);
+                    pav[m] = (unsigned)__builtin_amdgcn_raw_buffer_load_b16(rpa, op, 0, 0);
+                } else {
+                    dzv[m] = bload<V>(rdz, o);
+                }
                 yv[m] = bload<V>(ry, o);
                 xv[m] = bload<V>(rx, o);
             }
@@ -237,6 +256,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
                 if (!((exist >> m) & 1)) continue;
                 const bool in = (ok >> m) & 1;
                 const float a3 = in ? A3 : 0.f, tt = in ? xt : 0.f;
+                if constexpr (PD) {
+                    // dz of the 4 columns: each pooled gradient goes to its window's selected element (row
+                    // parity i of this image row, column parity j), zero elsewhere
+                    const unsigned i2 = 2u * (unsigned)((2 * st + 1 + m / NIR) & 1);
+#pragma unroll
+                    for (int e = 0; e < V; ++e) {
+                        const unsigned sel = (pav[m] >> (8 * (e >> 1))) & 3u;
+                        dzv[m][e] = sel == i2 + (unsigned)(e & 1) ? dpv[m][e >> 1] : 0.f;
+                    }
+                }
                 vecf<V> d, x;
 #pragma unroll
                 for (int e = 0; e < V; ++e) {
@@ -504,17 +533,22 @@ int launch_wgbd_wino(WinoBwdArgs a, hipStream_t s) {
                   "wgbd_wino: geometry mismatch");
     PCX_CHECK_ARG(a.dz && a.y && a.cf_dy && a.yp && a.cf_x && a.up && a.part && a.dzp && a.bn0 && a.bn1,
                   "wgbd_wino: NULL argument");
-#define PCX_WB(XC_)                                                                                    \
-    if (a.XCS == XC_ || XC_ == 0) {                                                                    \
-        (void)hipFuncSetAttribute((const void*)wgbd_wino_kernel<4, 2, XC_>,                            \
+    const bool pd = a.dzpool != nullptr;
+    if (pd) {  // pooled dz: whole windows, 2-byte aligned selection pairs (even strip starts)
+        PCX_CHECK_ARG(a.parg && !(a.H & 1) && a.W % 4 == 0, "wgbd_wino: pooled dz needs parg, even H, W %% 4 == 0");
+        for (int i = 0; i < a.nseg; ++i) PCX_CHECK_ARG(!(a.seg_t0[i] & 1), "wgbd_wino: odd strip start %d", a.seg_t0[i]);
+    }
+#define PCX_WB(XC_, PD_)                                                                               \
+    if ((a.XCS == XC_ || XC_ == 0) && pd == PD_) {                                                     \
+        (void)hipFuncSetAttribute((const void*)wgbd_wino_kernel<4, 2, XC_, PD_>,                       \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)a.lds);              \
-        wgbd_wino_kernel<4, 2, XC_><<<dim3((unsigned)a.nslice), 512, a.lds, s>>>(a);                   \
+        wgbd_wino_kernel<4, 2, XC_, PD_><<<dim3((unsigned)a.nslice), 512, a.lds, s>>>(a);              \
         PCX_LAUNCH_CHECK("wgbd_wino_kernel");                                                          \
         return PCX_OK;                                                                                 \
     }
-    PCX_WB(110)  // T = 200 (strips of 48 / 52 tiles)
-    PCX_WB(106)  // T = 100
-    PCX_WB(0)
+    PCX_WB(110, false) PCX_WB(110, true)  // T = 200 (strips of 48 / 52 tiles)
+    PCX_WB(106, false)                    // T = 100
+    PCX_WB(0, false) PCX_WB(0, true)
 #undef PCX_WB
     return PCX_OK;
 }

@@ -40,10 +40,12 @@ def test_winograd_epilogues_match_direct_engine(case):
 
 
 WB = os.path.join(ROOT, "tools", "wb_bench")
-WB_CASES = [  # H, W, B, reps: the fused layer-2 backward (wgbd_wino) vs wgrad_wino + conv_wino's data gradient
+WB_CASES = [  # H, W, B, reps [, pooled dz]: the fused layer-2 backward (wgbd_wino) vs wgrad_wino + conv_wino's data gradient
     (40, 200, 48, 1),   # cnn_small T = 200: strips of 48 + 52 tiles
     (20, 100, 24, 1),   # T = 100: one 50-tile strip (4 data-gradient groups, the last partial)
     (21, 56, 16, 1),    # odd H (a half tile row at the bottom), one 28-tile strip
+    (40, 200, 48, 1, 1),  # dz as layer 3's pooled gradient + window selection (EPI_BWD_POOLSELP's output)
+    (20, 100, 24, 1, 1),
 ]
 
 

@@ -1,7 +1,9 @@
 // Cross-check + timing of the fused layer-2 backward (wgbd_wino: Winograd weight AND data gradient in
 // one pass) against the two-kernel path it replaces (wgrad_wino writing dy, then conv_wino's data
 // gradient with the EPI_BWD_RELU epilogue), on random operands of one shape.
-//   wb_bench H W [B] [reps]
+//   wb_bench H W [B] [reps] [pd]      pd = 1: the fused kernel reads dz as a pooled gradient + 2x2 window
+//                                     selection (WinoBwdArgs::dzpool / parg); the reference gets the
+//                                     expanded full-resolution dz
 // Prints both times and the differences: dW (max |a - b| / max |b|), dz_prev (max |a - b| / max |b|),
 // the producer-BN backward sums (relative, per channel).  Exit 2 when a difference exceeds 2e-5
 // (tests/test_wino_engine_gpu.py runs it).
@@ -19,6 +21,28 @@ __global__ void fill(float* p, size_t n, unsigned seed, float scale, float off) 
         unsigned h = (unsigned)i * 2654435761u ^ seed;
         h ^= h >> 13; h *= 0x5bd1e995; h ^= h >> 15;
         p[i] = off + scale * ((h & 0xffffff) / 16777216.0f - 0.5f);
+    }
+}
+
+// dz[b][c][2h + i][2w + j] = sel[b][c][h][w] == 2 i + j ? dp[b][c][h][w] : 0
+__global__ void expand_pool(const float* dp, const uint8_t* sel, float* dz, size_t np, int Wp) {
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    for (; i < np; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t row = i / Wp, w = i - row * Wp;  // row = (b c) Hp + h
+        const int s = sel[i] & 3;
+        float* o = dz + (2 * row) * (2 * (size_t)Wp) + 2 * w;
+        o[0] = s == 0 ? dp[i] : 0.f;
+        o[1] = s == 1 ? dp[i] : 0.f;
+        o[2 * Wp] = s == 2 ? dp[i] : 0.f;
+        o[2 * Wp + 1] = s == 3 ? dp[i] : 0.f;
+    }
+}
+__global__ void fill_sel(uint8_t* p, size_t n, unsigned seed) {
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    for (; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        unsigned h = (unsigned)i * 2246822519u ^ seed;
+        h ^= h >> 15; h *= 0x2c1b3c6d; h ^= h >> 12;
+        p[i] = (uint8_t)(h & 3);
     }
 }
 
@@ -44,6 +68,7 @@ int main(int argc, char** argv) {
     if (argc < 3) { printf("usage: wb_bench H W [B] [reps]\n"); return 2; }
     const int H = atoi(argv[1]), W = atoi(argv[2]);
     const int B = argc > 3 ? atoi(argv[3]) : 4096, reps = argc > 4 ? atoi(argv[4]) : 5;
+    const bool pd = argc > 5 && atoi(argv[5]) != 0;
     const int C = 32;
     pcx::WinoBwdArgs f{};
     pcx::WinoWgradArgs w{};
@@ -67,10 +92,19 @@ int main(int argc, char** argv) {
     fill<<<1, 256>>>(wt, nw, 6, 0.4f, 0.f);
     (void)hipMemset(dzp1, 0, n * 4); (void)hipMemset(dzp2, 0, n * 4);
     check(pcx::launch_wino_pack(wt, up, C, C, 1, 0), "wino_pack");
+    float* dpool = nullptr;
+    uint8_t* sel = nullptr;
+    if (pd) {  // a pooled gradient + selection; the reference path reads its expansion
+        const size_t np = n / 4;
+        (void)hipMalloc(&dpool, np * 4); (void)hipMalloc(&sel, np);
+        fill<<<4096, 256>>>(dpool, np, 7, 2.f, 0.f);
+        fill_sel<<<4096, 256>>>(sel, np, 8);
+        expand_pool<<<4096, 256>>>(dpool, sel, dz, np, W / 2);
+    }
 
     // fused
     f.B = B; f.H = H; f.W = W;
-    f.dz = dz; f.y = y; f.cf_dy = (const float4*)cfd; f.yp = yp; f.cf_x = (const float4*)cfx; f.up = up;
+    f.dz = pd ? nullptr : dz; f.dzpool = dpool; f.parg = sel; f.y = y; f.cf_dy = (const float4*)cfd; f.yp = yp; f.cf_x = (const float4*)cfx; f.up = up;
     f.part = part; f.dzp = dzp1; f.bn0 = bn; f.bn1 = bn + (size_t)C * f.nslice;
     auto fused = [&]() {
         check(pcx::launch_wgbd_wino(f, 0), "wgbd_wino");
@@ -134,8 +168,8 @@ int main(int argc, char** argv) {
     for (int i = 0; i < reps; ++i) twok();
     (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
     (void)hipEventElapsedTime(&tr, e0, e1);
-    printf("wgbd H=%d W=%d B=%d strips=%d (%d,%d) nslice=%d: fused %.3f ms, two-kernel %.3f ms; "
-           "dW rel %.2e, dz_prev rel %.2e, BN sums rel %.2e\n", H, W, B, f.nseg, f.seg_S[0], f.seg_S[1], f.nslice,
+    printf("wgbd%s H=%d W=%d B=%d strips=%d (%d,%d) nslice=%d: fused %.3f ms, two-kernel %.3f ms; "
+           "dW rel %.2e, dz_prev rel %.2e, BN sums rel %.2e\n", pd ? " (pooled dz)" : "", H, W, B, f.nseg, f.seg_S[0], f.seg_S[1], f.nslice,
            tf / reps, tr / reps, ew, ed, eb);
     return (ew < 2e-5 && ed < 2e-5 && eb < 2e-5) ? 0 : 2;
 }
