@@ -531,7 +531,8 @@ int launch_wgbd_wino(WinoBwdArgs a, hipStream_t s) {
     PCX_CHECK_ARG(g.XCS == a.XCS && g.nslice == a.nslice && g.per_slice == a.per_slice && g.ntask == a.ntask &&
                       g.nseg == a.nseg,
                   "wgbd_wino: geometry mismatch");
-    PCX_CHECK_ARG(a.dz && a.y && a.cf_dy && a.yp && a.cf_x && a.up && a.part && a.dzp && a.bn0 && a.bn1,
+    PCX_CHECK_ARG((a.dz != nullptr) != (a.dzpool != nullptr), "wgbd_wino: exactly one of dz / dzpool");
+    PCX_CHECK_ARG(a.y && a.cf_dy && a.yp && a.cf_x && a.up && a.part && a.dzp && a.bn0 && a.bn1,
                   "wgbd_wino: NULL argument");
     const bool pd = a.dzpool != nullptr;
     if (pd) {  // pooled dz: whole windows, 2-byte aligned selection pairs (even strip starts)
