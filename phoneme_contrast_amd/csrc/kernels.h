@@ -125,6 +125,8 @@ int launch_wgrad_s(int pro, WgradArgs a, hipStream_t s);
 struct WinoWgradArgs {
     int B, H, W, cin, cout;
     const float* dz;
+    const float* dzpool;  // (instead of dz, optional) behind a 2x2 MaxPool: the routed gradient at the pooled
+    const uint8_t* parg;  //   resolution + the window selection (conv_wino EPI_BWD_POOLSELP); dz rebuilt
     const float* y;
     const float4* cf_dy;  // {a, mb, mgi, mean}: dy = BN backward of (dz, y)
     const float* src;     // x (raw, or the producer's y under PRO_BNRELU)

@@ -97,6 +97,11 @@ int build_small(Plan& p) {
         L2.pd = L2.wgbd && L3.pooled_in && L3.ysel && L3.wino && !(L2.H & 1) && L2.W % 4 == 0 &&
                 L3.H == L2.H / 2 && L3.W == L2.W / 2 && getenv("PCX_NO_POOLDZ") == nullptr;
         for (int i = 0; L2.pd && i < L2.wb.nseg; ++i) L2.pd = !(L2.wb.seg_t0[i] & 1);
+        // likewise layer 4's Winograd weight gradient behind layer 5's pool (its data gradient reads dy)
+        Layer &L4 = p.L[4], &L5 = p.L[5];
+        L4.pd = L4.wgw && !L4.wgbd && !L4.pooled_in && L5.pooled_in && L5.ysel && L5.wino && !(L4.H & 1) &&
+                L4.W % 4 == 0 && L4.ww.V == 4 && (L4.ww.nseg == 1 || !(L4.ww.S & 1)) && L5.H == L4.H / 2 &&
+                L5.W == L4.W / 2 && getenv("PCX_NO_POOLDZ") == nullptr;
     }
     // first-layer weight gradient slices
     {
@@ -381,6 +386,11 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
             WinoWgradArgs w = L.ww;
             w.B = B; w.H = L.H; w.W = L.W; w.cin = L.cin; w.cout = L.cout;
             w.dz = at<float>(ws, L.dz);
+            if (L.pd) {  // the next layer's data gradient left dz pooled (EPI_BWD_POOLSELP): rebuilt while staging
+                w.dz = nullptr;
+                w.dzpool = at<float>(ws, L.dz);
+                w.parg = at<uint8_t>(ws, p.L[l + 1].parg);
+            }
             w.y = at<float>(ws, L.y);
             w.cf_dy = at<float4>(ws, L.cfb);
             w.src = L.pooled_in ? at<float>(ws, L.xp) : at<float>(ws, Lp.y);
@@ -454,7 +464,7 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
                 if (epi == EPI_BWD_POOLSEL) {
                     c.ysel = at<float>(ws, L.ysel);
                     c.parg = at<uint8_t>(ws, L.parg);
-                    if (l == 3 && Lp.pd) {  // the fused layer-2 backward rebuilds dz2's windows itself
+                    if (Lp.pd) {  // the previous layer's weight gradient rebuilds dz's windows itself
                         epi = EPI_BWD_POOLSELP;
                         c.dpool = dzp;
                     }

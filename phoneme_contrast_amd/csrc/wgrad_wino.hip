@@ -126,7 +126,7 @@ __device__ __forceinline__ void kloop(const float* w, const float* u, const floa
 }
 
 // one wave's work: Winograd row Q = wave (elements 4 Q .. 4 Q + 3) of the 32 x 32 channel block
-template <int PRO, int V>
+template <int PRO, int V, bool PD>
 __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int co0, int ci0, int slice) {
     const int tid = threadIdx.x, lane = tid & 63, c32 = lane & 31, g = lane >> 5;
     const int Q = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -168,12 +168,18 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
     const int TR = (H + 1) >> 1;
     const int t0s = slice * a.per_slice, t1s = min(a.ntask, t0s + a.per_slice);
     vecf<V> dzv[NIT], yv[NIT], xv[NIT];
+    static_assert(!PD || V == 4, "pooled dz: 4-column items");
+    const int Wp = W >> 1, HWp = (H >> 1) * Wp;
 
     for (int task = t0s; task < t1s; ++task) {
         const int b = task / a.nseg;
         const int t0 = (task - b * a.nseg) * a.S;
         const int c0 = 2 * t0;
-        const __amdgpu_buffer_rsrc_t rdz = rsrc(a.dz + ((int64_t)b * a.cout + co0) * HW, (int64_t)32 * HW * 4);
+        const __amdgpu_buffer_rsrc_t rdz = PD ? rsrc(a.dzpool + ((int64_t)b * a.cout + co0) * HWp, (int64_t)32 * HWp * 4)
+                                              : rsrc(a.dz + ((int64_t)b * a.cout + co0) * HW, (int64_t)32 * HW * 4);
+        const __amdgpu_buffer_rsrc_t rpa =
+            rsrc(reinterpret_cast<const float*>(PD ? a.parg + ((int64_t)b * a.cout + co0) * HWp : nullptr),
+                 PD ? (int64_t)32 * HWp : 0);
         const __amdgpu_buffer_rsrc_t ry = rsrc(a.y + ((int64_t)b * a.cout + co0) * HW, (int64_t)32 * HW * 4);
         const __amdgpu_buffer_rsrc_t rdo =
             rsrc(write_dy ? a.dy_out + ((int64_t)b * a.cout + co0) * HW : a.dz, write_dy ? (int64_t)32 * HW * 4 : 0);
@@ -205,11 +211,21 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
             masks(st, dm, xm);
             int db = 2 * st * W + c0 + dgb;
             asm volatile("" : "+v"(db));  // opaque: per-item offsets formed at the load, not kept live
+            int pb = ch * HWp + st * Wp + ((c0 + V * j0) >> 1);  // PD: pooled row st (dy rows 2 st, 2 st + 1)
+            if constexpr (PD) asm volatile("" : "+v"(pb));
 #pragma unroll
             for (int m = 0; m < NIT; ++m) {
                 if (part >= 0 && m * NPT / NIT != part) continue;
                 const int o = (dm >> m) & 1 ? 4 * (dgo(m) - dgb + db) : OOB;
-                dzv[m] = bload<V>(rdz, o);
+                if constexpr (PD) {  // (held in dzv[m]: the two pooled gradients and the selection bytes)
+                    const int op = (dm >> m) & 1 ? pb + 4 * V * (m % NIR) : OOB / 4;
+                    const vecf<2> dp = bload<2>(rdz, 4 * op);
+                    dzv[m][0] = dp[0];
+                    dzv[m][1] = dp[1];
+                    dzv[m][2] = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_raw_buffer_load_b16(rpa, op, 0, 0));
+                } else {
+                    dzv[m] = bload<V>(rdz, o);
+                }
                 yv[m] = bload<V>(ry, o);
             }
         };
@@ -220,6 +236,13 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
 #pragma unroll
             for (int m = 0; m < NIT; ++m) {
                 const float a3 = (dm >> m) & 1 ? A3 : 0.f;
+                if constexpr (PD) {  // dz: each pooled gradient at its window's selected element (row parity m / NIR)
+                    const float g0 = dzv[m][0], g1 = dzv[m][1];
+                    const unsigned pa = __builtin_bit_cast(unsigned, dzv[m][2]), i2 = 2u * (unsigned)(m / NIR);
+#pragma unroll
+                    for (int e = 0; e < V; ++e)
+                        dzv[m][e] = ((pa >> (8 * (e >> 1))) & 3u) == i2 + (unsigned)(e & 1) ? (e >> 1 ? g1 : g0) : 0.f;
+                }
 #pragma unroll
                 for (int e = 0; e < V; ++e) dzv[m][e] = fma1(A1, dzv[m][e], fma1(A2, yv[m][e], a3));
             }
@@ -341,7 +364,7 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
     }
 }
 
-template <int PRO, int V>
+template <int PRO, int V, bool PD>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void wgrad_wino_kernel(WinoWgradArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x;
@@ -355,7 +378,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
     const int nz = 4 + 4 * 32 * a.XCS + 2 * 32 * a.DCS;
     for (int i = tid; i < nz; i += 256) smem[i] = 0.f;
     __syncthreads();
-    ww_body<PRO, V>(a, smem, co0, ci0, slice);
+    ww_body<PRO, V, PD>(a, smem, co0, ci0, slice);
 }
 
 // dW[n][c] = G^T dU G per (n, c) from the slices' sum (float64, fixed order); the partials carry
@@ -476,18 +499,24 @@ int launch_wgrad_wino(int pro, WinoWgradArgs a, hipStream_t s) {
     PCX_CHECK_ARG(pro == PRO_RAW || pro == PRO_BNRELU, "wgrad_wino: prologue %d", pro);
     const int ngroups = (a.cout / 32) * (a.cin / 32);
     dim3 grid((unsigned)(((a.nslice + 7) / 8) * 8 * ngroups));
-#define PCX_WW(P_, V_)                                                                                   \
-    if (pro == P_ && a.V == V_) {                                                                        \
-        (void)hipFuncSetAttribute((const void*)wgrad_wino_kernel<P_, V_>,                                \
+    PCX_CHECK_ARG((a.dz != nullptr) != (a.dzpool != nullptr), "wgrad_wino: exactly one of dz / dzpool");
+    const bool pd = a.dzpool != nullptr;
+    // pooled dz: 4-column items over whole windows, 2-byte aligned selection pairs (even strip starts)
+    PCX_CHECK_ARG(!pd || (a.parg && pro == PRO_BNRELU && a.V == 4 && !(a.H & 1) && (a.nseg == 1 || !(a.S & 1))),
+                  "wgrad_wino: pooled dz needs parg, PRO_BNRELU, V = 4, even H and even strip starts");
+#define PCX_WW(P_, V_, PD_)                                                                              \
+    if (pro == P_ && a.V == V_ && pd == PD_) {                                                           \
+        (void)hipFuncSetAttribute((const void*)wgrad_wino_kernel<P_, V_, PD_>,                           \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)a.lds);               \
-        wgrad_wino_kernel<P_, V_><<<grid, 256, a.lds, s>>>(a);                                           \
+        wgrad_wino_kernel<P_, V_, PD_><<<grid, 256, a.lds, s>>>(a);                                      \
         PCX_LAUNCH_CHECK("wgrad_wino_kernel");                                                           \
         return PCX_OK;                                                                                   \
     }
-    PCX_WW(PRO_RAW, 4)
-    PCX_WW(PRO_RAW, 2)
-    PCX_WW(PRO_BNRELU, 4)
-    PCX_WW(PRO_BNRELU, 2)
+    PCX_WW(PRO_RAW, 4, false)
+    PCX_WW(PRO_RAW, 2, false)
+    PCX_WW(PRO_BNRELU, 4, false)
+    PCX_WW(PRO_BNRELU, 2, false)
+    PCX_WW(PRO_BNRELU, 4, true)  // cnn_small layer 4 (behind layer 5's pool)
 #undef PCX_WW
     set_error("wgrad_wino: unsupported combination (pro %d, vec %d)", pro, a.V);
     return PCX_EINVAL;

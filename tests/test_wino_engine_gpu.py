@@ -57,3 +57,20 @@ def test_fused_layer2_backward_matches_two_kernel_path(case):
     r = subprocess.run([WB] + [str(v) for v in case], capture_output=True, text=True, timeout=120)
     print(r.stdout)
     assert r.returncode == 0, (case, r.stdout, r.stderr)
+
+
+WW = os.path.join(ROOT, "tools", "ww_bench")
+WW_CASES = [  # H, W, cin, cout, B, reps, prologue, pooled dz
+    (20, 100, 64, 64, 48, 1, 1, 1),  # cnn_small layer 4 behind layer 5's pool: dz rebuilt from the selection
+    (20, 100, 64, 64, 48, 1, 1, 0),
+]
+
+
+@pytest.mark.parametrize("case", WW_CASES)
+def test_winograd_wgrad_pooled_dz_matches_pixel_stream(case):
+    """wgrad_wino reading dz as a pooled gradient + window selection (EPI_BWD_POOLSELP's output) against
+    the pixel-stream weight gradient on the expanded full-resolution dz (dW within 1e-4, dy exact)."""
+    assert os.path.exists(WW), "tools/ww_bench missing: run make"
+    r = subprocess.run([WW] + [str(v) for v in case], capture_output=True, text=True, timeout=120)
+    print(r.stdout)
+    assert r.returncode == 0, (case, r.stdout, r.stderr)
