@@ -169,6 +169,7 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
     const int t0s = slice * a.per_slice, t1s = min(a.ntask, t0s + a.per_slice);
     vecf<V> dzv[NIT], yv[NIT], xv[NIT];
     static_assert(!PD || V == 4, "pooled dz: 4-column items");
+    unsigned pav[NIT];  // PD: the items' two selection bytes (their two pooled gradients wait in dzv[m][0..1])
     const int Wp = W >> 1, HWp = (H >> 1) * Wp;
 
     for (int task = t0s; task < t1s; ++task) {
@@ -217,12 +218,12 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
             for (int m = 0; m < NIT; ++m) {
                 if (part >= 0 && m * NPT / NIT != part) continue;
                 const int o = (dm >> m) & 1 ? 4 * (dgo(m) - dgb + db) : OOB;
-                if constexpr (PD) {  // (held in dzv[m]: the two pooled gradients and the selection bytes)
+                if constexpr (PD) {
                     const int op = (dm >> m) & 1 ? pb + 4 * V * (m % NIR) : OOB / 4;
                     const vecf<2> dp = bload<2>(rdz, 4 * op);
                     dzv[m][0] = dp[0];
                     dzv[m][1] = dp[1];
-                    dzv[m][2] = __builtin_bit_cast(float, (unsigned)__builtin_amdgcn_raw_buffer_load_b16(rpa, op, 0, 0));
+                    pav[m] = (unsigned)__builtin_amdgcn_raw_buffer_load_b16(rpa, op, 0, 0);
                 } else {
                     dzv[m] = bload<V>(rdz, o);
                 }
@@ -238,7 +239,7 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
                 const float a3 = (dm >> m) & 1 ? A3 : 0.f;
                 if constexpr (PD) {  // dz: each pooled gradient at its window's selected element (row parity m / NIR)
                     const float g0 = dzv[m][0], g1 = dzv[m][1];
-                    const unsigned pa = __builtin_bit_cast(unsigned, dzv[m][2]), i2 = 2u * (unsigned)(m / NIR);
+                    const unsigned pa = pav[m], i2 = 2u * (unsigned)(m / NIR);
 #pragma unroll
                     for (int e = 0; e < V; ++e)
                         dzv[m][e] = ((pa >> (8 * (e >> 1))) & 3u) == i2 + (unsigned)(e & 1) ? (e >> 1 ? g1 : g0) : 0.f;

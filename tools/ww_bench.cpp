@@ -117,5 +117,15 @@ int main(int argc, char** argv) {
            "%.3f exec) + reduce %.3f ms | dW rel %.2e (worst [%d] %g vs %g) dy diff %.2e of %.2e\n",
            pd ? "(pooled dz) " : "", H, W, cin, cout, pro, B, ms_s, fl / ms_s / 1e9 / 157.3, w.S, w.V, w.nslice, ms_w, fl / ms_w / 1e9 / 157.3,
            fl * 4 / 9 / ms_w / 1e9 / 157.3, ms_r, emax / gmax, worst, h2[worst], h1[worst], dmax, dyabs);
-    return (emax / gmax < 1e-4 && dmax <= 1e-6 * dyabs) ? 0 : 3;
+    const bool ok = emax / gmax < 1e-4 && dmax <= 1e-6 * dyabs;
+    if (!ok) {  // the first dy mismatches as (sample, channel, row, column)
+        int shown = 0;
+        for (size_t i = 0; i < ny && shown < 8; ++i)
+            if (std::fabs((double)d1[i] - d2[i]) > 1e-6 * dyabs) {
+                const size_t wq = i % W, hq = (i / W) % H, cq = (i / ((size_t)W * H)) % cout, bq = i / ((size_t)W * H * cout);
+                printf("  dy mismatch b %zu c %zu h %zu w %zu: %g vs %g\n", bq, cq, hq, wq, d2[i], d1[i]);
+                ++shown;
+            }
+    }
+    return ok ? 0 : 3;
 }
