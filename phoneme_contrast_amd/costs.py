@@ -25,6 +25,10 @@ def kernel_costs(B, F, T, D=128):
     L = {l: (ci, co, h, w) for l, ci, co, h, w in small_layers(B, F, T)}
     src_res = {1: (F, T), 2: (F, T), 3: (F, T), 4: (F // 2, T // 2), 5: (F // 2, T // 2), 6: (F // 4, T // 4)}
     out = {}
+    # pooled gradient hand-over (net.hip Layer::pd, even widths): layer 3 / 5's data gradient writes the
+    # routed gradient at the pooled resolution and layer 2 / 4's weight gradient rebuilds dz from it and the
+    # window selection (4 + 1 bytes per pooled element instead of 4 per full-resolution element)
+    pd = {2: T % 4 == 0 and F % 2 == 0, 4: (T // 2) % 4 == 0 and (F // 2) % 2 == 0}
     for l, (ci, co, h, w) in L.items():
         macs = B * h * w * co * ci * 9
         sh, sw = src_res[l]
@@ -41,11 +45,13 @@ def kernel_costs(B, F, T, D=128):
         # selection (y at the selected element + its index: 5 bytes per pooled input, EPI_BWD_POOLSEL) --
         # and writes dz_{l-1} at full resolution
         prod = 5 * B * ci * h * w if (sh, sw) != (h, w) else x_in
-        out[f"conv_dgrad_L{l}"] = (2 * macs, y_out + prod + x_in)
-        # wgrad: reads dz_l, y_l and the forward input source
-        out[f"wgrad_L{l}"] = (2 * macs, 2 * y_out + x_in)
+        dz_prev = B * ci * h * w * 4 if pd.get(l - 1) else x_in  # pooled hand-over: dz_{l-1} at h x w
+        out[f"conv_dgrad_L{l}"] = (2 * macs, y_out + prod + dz_prev)
+        # wgrad: reads dz_l (or its pooled form + selection), y_l and the forward input source
+        dz_in = y_out * 5 // 16 if pd.get(l) else y_out
+        out[f"wgrad_L{l}"] = (2 * macs, dz_in + y_out + x_in)
         if l == 2:  # the fused layer-2 backward (wgbd_wino.hip): both GEMMs; dz2, y2, y1 read, dz1 written
-            out["wgbd_L2"] = (4 * macs, 2 * y_out + 2 * x_in)
+            out["wgbd_L2"] = (4 * macs, dz_in + y_out + 2 * x_in)
     # elementwise / head passes (bytes: each tensor read once, each output written once)
     H1, W1, H3, W3, H5, W5 = F, T, F // 2, T // 2, F // 4, T // 4
     # (+ the recorded selection for the pooled data gradient: y at the selected element, its index)
