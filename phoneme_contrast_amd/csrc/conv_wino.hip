@@ -524,7 +524,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     const int nunits = a.B * g.BPS * g.ncg;
     const int G = gridDim.x;
     // XCD-contiguous slot of this workgroup inside a round (dispatch is round-robin over the 8 XCDs)
-    const int slot = (G & 7) ? (int)blockIdx.x : (int)(blockIdx.x & 7) * (G >> 3) + (int)(blockIdx.x >> 3);
+    const int slot = ((G & 7) || g.naive_slots) ? (int)blockIdx.x : (int)(blockIdx.x & 7) * (G >> 3) + (int)(blockIdx.x >> 3);
+    // Unit queue (a.queue): the static order u = it G + slot lets the workgroups drift apart over the
+    // ~250 rounds of a B = 4096 launch, and the halo rows two neighbouring units share then miss the XCD's
+    // L2 (L2-miss bytes 2.1x the input at B = 4096 against 1.3x at B = 512: profiles/r4_wino_l2_order.txt).
+    // With the queue each XCD's workgroups take the units of one contiguous eighth of the launch in
+    // order from that XCD's counter (then help the other XCDs), so neighbours are in flight together.
+    const int nq = (a.queue && !(G & 7)) ? 8 : 1;
+    int* qsl = reinterpret_cast<int*>(red + 512);  // [2]: the next unit, by unit parity
+    auto grab = [&]() -> int {  // lane 0 of wave 0 only
+        const int x0 = nq == 8 ? (int)(blockIdx.x & 7) : 0;
+        for (int k = 0; k < nq; ++k) {
+            const int q = (x0 + k) & (nq - 1);
+            const int lo = (int)((int64_t)q * nunits / nq), len = (int)((int64_t)(q + 1) * nunits / nq) - lo;
+            const int v = atomicAdd(a.queue + 32 * q, 1);
+            if (v < len) return lo + v;
+        }
+        return nunits;
+    };
 
     struct Unit { int b, tb, cg, tw, tr_a, tc_a; };
     // (wave-uniform divisions by float reciprocals: a few VALU instead of ~30 per integer division)
@@ -611,6 +628,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
 
     const int nchunk = a.cin / CK;
     int u = slot;
+    if (a.queue) {
+        if (tid == 0) qsl[0] = grab();
+        __syncthreads();
+        u = __builtin_amdgcn_readfirstlane(qsl[0]);
+    }
+    int par = 0;  // unit parity (queue slot of the next unit: qsl[par ^ 1])
     Unit cur = unit_of(u < nunits ? u : 0);
     if (u < nunits) {
         plan_copies(cur);
@@ -618,8 +641,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     }
     int kk = 0;  // chunks issued so far (buffer = kk & 1)
     while (u < nunits) {
-        const int un = u + G;
-        const Unit nxt = unit_of(un < nunits ? un : u);
+        // next unit: static, or taken from the queue now (its atomic returns while this unit's first
+        // chunks run) and published to the block through LDS in the last chunk
+        int un = u + G;
+        int qv = 0;
+        if (a.queue && tid == 0) qv = grab();
+        Unit nxt = unit_of(un < nunits ? un : u);
         // this lane's tile of the current unit
         const int len_a = min(16, g.TC - cur.tc_a);
         const bool seg1 = n >= len_a;
@@ -730,6 +757,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
             };
             auto chunk = [&](int k, auto ftag) {
                 const int c0 = k * CK;
+                if (a.queue && tid == 0 && k + 1 == nchunk) qsl[par ^ 1] = qv;
 #if !(defined(WINO_KO) && (WINO_KO & 4))  // analysis builds only: no chunk synchronisation
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();  // chunk kk visible; chunk kk-1 fully consumed
@@ -737,6 +765,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
                 // the next chunk (of this unit, or the next unit's first), copied part by part
                 // ahead of this chunk's K-steps
                 const bool more = k + 1 < nchunk;
+                if (!more && a.queue) {
+                    un = __builtin_amdgcn_readfirstlane(qsl[par ^ 1]);
+                    nxt = unit_of(un < nunits ? un : u);
+                }
                 const bool pre = more || un < nunits;
                 if (!more && pre) plan_copies(nxt);
                 const Unit& tgt = more ? cur : nxt;
@@ -802,6 +834,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
 #endif
         u = un;
         cur = nxt;
+        par ^= 1;
+    }
+    // the last workgroup out leaves the queue zero for the next launch (every workgroup has taken its
+    // last unit: its own counter and the others' are past their ranges)
+    if (a.queue && tid == 0) {
+        __threadfence();
+        if (atomicAdd(a.queue + 32 * 8, 1) == G - 1) {
+            for (int q = 0; q < 9; ++q) atomicExch(a.queue + 32 * q, 0);
+        }
     }
 }
 
@@ -887,13 +928,15 @@ int launch_conv3x3_wino(int pro, int epi, ConvArgs a, hipStream_t s) {
     PCX_CHECK_ARG(epi != EPI_BWD_POOLSELP || a.dpool, "conv3x3_wino: EPI_BWD_POOLSELP needs dpool");
     const int ck = wino_ck(a.cin);
     const size_t buff = (size_t)4 * (ck * WSP + 32) + (size_t)ck * 512;
-    const size_t smem = (2 * buff + 2 * (size_t)a.cin + 512) * 4;
+    const size_t smem = (2 * buff + 2 * (size_t)a.cin + 512 + 4) * 4;  // + the queue's 2 ints
     PCX_CHECK_ARG(smem <= 160 * 1024, "conv3x3_wino: %zu B of LDS", smem);
     // persistent workgroups: two per CU (a multiple of 8, one XCD-contiguous run of units each round)
     const int64_t units = (int64_t)a.B * g.BPS * g.ncg;
     int64_t nwg = std::min<int64_t>(units, 2 * (int64_t)num_cus());
     if (nwg >= 8) nwg &= ~(int64_t)7;
     dim3 grid((unsigned)nwg);
+    static const bool naive_env = getenv("PCX_WINO_SLOT") && atoi(getenv("PCX_WINO_SLOT")) == 1;
+    g.naive_slots = naive_env;
     // pooled data gradient with 16-byte source rows
     const bool v4 = (epi == EPI_BWD_POOL || epi == EPI_BWD_POOLSEL) && (a.Ws & 3) == 0 && !(a.H & 1) && !(a.W & 1);
     // 16-byte operand copies where the caller guarantees 4 readable bytes before src (PCX_WINO_X4=0: dword copies)

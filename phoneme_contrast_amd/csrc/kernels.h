@@ -52,7 +52,10 @@ struct ConvArgs {
     const float* ysel;    // EPI_BWD_POOLSEL: y at each 2x2 window's selected element [B][cout][H][W] (pooled res)
     const uint8_t* parg;  // EPI_BWD_POOLSEL: the selected element (0..3, row-major) of each window
     float* dpool;         // EPI_BWD_POOLSELP: the routed gradient at the pooled resolution [B][cout][H][W]
+    int* queue;           // conv_wino: unit queue (WINO_QUEUE_INTS, zero before the first launch; each launch
+                          // leaves it zero), nullptr = static unit order
 };
+constexpr int WINO_QUEUE_INTS = 9 * 32;  // 8 per-XCD unit counters + a completion counter, 128 B apart
 
 size_t conv3x3_nblk(int B, int H, int W, int cout);
 // Raw rows DMA'd into LDS (global_load_lds, double-buffered), the prologue applied at operand-read
@@ -65,6 +68,7 @@ struct WinoGeo {
     int TR, TC, NTS, BPS;  // tile rows / columns per sample, tiles per sample, 64-tile blocks per sample
     int ncg;               // output-channel groups of 32
     float inv_ncg, inv_BPS, inv_TC;  // reciprocals for the kernel's unit decode
+    int naive_slots;                 // analysis: blockIdx order instead of the XCD-contiguous one (PCX_WINO_SLOT=1)
 };
 bool wino_geometry(int B, int H, int W, int cin, int cout, WinoGeo* g);
 size_t wino_nblk(int B, int H, int W, int cin, int cout);

@@ -114,6 +114,9 @@ int build_small(Plan& p) {
     p.P6 = H5 * W5;
     stat = std::max(stat, (size_t)2 * p.C6 * B);
     p.stat_part = p.carve("stat_part", stat * 4);
+    // the Winograd convs take their units from a per-XCD queue (PCX_NO_WINO_QUEUE=1: static order)
+    p.wq = getenv("PCX_NO_WINO_QUEUE") && atoi(getenv("PCX_NO_WINO_QUEUE")) ? 0
+                                                                           : p.carve("wino_queue", WINO_QUEUE_INTS * 4);
     {
         size_t dymax = 0;
         for (int l = 2; l <= 6; ++l) dymax = std::max(dymax, (size_t)B * p.L[l].cout * p.L[l].H * p.L[l].W);
@@ -152,6 +155,7 @@ int small_forward(const Plan& p, const float* const* P, float* const* bnstat, in
                   const float* x, const float* const* drop, int train, float* emb, void* ws,
                   hipStream_t s) {
     const int B = p.B;
+    if (p.wq) RC(hip_status_ok(hipMemsetAsync(at<int>(ws, p.wq), 0, WINO_QUEUE_INTS * 4, s), "memset queue"));
     const float mom = 0.1f, eps = 1e-5f;
     const float* dmask[3] = {nullptr, nullptr, nullptr};
     if (train && drop)
@@ -214,6 +218,7 @@ int small_forward(const Plan& p, const float* const* P, float* const* bnstat, in
         c.partn = part + (size_t)2 * L.cout * L.nblk;
         c.nblk = L.wino ? L.nblk : (int)conv3x3_nblk(B, L.H, L.W, L.cout);
         c.src_guard = 1;  // workspace tensors (and the input never reaches a 3x3 conv)
+        c.queue = p.wq ? at<int>(ws, p.wq) : nullptr;
         int pro = PRO_BNRELU;
         if (L.pooled_in) {  // block tail materialised once; the conv and its wgrad read it raw
             Scope sc(&p.prof, s, "bn_relu_pool", l);
@@ -272,6 +277,7 @@ int small_forward(const Plan& p, const float* const* P, float* const* bnstat, in
 int small_backward(const Plan& p, const float* const* P, const float* x, const float* const* drop,
                    const float* emb, const float* demb, float* const* G, void* ws, hipStream_t s) {
     const int B = p.B;
+    if (p.wq) RC(hip_status_ok(hipMemsetAsync(at<int>(ws, p.wq), 0, WINO_QUEUE_INTS * 4, s), "memset queue"));
     const float* dmask[3] = {nullptr, nullptr, nullptr};
     if (drop)
         for (int i = 0; i < 3; ++i) dmask[i] = drop[i];
@@ -446,6 +452,7 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
             c.cf_in = at<float4>(ws, L.cfb);
             c.src = at<float>(ws, p.dyb);  // dy = BN backward of (dz, y), materialised by the weight gradient
             c.src_guard = 1;
+            c.queue = p.wq ? at<int>(ws, p.wq) : nullptr;
             c.srcH = L.H; c.srcW = L.W;
             c.wpack = at<float>(ws, L.wud);
             c.out = dzp;

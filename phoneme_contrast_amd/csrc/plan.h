@@ -152,6 +152,7 @@ struct Plan {
     int conv1_nblk, conv1_rows;
     int wg1_nslice, wg1_rows;
     size_t stat_part, stat_bytes;   // shared scratch for BN partials
+    size_t wq;                      // conv_wino unit queue (0: static unit order); zeroed by each pass
     size_t dyb;                     // dy of the layer being back-propagated (DMA path)
     size_t wg_part, wg_bytes;       // shared scratch for weight-gradient partials
     size_t proj_part;

@@ -32,11 +32,16 @@ CASES = [  # H, W, cin, cout, B, reps, epilogue, prologue
 ]
 
 
+@pytest.mark.parametrize("queue", [0, 1])
 @pytest.mark.parametrize("case", CASES)
-def test_winograd_epilogues_match_direct_engine(case):
+def test_winograd_epilogues_match_direct_engine(case, queue):
+    """queue = 1: units taken from the per-XCD work queue (ConvArgs::queue); wino_bench launches the
+    kernel several times on one queue, checks the last launch's output and that the queue is left zero."""
     assert os.path.exists(BENCH), "tools/wino_bench missing: run make"
-    r = subprocess.run([BENCH] + [str(v) for v in case], capture_output=True, text=True, timeout=120)
+    env = dict(os.environ, WINO_QUEUE=str(queue))
+    r = subprocess.run([BENCH] + [str(v) for v in case], capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0, (case, r.stdout, r.stderr)
+    assert ("(queue)" in r.stdout) == bool(queue), r.stdout
 
 
 WB = os.path.join(ROOT, "tools", "wb_bench")

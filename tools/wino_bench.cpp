@@ -61,6 +61,12 @@ int main(int argc, char** argv) {
     d.wpack = wp; d.out = o1; d.nblk = (int)nbd; d.part0 = part; d.part1 = part + cout * nbd; d.partn = part + 2 * cout * nbd;
     q.wpack = wu; q.out = o2; q.nblk = (int)nbw; q.part0 = part + (2 * cout * nbm + nbm); q.src_guard = 1;
     q.part1 = q.part0 + cout * nbw; q.partn = q.part0 + 2 * cout * nbw;
+    int* queue = nullptr;  // WINO_QUEUE=1: the Winograd conv takes its units from a work queue
+    if (getenv("WINO_QUEUE") && atoi(getenv("WINO_QUEUE"))) {
+        (void)hipMalloc(&queue, pcx::WINO_QUEUE_INTS * 4);
+        (void)hipMemset(queue, 0, pcx::WINO_QUEUE_INTS * 4);
+        q.queue = queue;
+    }
     int qepi = epi;
     if (sel) {  // the forward's pool records each window's selected y and its index
         float *xp, *ys;
@@ -79,6 +85,13 @@ int main(int argc, char** argv) {
     (void)hipMemset(o1, 0, ny * 4); (void)hipMemset(o2, 0, ny * 4);
     pcx::launch_conv3x3_dma(pro, epi, d, 0); pcx::launch_conv3x3_wino(pro, qepi, q, 0);
     (void)hipDeviceSynchronize();
+    if (queue) {  // every launch must leave the queue zero
+        std::vector<int> hq(pcx::WINO_QUEUE_INTS);
+        (void)hipMemcpy(hq.data(), queue, hq.size() * 4, hipMemcpyDeviceToHost);
+        for (int v : hq)
+            if (v) { printf("queue left non-zero\n"); return 3; }
+        printf("(queue) ");
+    }
     std::vector<float> h1(ny), h2(ny);
     (void)hipMemcpy(h1.data(), o1, ny * 4, hipMemcpyDeviceToHost); (void)hipMemcpy(h2.data(), o2, ny * 4, hipMemcpyDeviceToHost);
     double emax = 0, gmax = 0;
