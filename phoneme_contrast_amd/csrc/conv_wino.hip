@@ -500,9 +500,10 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
 // sources of the granules straddle the image's left / right edges, and the out-of-image columns they
 // bring in (the neighbouring rows' values) are zeroed by selects in the border waves, for every prologue.
 // Needs 4 readable bytes before a.src (ConvArgs::src_guard: the plans carve a guard at the workspace start).
-template <int PRO, int EPI, int CK, bool V4, bool X4>
+template <int PRO, int EPI, int CK, bool V4, bool X4, bool SP = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv_wino_kernel(ConvArgs a, WinoGeo g) {
     static_assert(!X4 || CK == 8, "16-byte staging covers whole 8-channel chunks");
+    static_assert(!SP || X4, "spanning units stage by 16-byte copies");
     constexpr int WROW = X4 ? 40 : WSW;       // slot row width (floats)
     constexpr int NCP = X4 ? 5 : 3;           // copy offsets per lane
     constexpr int WSLOT = CK * WSP + 32;      // floats of one wave's slot (+ the last plane's overflow)
@@ -521,7 +522,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
             cft[2 * c] = f.x;
             cft[2 * c + 1] = f.y;
         }
-    const int nunits = a.B * g.BPS * g.ncg;
+    const int nunits = (SP ? g.nblk : a.B * g.BPS) * g.ncg;
     const int G = gridDim.x;
     // XCD-contiguous slot of this workgroup inside a round (dispatch is round-robin over the 8 XCDs)
     const int slot = ((G & 7) || g.naive_slots) ? (int)blockIdx.x : (int)(blockIdx.x & 7) * (G >> 3) + (int)(blockIdx.x >> 3);
@@ -549,11 +550,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
         Unit x;
         x.tb = wdiv(u, g.ncg, g.inv_ncg);
         x.cg = u - x.tb * g.ncg;
-        x.b = wdiv(x.tb, g.BPS, g.inv_BPS);
-        x.tw = (x.tb - x.b * g.BPS) * 64 + wave * 16;  // the wave's first tile (within its sample)
-        x.tr_a = wdiv(x.tw, g.TC, g.inv_TC);
-        x.tc_a = x.tw - x.tr_a * g.TC;
+        if constexpr (SP) {  // tw = the wave's first tile in the batch-wide tile order
+            x.tw = x.tb * 64 + wave * 16;
+            x.b = wdiv(x.tw, g.NTS, g.inv_NTS);
+            const int rem = x.tw - x.b * g.NTS;
+            x.tr_a = wdiv(rem, g.TC, g.inv_TC);
+            x.tc_a = rem - x.tr_a * g.TC;
+        } else {
+            x.b = wdiv(x.tb, g.BPS, g.inv_BPS);
+            x.tw = (x.tb - x.b * g.BPS) * 64 + wave * 16;  // the wave's first tile (within its sample)
+            x.tr_a = wdiv(x.tw, g.TC, g.inv_TC);
+            x.tc_a = x.tw - x.tr_a * g.TC;
+        }
         return x;
+    };
+    // SP: the wave's 16 tiles as up to 4 row segments (rows of one or more samples) placed side by side
+    // in the slot row, each on its own 16-byte granule: segment s = tiles st[s] .. st[s] + len[s] - 1 of
+    // the wave, image row pair tr[s] of sample b[s], slot column p[s]; rows past the batch get len 0
+    struct Segs { int st[4], len[4], p[4], b[4], tr[4]; };
+    auto segs_of = [&](const Unit& x) {
+        Segs S;
+        int j = 0, pc = 0, b = x.b, tr = x.tr_a, tc = x.tc_a;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int len = min(16 - j, g.TC - tc);
+            const int lv = b < a.B ? len : 0;
+            S.st[q] = j; S.len[q] = lv; S.p[q] = pc; S.b[q] = b; S.tr[q] = tr;
+            pc += lv > 0 ? ((2 * lv + 2 + 3) & ~3) : 0;
+            j += len;
+            tc = 0;
+            if (++tr == g.TR) { tr = 0; ++b; }
+        }
+        return S;
     };
     // Copies: per channel plane three 64-lane dword copies cover slot positions 0..191: 0..143 are
     // the 4 rows x WSW columns, 144..191 (out-of-range offsets: zeros) run into the next plane's
@@ -563,6 +591,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     // an out-of-range offset, which copies a 0.  (No exec masking next to in-flight MFMAs.)
     unsigned voff[NCP];
     auto plan_copies = [&](const Unit& x) {
+        if constexpr (SP) {
+            // granule gi = 64 j + lane: plane gi / 40, row (gi % 40) / 10, slot column 4 (gi % 10) -> segment by
+            // slot column; offsets relative to a.src + (b cin + c0) HW - 1 (b = the unit's first sample)
+            const Segs S = segs_of(x);
+#pragma unroll
+            for (int j = 0; j < NCP; ++j) {
+                const int gi = 64 * j + lane, pl = gi / 40, gg = gi - pl * 40, r = gg / 10, sc = 4 * (gg - r * 10);
+                int q = 0;
+#pragma unroll
+                for (int t = 1; t < 4; ++t) q += (S.len[t] > 0 && sc >= S.p[t]) ? 1 : 0;
+                int len = S.len[0], p0 = S.p[0], bq = S.b[0], trq = S.tr[0];
+#pragma unroll
+                for (int t = 1; t < 4; ++t)
+                    if (q == t) { len = S.len[t]; p0 = S.p[t]; bq = S.b[t]; trq = S.tr[t]; }
+                const int cs = sc - p0, grow = 2 * trq - 1 + r, gcol = (q == 0 ? 2 * x.tc_a - 1 : -1) + cs;
+                const bool ok = len > 0 && cs < 2 * len + 2 && (unsigned)grow < (unsigned)a.H;
+                voff[j] = ok ? 4u * (unsigned)((bq - x.b) * a.cin * HW + pl * HW + grow * a.W + gcol + 1) : 0x80000000u;
+            }
+            return;
+        }
         const int len_a = min(16, g.TC - x.tc_a);
         const int segw = 2 * len_a + 2;
         const int rb0 = 2 * x.tr_a - 1, rb1 = 2 * x.tr_a + 1;
@@ -601,7 +649,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
         const float* sb = a.src + ((int64_t)x.b * a.cin + c0) * HW;
         const unsigned sl = lds0 + 4u * (unsigned)(buf * BUFF + wave * WSLOT);
         if constexpr (X4) {  // 5 granule copies per chunk: parts of 3 + 2
-            const __amdgpu_buffer_rsrc_t r = wrsrc(sb - 1, 4 * (CK * HW + 1));
+            // (SP: the following samples' planes too, up to the end of the batch)
+            // (a wave past the batch has every offset out of range: num_records 1 keeps them so)
+            int nrec = CK * HW + 1;
+            if constexpr (SP) {
+                const int64_t rest = (int64_t)(a.B - x.b) * a.cin * HW - (int64_t)c0 * HW + 1;
+                nrec = rest < 1 ? 1 : rest > 0x1ffffff0 ? 0x1ffffff0 : (int)rest;
+            }
+            const __amdgpu_buffer_rsrc_t r = wrsrc(sb - 1, 4 * nrec);
             const int j0 = part == 0 ? 0 : 3, j1 = np == 1 ? NCP : (part == 0 ? 3 : NCP);
 #pragma unroll
             for (int j = 0; j < NCP; ++j)
@@ -648,13 +703,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
         if (a.queue && tid == 0) qv = grab();
         Unit nxt = unit_of(un < nunits ? un : u);
         // this lane's tile of the current unit
-        const int len_a = min(16, g.TC - cur.tc_a);
-        const bool seg1 = n >= len_a;
-        const int tr = seg1 ? cur.tr_a + 1 : cur.tr_a, tc = seg1 ? n - len_a : cur.tc_a + n;
-        const bool tvalid = cur.tw + n < g.NTS;
-        // (X4: segment B starts at the granule after segment A's segw columns)
-        const int bshift = X4 ? (((2 * len_a + 2 + 3) & ~3) - (2 * len_a + 2)) : 0;
-        const int pbase = wave * WSLOT + kq * WSP + (seg1 ? 2 * n + 2 + bshift : 2 * n);
+        int tr, tc, pbase, lb = cur.b;
+        bool tvalid;
+        if constexpr (SP) {
+            const Segs S = segs_of(cur);
+            int q = 0;
+#pragma unroll
+            for (int t = 1; t < 4; ++t) q += (S.len[t] > 0 && n >= S.st[t]) ? 1 : 0;
+            int st = S.st[0], p0 = S.p[0], bq = S.b[0], trq = S.tr[0];
+#pragma unroll
+            for (int t = 1; t < 4; ++t)
+                if (q == t) { st = S.st[t]; p0 = S.p[t]; bq = S.b[t]; trq = S.tr[t]; }
+            tr = trq;
+            tc = (q == 0 ? cur.tc_a : 0) + n - st;
+            lb = bq;
+            tvalid = cur.tw + n < g.NTOT;
+            pbase = wave * WSLOT + kq * WSP + p0 + 2 * (n - st);
+        } else {
+            const int len_a = min(16, g.TC - cur.tc_a);
+            const bool seg1 = n >= len_a;
+            tr = seg1 ? cur.tr_a + 1 : cur.tr_a;
+            tc = seg1 ? n - len_a : cur.tc_a + n;
+            tvalid = cur.tw + n < g.NTS;
+            // (X4: segment B starts at the granule after segment A's segw columns)
+            const int bshift = X4 ? (((2 * len_a + 2 + 3) & ~3) - (2 * len_a + 2)) : 0;
+            pbase = wave * WSLOT + kq * WSP + (seg1 ? 2 * n + 2 + bshift : 2 * n);
+        }
         // BN+ReLU operands: out-of-image patch rows / columns must be 0 after the prologue (the copy
         // wrote raw 0s there); a factor per patch row / column, applied only in waves that touch the
         // image border
@@ -830,7 +904,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
             if (t == 1234.5f) a.out[tid] = t;
         }
 #else
-        wino_epilogue<EPI, V4>(a, y, red, cur.b, cur.tb, cur.cg * 32, tr, tc, tvalid, wave, tid);
+        wino_epilogue<EPI, V4>(a, y, red, lb, cur.tb, cur.cg * 32, tr, tc, tvalid, wave, tid);
 #endif
         u = un;
         cur = nxt;
@@ -881,8 +955,7 @@ __global__ void wino_pack_kernel(const float* __restrict__ w, float* __restrict_
 // ====================================================================== host side
 static int wino_ck(int cin) { return cin % 8 == 0 ? 8 : 4; }
 
-bool wino_geometry(int B, int H, int W, int cin, int cout, WinoGeo* g) {
-    if (cout % 32 || cin % 4 || H < 1 || W < 31) return false;  // 16 tiles of a wave span <= 2 tile rows
+static WinoGeo wino_base(int B, int H, int W, int cout) {
     WinoGeo r{};
     r.TR = (H + 1) / 2;
     r.TC = (W + 1) / 2;
@@ -892,6 +965,16 @@ bool wino_geometry(int B, int H, int W, int cin, int cout, WinoGeo* g) {
     r.inv_ncg = 1.f / r.ncg;
     r.inv_BPS = 1.f / r.BPS;
     r.inv_TC = 1.f / r.TC;
+    r.inv_NTS = 1.f / r.NTS;
+    r.inv_TR = 1.f / r.TR;
+    r.NTOT = B * r.NTS;
+    r.nblk = B * r.BPS;
+    return r;
+}
+
+bool wino_geometry(int B, int H, int W, int cin, int cout, WinoGeo* g) {
+    if (cout % 32 || cin % 4 || H < 1 || W < 31) return false;  // 16 tiles of a wave span <= 2 tile rows
+    const WinoGeo r = wino_base(B, H, W, cout);
     if ((int64_t)B * r.BPS * r.ncg >= ((int64_t)1 << 22)) return false;  // unit indices (float division)
     if ((int64_t)cin * H * W >= ((int64_t)1 << 30)) return false;
     if ((int64_t)wino_ck(cin) * H * W + 4 * W + 64 >= ((int64_t)1 << 24)) return false;  // packed copy offsets
@@ -899,10 +982,35 @@ bool wino_geometry(int B, int H, int W, int cin, int cout, WinoGeo* g) {
     return true;
 }
 
+bool wino_span_geometry(int B, int H, int W, int cin, int cout, WinoGeo* g) {
+    if (cout % 32 || cin % 8 || H < 1 || W < 1 || W >= 31 || B < 1) return false;
+    WinoGeo r = wino_base(B, H, W, cout);
+    r.span = 1;
+    if ((int64_t)B * r.NTS >= ((int64_t)1 << 22)) return false;  // batch-wide tile indices (float division)
+    r.nblk = (int)ceil_div((int64_t)B * r.NTS, 64);
+    if ((int64_t)r.nblk * r.ncg >= ((int64_t)1 << 22)) return false;
+    if ((int64_t)4 * (4 * (int64_t)cin * H * W + 8 * H * W + 64) >= ((int64_t)1 << 30)) return false;  // copy offsets
+    // every window of 16 consecutive tiles (it starts at any column of a row) must fit the slot row:
+    // at most 4 row segments, each 2 len + 2 columns rounded up to a 16-byte granule, 40 columns in all
+    for (int c0 = 0; c0 < r.TC; ++c0) {
+        int j = 0, tc = c0, pc = 0, ns = 0;
+        while (j < 16) {
+            const int len = std::min(16 - j, r.TC - tc);
+            pc += (2 * len + 2 + 3) & ~3;
+            j += len;
+            tc = 0;
+            ++ns;
+        }
+        if (ns > 4 || pc > 40) return false;
+    }
+    if (g) *g = r;
+    return true;
+}
+
 size_t wino_nblk(int B, int H, int W, int cin, int cout) {
     WinoGeo g;
-    if (!wino_geometry(B, H, W, cin, cout, &g)) return 0;
-    return (size_t)B * g.BPS;
+    if (wino_geometry(B, H, W, cin, cout, &g) || wino_span_geometry(B, H, W, cin, cout, &g)) return (size_t)g.nblk;
+    return 0;
 }
 
 int launch_wino_pack(const float* w, float* u, int M, int K, int flip, hipStream_t s) {
@@ -915,10 +1023,12 @@ int launch_wino_pack(const float* w, float* u, int M, int K, int flip, hipStream
 
 int launch_conv3x3_wino(int pro, int epi, ConvArgs a, hipStream_t s) {
     WinoGeo g;
-    PCX_CHECK_ARG(wino_geometry(a.B, a.H, a.W, a.cin, a.cout, &g),
+    const bool sp = !wino_geometry(a.B, a.H, a.W, a.cin, a.cout, &g);
+    PCX_CHECK_ARG(!sp || wino_span_geometry(a.B, a.H, a.W, a.cin, a.cout, &g),
                   "conv3x3_wino: unsupported shape (B %d, %dx%d, cin %d, cout %d)", a.B, a.H, a.W, a.cin, a.cout);
-    PCX_CHECK_ARG(a.nblk == a.B * g.BPS, "conv3x3_wino: partial buffer sized for %d tiles, need %d", a.nblk,
-                  a.B * g.BPS);
+    PCX_CHECK_ARG(!sp || (pro == PRO_RAW && (epi == EPI_FWD || epi == EPI_BWD_STORE) && a.src_guard),
+                  "conv3x3_wino: %dx%d images need PRO_RAW, EPI_FWD / EPI_BWD_STORE and src_guard", a.H, a.W);
+    PCX_CHECK_ARG(a.nblk == g.nblk, "conv3x3_wino: partial buffer sized for %d tiles, need %d", a.nblk, g.nblk);
     PCX_CHECK_ARG(pro == PRO_RAW || pro == PRO_BNRELU, "conv3x3_wino: prologue %d", pro);
     if (epi == EPI_BWD_POOL || epi == EPI_BWD_POOLSEL)
         PCX_CHECK_ARG(a.Hs >= 2 * a.H && a.Ws >= 2 * a.W, "conv3x3_wino: pooled source %dx%d for %dx%d", a.Hs, a.Ws,
@@ -931,7 +1041,7 @@ int launch_conv3x3_wino(int pro, int epi, ConvArgs a, hipStream_t s) {
     const size_t smem = (2 * buff + 2 * (size_t)a.cin + 512 + 4) * 4;  // + the queue's 2 ints
     PCX_CHECK_ARG(smem <= 160 * 1024, "conv3x3_wino: %zu B of LDS", smem);
     // persistent workgroups: two per CU (a multiple of 8, one XCD-contiguous run of units each round)
-    const int64_t units = (int64_t)a.B * g.BPS * g.ncg;
+    const int64_t units = (int64_t)g.nblk * g.ncg;
     int64_t nwg = std::min<int64_t>(units, 2 * (int64_t)num_cus());
     if (nwg >= 8) nwg &= ~(int64_t)7;
     dim3 grid((unsigned)nwg);
@@ -953,6 +1063,19 @@ int launch_conv3x3_wino(int pro, int epi, ConvArgs a, hipStream_t s) {
         conv_wino_kernel<P_, E_, CK_, V4_, X4_><<<grid, 256, smem, s>>>(a, g);                          \
         PCX_LAUNCH_CHECK("conv_wino_kernel");                                                           \
         return PCX_OK;                                                                                  \
+    }
+    if (sp) {
+        if (epi == EPI_FWD) {
+            (void)hipFuncSetAttribute((const void*)conv_wino_kernel<PRO_RAW, EPI_FWD, 8, false, true, true>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+            conv_wino_kernel<PRO_RAW, EPI_FWD, 8, false, true, true><<<grid, 256, smem, s>>>(a, g);
+        } else {
+            (void)hipFuncSetAttribute((const void*)conv_wino_kernel<PRO_RAW, EPI_BWD_STORE, 8, false, true, true>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+            conv_wino_kernel<PRO_RAW, EPI_BWD_STORE, 8, false, true, true><<<grid, 256, smem, s>>>(a, g);
+        }
+        PCX_LAUNCH_CHECK("conv_wino_kernel (spanning units)");
+        return PCX_OK;
     }
 #define PCX_WINO_CK(P_, E_, V4_) PCX_WINO_CASE(P_, E_, 8, V4_, false) PCX_WINO_CASE(P_, E_, 4, V4_, false) \
     PCX_WINO_CASE(P_, E_, 8, V4_, true)

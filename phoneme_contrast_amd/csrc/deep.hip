@@ -40,6 +40,13 @@ struct DeepBlock {
     size_t m8;                     // channel-last next block: the output's ReLU mask as bytes (no float32 out)
 };
 
+// narrow stride-1 images (5 x 25, 3 x 13) on the Winograd conv with batch-spanning units
+// (PCX_NO_WINO_SPAN=1: the direct LDS-DMA conv)
+static bool wino_span_ok() {
+    static const bool off = getenv("PCX_NO_WINO_SPAN") && atoi(getenv("PCX_NO_WINO_SPAN"));
+    return !off;
+}
+
 struct DeepPlan {
     bool residual;
     bool bf16;                     // every conv on convg_bf16 (bf16 operands, float32 accumulation)
@@ -136,7 +143,8 @@ int build_deep(Plan& p) {
         *w32 = *ww || (route && (w >= 50 ? wgrad_s_geometry(B, h, w, ci, co, wga) : wgrad_w32_geometry(B, h, w, ci, co, wga)));
         *nblk = 0;
         if (*fwd) {
-            // the Winograd conv takes the layers whose rows are >= 31 columns wide (its own tile blocks)
+            // the Winograd conv takes the layers whose rows are >= 31 columns wide (its own tile blocks) and
+            // the narrow ones it can span (5 x 25 / 3 x 13: units over rows and samples)
             *nblk = (int)std::max({conv3x3_nblk(B, h, w, co), conv3x3_nblk(B, h, w, ci), wino_nblk(B, h, w, ci, co),
                                    wino_nblk(B, h, w, co, ci)});
             stat = std::max(stat, (size_t)2 * std::max(ci, co) * (*nblk) + *nblk);
@@ -213,6 +221,9 @@ int build_deep(Plan& p) {
     stat = std::max(stat, (size_t)2 * C4 * B);
     if (d.stem_fused) stat = std::max(stat, (size_t)2 * C0 * B);  // stem_pool_bwd partials [C0][B] x 2
     d.stat = p.carve("stat_part", stat * 4);
+    // stride-1 Winograd convs take their units from a per-XCD queue (PCX_NO_WINO_QUEUE=1: static order)
+    p.wq = getenv("PCX_NO_WINO_QUEUE") && atoi(getenv("PCX_NO_WINO_QUEUE")) ? 0
+                                                                           : p.carve("wino_queue", WINO_QUEUE_INTS * 4);
     d.wgp = p.carve("wg_part", wg * 4);
     d.ident = p.carve("ident", (size_t)C4 * 16);
     d.identw = p.carve("identw", (size_t)cmax * 16);
@@ -293,7 +304,8 @@ int conv_bn_fwd(const Ctx& c, const char* label, int layer, const float* x, int 
     f.C = cout;
     if (dma_nblk) {  // stride-1 3x3 on the LDS-DMA conv: its epilogue writes the BN partials
         float* wp = c.w<float>(c.d.wpk);
-        const bool wino = wino_geometry(c.p.B, OH, OW, cin, cout, nullptr);
+        const bool wino = wino_geometry(c.p.B, OH, OW, cin, cout, nullptr) ||
+                          (wino_span_ok() && wino_span_geometry(c.p.B, OH, OW, cin, cout, nullptr));
         if (wino) RC(launch_wino_pack(wgt, wp, cout, cin, 0, c.s));
         else RC(launch_pack_fwd(wgt, wp, cout, cin, c.s));
         ConvArgs a{};
@@ -301,6 +313,7 @@ int conv_bn_fwd(const Ctx& c, const char* label, int layer, const float* x, int 
         a.src = x;
         a.src_guard = 1;  // workspace tensor
         a.srcH = IH; a.srcW = IW;
+        a.queue = c.p.wq ? c.w<int>(c.p.wq) : nullptr;
         a.wpack = wp;
         a.out = y;
         a.nblk = wino ? (int)wino_nblk(c.p.B, OH, OW, cin, cout) : (int)conv3x3_nblk(c.p.B, OH, OW, cout);
@@ -429,7 +442,8 @@ int conv_dgrad(const Ctx& c, int layer, const float* dy, int cout, int OH, int O
                const void* dyn = nullptr, float* par_out = nullptr, const ConvGArgs* ep = nullptr) {
     if (dma) {  // stride-1 3x3: the LDS-DMA conv on flipped weights, plain store / accumulate
         float* wp = c.w<float>(c.d.wpk);
-        const bool wino = wino_geometry(c.p.B, IH, IW, cout, cin, nullptr);
+        const bool wino = wino_geometry(c.p.B, IH, IW, cout, cin, nullptr) ||
+                          (wino_span_ok() && wino_span_geometry(c.p.B, IH, IW, cout, cin, nullptr));
         if (wino) RC(launch_wino_pack(wgt, wp, cin, cout, 1, c.s));
         else RC(launch_pack_dgrad(wgt, wp, cout, cin, c.s));
         ConvArgs a{};
@@ -437,6 +451,7 @@ int conv_dgrad(const Ctx& c, int layer, const float* dy, int cout, int OH, int O
         a.src = dy;
         a.src_guard = 1;  // workspace tensor
         a.srcH = OH; a.srcW = OW;
+        a.queue = c.p.wq ? c.w<int>(c.p.wq) : nullptr;
         a.wpack = wp;
         a.out = dx;
         a.accumulate = accumulate;
@@ -480,6 +495,7 @@ int deep_forward(const Plan& p, const float* const* P, float* const* bnstat, int
                  const float* const* drop, int train, float* emb, void* ws, hipStream_t s) {
     const DeepPlan& d = *p.deep;
     const Ctx c{p, d, ws, s};
+    if (p.wq) RC(hip_status_ok(hipMemsetAsync(c.w<int>(p.wq), 0, WINO_QUEUE_INTS * 4, s), "memset queue"));
     const int B = p.B;
     const float* dmask[4] = {nullptr, nullptr, nullptr, nullptr};
     if (train && drop)
@@ -638,6 +654,7 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
                   const float* demb, float* const* G, void* ws, hipStream_t s) {
     const DeepPlan& d = *p.deep;
     const Ctx c{p, d, ws, s};
+    if (p.wq) RC(hip_status_ok(hipMemsetAsync(c.w<int>(p.wq), 0, WINO_QUEUE_INTS * 4, s), "memset queue"));
     const int B = p.B;
     const float* dmask[4] = {nullptr, nullptr, nullptr, nullptr};
     if (drop)

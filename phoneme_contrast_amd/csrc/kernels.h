@@ -69,8 +69,15 @@ struct WinoGeo {
     int ncg;               // output-channel groups of 32
     float inv_ncg, inv_BPS, inv_TC;  // reciprocals for the kernel's unit decode
     int naive_slots;                 // analysis: blockIdx order instead of the XCD-contiguous one (PCX_WINO_SLOT=1)
+    int span;                        // units of 64 consecutive tiles of the whole batch (narrow images)
+    int NTOT, nblk;                  // B * NTS; 64-tile blocks (BN partials) of the launch
+    float inv_NTS, inv_TR;
 };
 bool wino_geometry(int B, int H, int W, int cin, int cout, WinoGeo* g);
+// Narrow images (W < 31, the 5 x 25 / 3 x 13 blocks of cnn_deep): units span rows and samples (a wave's 16
+// tiles in up to 4 row segments side by side in its slot).  PRO_RAW with EPI_FWD / EPI_BWD_STORE, 16-byte
+// staging only (ConvArgs::src_guard), cin % 8 == 0.
+bool wino_span_geometry(int B, int H, int W, int cin, int cout, WinoGeo* g);
 size_t wino_nblk(int B, int H, int W, int cin, int cout);
 // flip = 0: forward weights w[M][K][3][3]; flip = 1: data gradient of forward weights w[K][M][3][3]
 int launch_wino_pack(const float* w, float* u, int M, int K, int flip, hipStream_t s);

@@ -29,6 +29,15 @@ CASES = [  # H, W, cin, cout, B, reps, epilogue, prologue
     (40, 201, 32, 32, 24, 1, 0, 1),    # T = 201: odd width, scalar stores
     (40, 201, 32, 32, 24, 1, 1, 0),
     (20, 100, 64, 64, 24, 1, 3, 0),    # plain store (cnn_deep's stride-1 data gradients)
+    # narrow images on batch-spanning units (cnn_deep blocks 3 / 4 at T = 200 / 201): a wave's 16 tiles in
+    # up to 4 row segments of several samples; odd batches end inside a unit
+    (5, 25, 256, 256, 24, 1, 0, 0),
+    (5, 25, 256, 256, 23, 1, 3, 0),
+    (3, 13, 512, 512, 16, 1, 0, 0),
+    (3, 13, 512, 512, 17, 1, 3, 0),
+    (5, 26, 64, 128, 9, 1, 0, 0),
+    (4, 14, 32, 64, 5, 1, 3, 0),
+    (1, 30, 32, 32, 3, 1, 0, 0),
 ]
 
 
