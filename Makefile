@@ -8,7 +8,7 @@ OBJ = $(patsubst phoneme_contrast_amd/csrc/%.hip,build/%.o,$(SRC))
 HDR = $(wildcard phoneme_contrast_amd/csrc/*.h) include/pcx.h
 LIB = phoneme_contrast_amd/libpcx.so
 
-TOOLS = tools/wino_bench tools/ww_bench tools/stem_bench tools/wb_bench
+TOOLS = tools/wino_bench tools/ww_bench tools/stem_bench tools/wb_bench tools/ws_bench
 
 all: $(LIB) $(TOOLS)
 
@@ -19,6 +19,11 @@ tools/wino_bench: tools/wino_bench.cpp $(LIB) $(HDR)
 
 # Winograd weight gradient vs the pixel-stream kernel (tests/test_wino_engine_gpu.py runs it)
 tools/ww_bench: tools/ww_bench.cpp $(LIB) $(HDR)
+	$(HIPCC) -O2 -std=c++17 --offload-arch=$(ARCH) -Iinclude $< -Lphoneme_contrast_amd -lpcx \
+	    -Wl,-rpath,'$$ORIGIN/../phoneme_contrast_amd' -o $@
+
+# 32x32 row-window weight gradient (wgrad_w32) vs the pixel-stream kernel (tests/test_wino_engine_gpu.py runs it)
+tools/ws_bench: tools/ws_bench.cpp $(LIB) $(HDR)
 	$(HIPCC) -O2 -std=c++17 --offload-arch=$(ARCH) -Iinclude $< -Lphoneme_contrast_amd -lpcx \
 	    -Wl,-rpath,'$$ORIGIN/../phoneme_contrast_amd' -o $@
 

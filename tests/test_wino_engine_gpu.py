@@ -88,3 +88,22 @@ def test_winograd_wgrad_pooled_dz_matches_pixel_stream(case):
     r = subprocess.run([WW] + [str(v) for v in case], capture_output=True, text=True, timeout=120)
     print(r.stdout)
     assert r.returncode == 0, (case, r.stdout, r.stderr)
+
+
+WS = os.path.join(ROOT, "tools", "ws_bench")
+WS_CASES = [  # H, W, cin, cout, B, reps, prologue: the 32x32 row-window weight gradient (cnn_deep's narrow
+    # blocks) vs the pixel-stream kernel; a slice's tasks stream their rows across task ends
+    (3, 13, 512, 512, 24, 1, 0),
+    (5, 25, 256, 256, 23, 1, 0),
+    (5, 26, 256, 256, 9, 1, 1),
+    (1, 30, 64, 64, 7, 1, 1),
+    (10, 50, 128, 128, 5, 1, 0),
+]
+
+
+@pytest.mark.parametrize("case", WS_CASES)
+def test_row_window_wgrad_matches_pixel_stream(case):
+    assert os.path.exists(WS), "tools/ws_bench missing: run make"
+    r = subprocess.run([WS] + [str(v) for v in case], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, (case, r.stdout, r.stderr)
+    assert " w32: " in r.stdout, r.stdout

@@ -76,5 +76,7 @@ int main(int argc, char** argv) {
     printf("H%d W%d %d->%d pro%d | s: TM %d CW %d V %d R %d slices %d: %.3f ms %.3f roof | old %s: %.3f ms %.3f roof"
            " | dW rel %.2e dy-vs-old %.2e dy-vs-host %.2e\n", H, W, cin, cout, pro, s.NPM, s.CW, s.VX, s.R0, s.ntslice, ms_s, fl / ms_s / 1e9 / 157.3,
            w32 ? "w32" : "s", ms_o, fl / ms_o / 1e9 / 157.3, emax / gmax, dmax, dref);
-    return 0;
+    // exit 3 when the two kernels disagree (dW beyond fp32 summation-order noise, dy beyond rounding:
+    // the two evaluate the BN backward in different orders)
+    return (emax / gmax < 1e-4 && dmax < 1e-5 && nbad == 0) ? 0 : 3;
 }
