@@ -175,6 +175,7 @@ struct WinoBwdArgs {
     int V, NIR, XCS;
     size_t lds;
     int ntask, per_slice, nslice;
+    int paired;            // the two strips of a sample on two blocks of one XCD at the same time
 };
 bool wgbd_wino_geometry(int B, int H, int W, int C, WinoBwdArgs* a);
 int launch_wgbd_wino(WinoBwdArgs a, hipStream_t s);

@@ -186,8 +186,21 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
     auto run = [&](auto role) {
     constexpr bool DG = decltype(role)::value;
     const int t0s = slice * a.per_slice, t1s = min(a.ntask, t0s + a.per_slice);
-    for (int task = t0s; task < t1s; ++task) {
-        const int b = task / a.nseg, seg = task - b * a.nseg;
+    // paired: the two strips of a sample run at the same time on two blocks of one XCD (slice, slice + 8),
+    // so the 128-byte lines around the strip boundary are fetched once into that XCD's L2; each block
+    // alternates strips (48 / 52 tiles), so the pair keeps pace
+    const int pair = (slice >> 4) * 8 + (slice & 7), prole = (slice >> 3) & 1;
+    const int nk = a.paired ? a.per_slice : t1s - t0s;
+    for (int k = 0; k < nk; ++k) {
+        int b, seg;
+        if (a.paired) {
+            b = pair * a.per_slice + k;
+            seg = (k + prole) & 1;
+        } else {
+            const int task = t0s + k;
+            b = task / a.nseg;
+            seg = task - b * a.nseg;
+        }
         const int t0 = a.seg_t0[seg], S = a.seg_S[seg];
         const int c0 = 2 * t0;
         const int ng = (S + 15) >> 4, Ks = S >> 1;
@@ -521,6 +534,9 @@ bool wgbd_wino_geometry(int B, int H, int W, int C, WinoBwdArgs* a) {
         const int want = std::min(num_cus(), a->ntask);  // one block per CU
         a->per_slice = ceil_div(a->ntask, want);
         a->nslice = ceil_div(a->ntask, a->per_slice);
+        // XCD-paired strips (PCX_WGBD_UNPAIRED=1: each block walks its own run of tasks)
+        static const bool unpaired = getenv("PCX_WGBD_UNPAIRED") && atoi(getenv("PCX_WGBD_UNPAIRED"));
+        a->paired = !unpaired && nseg == 2 && a->nslice % 16 == 0 && a->nslice * a->per_slice == a->ntask;
     }
     return true;
 }
@@ -529,7 +545,7 @@ int launch_wgbd_wino(WinoBwdArgs a, hipStream_t s) {
     WinoBwdArgs g{};
     PCX_CHECK_ARG(wgbd_wino_geometry(a.B, a.H, a.W, CH, &g), "wgbd_wino: unsupported shape %dx%d", a.H, a.W);
     PCX_CHECK_ARG(g.XCS == a.XCS && g.nslice == a.nslice && g.per_slice == a.per_slice && g.ntask == a.ntask &&
-                      g.nseg == a.nseg,
+                      g.nseg == a.nseg && g.paired == a.paired,
                   "wgbd_wino: geometry mismatch");
     PCX_CHECK_ARG((a.dz != nullptr) != (a.dzpool != nullptr), "wgbd_wino: exactly one of dz / dzpool");
     PCX_CHECK_ARG(a.y && a.cf_dy && a.yp && a.cf_x && a.up && a.part && a.dzp && a.bn0 && a.bn1,
