@@ -598,6 +598,61 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* g, const
         dy[o + p] = k.x * (g[o + p] - k.y - (y[o + p] - k.w) * k.z);
 }
 
+// Flat forms of the two kernels above for short rows (the 10 x 50 .. 3 x 13 planes of cnn_deep's later
+// blocks): a row per 64-256 threads left most lanes idle and launched one block per 1-4 rows; here
+// each thread takes 4 consecutive elements (one 16-byte access per operand, rows cross freely: the
+// channel of each element follows from one division per quad), 2048 elements per block.
+template <int OP>  // 0: bn_act, 1: bn_bwd_apply
+__global__ __launch_bounds__(256) void bn_flat_kernel(const float* __restrict__ y, const float4* __restrict__ cf,
+                                                      const float* __restrict__ res, const float4* __restrict__ rcf,
+                                                      const float* __restrict__ drop, const float* g,
+                                                      float* out, int64_t n, int C, int P) {
+    for (int64_t q = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; q < n; q += (int64_t)gridDim.x * 1024) {
+        const int64_t row0 = q / P;
+        int p = (int)(q - row0 * P), row = (int)row0, c = row % C;
+        float4 yv, rv = make_float4(0.f, 0.f, 0.f, 0.f), gv = make_float4(0.f, 0.f, 0.f, 0.f);
+        const bool full = q + 4 <= n;
+        if (full) {
+            yv = *reinterpret_cast<const float4*>(y + q);
+            if (OP == 0 && res) rv = *reinterpret_cast<const float4*>(res + q);
+            if (OP == 1) gv = *reinterpret_cast<const float4*>(g + q);
+        } else {
+            float t[4] = {0.f, 0.f, 0.f, 0.f}, r[4] = {0.f, 0.f, 0.f, 0.f}, u[4] = {0.f, 0.f, 0.f, 0.f};
+            for (int j = 0; j < 4 && q + j < n; ++j) {
+                t[j] = y[q + j];
+                if (OP == 0 && res) r[j] = res[q + j];
+                if (OP == 1) u[j] = g[q + j];
+            }
+            yv = make_float4(t[0], t[1], t[2], t[3]);
+            rv = make_float4(r[0], r[1], r[2], r[3]);
+            gv = make_float4(u[0], u[1], u[2], u[3]);
+        }
+        float yy[4] = {yv.x, yv.y, yv.z, yv.w}, rr[4] = {rv.x, rv.y, rv.z, rv.w}, gg[4] = {gv.x, gv.y, gv.z, gv.w};
+        float o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float4 k = cf[c];
+            if (OP == 0) {
+                const float4 rk = rcf ? rcf[c] : make_float4(1.f, 0.f, 0.f, 0.f);
+                const float d = drop ? drop[row] : 1.f;
+                float v = fmaf(yy[j], k.x, k.y);
+                if (res) v += fmaf(rr[j], rk.x, rk.y);
+                o[j] = d * fmaxf(v, 0.f);
+            } else {
+                o[j] = k.x * (gg[j] - k.y - (yy[j] - k.w) * k.z);
+            }
+            if (++p == P) {
+                p = 0;
+                ++row;
+                if (++c == C) c = 0;
+            }
+        }
+        if (full) *reinterpret_cast<float4*>(out + q) = make_float4(o[0], o[1], o[2], o[3]);
+        else
+            for (int j = 0; j < 4 && q + j < n; ++j) out[q + j] = o[j];
+    }
+}
+
 // MaxPool2d(3, stride 2, pad 1) of relu(BN(y))  (reference phoneme_cnn.py:211-216).  One block per
 // channel plane (32-bit index math).  Also records, per window, the tap (kh*3 + kw) of its first
 // maximum in row-major scan order (torch's tie rule), or 255 when that maximum is 0 (the ReLU then
@@ -1020,8 +1075,22 @@ int launch_bwd_prep(BwdPrepArgs a, int* nslice, hipStream_t s) {
     return PCX_OK;
 }
 
+// short rows (flat form; PCX_BN_ROWTILE=1: the row tiles)
+static bool bn_flat(int64_t P, int64_t n, const void* a, const void* b, const void* c) {
+    static const bool off = getenv("PCX_BN_ROWTILE") && atoi(getenv("PCX_BN_ROWTILE"));
+    auto al = [](const void* p) { return p == nullptr || ((uintptr_t)p & 15) == 0; };
+    return !off && P < 1024 && n / P < ((int64_t)1 << 31) && al(a) && al(b) && al(c) && n > 0;
+}
+
 int launch_bn_act(const float* y, const float4* cf, const float* res, const float4* rcf, const float* drop,
                   float* out, int B, int C, int64_t P, hipStream_t s) {
+    const int64_t n = (int64_t)B * C * P;
+    if (bn_flat(P, n, y, res, out)) {
+        const int64_t nb = std::min<int64_t>(ceil_div(n, 2048), (int64_t)1 << 20);
+        bn_flat_kernel<0><<<(unsigned)nb, 256, 0, s>>>(y, cf, res, rcf, drop, nullptr, out, n, C, (int)P);
+        PCX_LAUNCH_CHECK("bn_flat_kernel");
+        return PCX_OK;
+    }
     const int tp = row_threads(P);
     const int64_t rows = (int64_t)B * C;
     bn_act_kernel<<<ceil_div(rows, 256 / tp), 256, 0, s>>>(y, cf, res, rcf, drop, out, rows, C, P, tp);
@@ -1031,6 +1100,13 @@ int launch_bn_act(const float* y, const float4* cf, const float* res, const floa
 
 int launch_bn_bwd_apply(const float* g, const float* y, const float4* cf, float* dy, int B, int C, int64_t P,
                         hipStream_t s) {
+    const int64_t n = (int64_t)B * C * P;
+    if (bn_flat(P, n, g, y, dy)) {
+        const int64_t nb = std::min<int64_t>(ceil_div(n, 2048), (int64_t)1 << 20);
+        bn_flat_kernel<1><<<(unsigned)nb, 256, 0, s>>>(y, cf, nullptr, nullptr, nullptr, g, dy, n, C, (int)P);
+        PCX_LAUNCH_CHECK("bn_flat_kernel");
+        return PCX_OK;
+    }
     const int tp = row_threads(P);
     const int64_t rows = (int64_t)B * C;
     bn_bwd_apply_kernel<<<ceil_div(rows, 256 / tp), 256, 0, s>>>(g, y, cf, dy, rows, C, P, tp);

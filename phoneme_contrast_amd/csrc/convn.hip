@@ -72,18 +72,22 @@ __global__ __launch_bounds__(256) void to_nhwc_kernel(NhwcArgs a) {
         *reinterpret_cast<bf16x8*>(dimg + ((int64_t)r * (Hp - 1) * Wp + wp) * a.C + 8 * g) = bf16x8{};
         if (two) *reinterpret_cast<bf16x8*>(dimg2 + ((int64_t)r * (Hp - 1) * Wp + wp) * a.C + 8 * g) = bf16x8{};
     }
-    // LDS tile [64][TW] with channel c's row at c TW + 4 (c >> 3): TW a multiple of 4 keeps the V-wide
-    // row writes aligned, and the 4 (c >> 3) shift puts the 8 channel rows a row-out read touches (lanes
-    // g = 0..7 of one pixel, 4 pixels per 32 lanes) on 32 different banks
-    const int W = a.W, TW = (W + 3) & ~3, nv = W / V, n = nc * nv;
+    // LDS tile [64][TW] with channel c's run of R image rows at c TW + 4 (c >> 3): TW a multiple of 4
+    // keeps the V-wide writes aligned, and the 4 (c >> 3) shift puts the 8 channel rows a row-out read
+    // touches (lanes g = 0..7 of one pixel, 4 pixels per 32 lanes) on 32 different banks.  R (a.rows,
+    // set by the launcher) image rows per step: narrow images (W = 50, 25, 13) fill a step with the same
+    // number of loads as a 100-wide row (the R rows of a channel are contiguous in NCHW).
+    const int W = a.W, R = a.rows, TW = (R * W + 3) & ~3, nv = W / V;
     float* t2 = t + 64 * TW + 32;  // (two: the second image's tile)
     const int64_t HW = (int64_t)a.H * W;
     const int64_t pbase = ((int64_t)b * a.C + c0) * HW;
     constexpr int U = 4;
     // the block walks its sample's rows: consecutive rows of the same 64 planes (page / line reuse)
-    float* rres = t + (two ? 2 : 1) * (64 * TW + 32);  // res_pool: the row's residual, transposed like t
-    for (int h = 0; h < a.H; ++h) {
-        const int64_t base = pbase + (int64_t)h * W;
+    float* rres = t + (two ? 2 : 1) * (64 * TW + 32);  // res_pool (R = 1): the row's residual, transposed like t
+    for (int h0 = 0; h0 < a.H; h0 += R) {
+        const int h = h0;
+        const int Rr = min(R, a.H - h0), nvr = Rr * nv, n = nc * nvr;
+        const int64_t base = pbase + (int64_t)h0 * W;
         if (OP == NHWC_ACT && a.res_pool) {  // pooled NHWC row (b, h): 16-byte runs of 4 channels, coalesced
             const float* rrow = a.res + ((int64_t)b * a.H + h) * W * a.C + c0;
             const int nq = W * (nc >> 2);
@@ -102,7 +106,7 @@ __global__ __launch_bounds__(256) void to_nhwc_kernel(NhwcArgs a) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {  // (tail items load a valid element and are dropped below)
                 const int i = min(i0 + u * 256 + (int)threadIdx.x, n - 1);
-                const int c = i / nv, w0 = (i - c * nv) * V;
+                const int c = i / nvr, w0 = (i - c * nvr) * V;
                 const int64_t o = base + c * HW + w0;
                 x[u] = *reinterpret_cast<const fv*>(a.src + o);
                 if (OP == NHWC_BNBWD) y2[u] = *reinterpret_cast<const fv*>(a.y + o);
@@ -119,7 +123,7 @@ __global__ __launch_bounds__(256) void to_nhwc_kernel(NhwcArgs a) {
             for (int u = 0; u < U; ++u) {
                 const int i = i0 + u * 256 + (int)threadIdx.x;
                 if (i < n) {
-                    const int c = i / nv, w0 = (i - c * nv) * V;
+                    const int c = i / nvr, w0 = (i - c * nvr) * V;
                     fv v = x[u];
                     if (OP == NHWC_BNBWD) {
                         const float4 k = kc[c];
@@ -164,22 +168,24 @@ __global__ __launch_bounds__(256) void to_nhwc_kernel(NhwcArgs a) {
             }
         }
         __syncthreads();
-        __bf16* drow = dimg + (int64_t)(h + 1) * Wp * a.C;
-        for (int i = threadIdx.x; i < Wp * ng; i += 256) {
-            const int wp = i / ng, g = i - wp * ng;
+        for (int i = threadIdx.x; i < Rr * Wp * ng; i += 256) {
+            const int hr = i / (Wp * ng), i2 = i - hr * (Wp * ng);
+            const int wp = i2 / ng, g = i2 - wp * ng;
+            const int px = hr * W + wp - 1;  // the pixel within the step's rows
             bf16x8 o{};
             if (wp > 0 && wp <= W) {
 #pragma unroll
-                for (int j = 0; j < 8; ++j) o[j] = (__bf16)t[(8 * g + j) * TW + 4 * g + wp - 1];
+                for (int j = 0; j < 8; ++j) o[j] = (__bf16)t[(8 * g + j) * TW + 4 * g + px];
             }
-            *reinterpret_cast<bf16x8*>(drow + (int64_t)wp * a.C + 8 * g) = o;
+            const int64_t ro = ((int64_t)(h0 + hr + 1) * Wp + wp) * a.C + 8 * g;
+            *reinterpret_cast<bf16x8*>(dimg + ro) = o;
             if (two) {
                 bf16x8 o2{};
                 if (wp > 0 && wp <= W) {
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) o2[j] = (__bf16)t2[(8 * g + j) * TW + 4 * g + wp - 1];
+                    for (int j = 0; j < 8; ++j) o2[j] = (__bf16)t2[(8 * g + j) * TW + 4 * g + px];
                 }
-                *reinterpret_cast<bf16x8*>(dimg2 + (int64_t)(h + 1) * Wp * a.C + (int64_t)wp * a.C + 8 * g) = o2;
+                *reinterpret_cast<bf16x8*>(dimg2 + ro) = o2;
             }
         }
     }
@@ -676,7 +682,11 @@ int launch_to_nhwc(NhwcArgs a, hipStream_t s) {
     PCX_CHECK_ARG(a.op != NHWC_ACT || a.cf, "to_nhwc: activation needs cf");
     PCX_CHECK_ARG(!a.res_pool || (a.op == NHWC_ACT && a.res && a.rcf), "to_nhwc: pooled residual needs res and rcf");
     PCX_CHECK_ARG(!a.dst_b || (a.op == NHWC_BNBWD && a.y_b && a.cf_b), "to_nhwc: second image needs y_b and cf_b");
-    const size_t sm = ((size_t)64 * ((a.W + 3) & ~3) + 32) * 4 * (a.dst_b || a.res_pool ? 2 : 1);
+    // image rows per step: up to 128 floats of a channel (narrow images: fewer, fuller steps); one row
+    // with the pooled residual (staged per row)
+    static const bool one_row = getenv("PCX_NHWC_ROWS1") && atoi(getenv("PCX_NHWC_ROWS1"));  // A/B: a row per step
+    a.rows = a.res_pool || one_row ? 1 : std::max(1, std::min(a.H, (a.dst_b ? 124 : 128) / a.W));
+    const size_t sm = ((size_t)64 * ((a.rows * a.W + 3) & ~3) + 32) * 4 * (a.dst_b || a.res_pool ? 2 : 1);
     PCX_CHECK_ARG(!a.res_pool || a.C % 4 == 0, "to_nhwc: pooled residual needs C %% 4 == 0");
     PCX_CHECK_ARG(sm <= 64 * 1024, "to_nhwc: row of %d pixels too long", a.W);
     dim3 grid((unsigned)a.B, (unsigned)ceil_div(a.C, 64));

@@ -421,6 +421,7 @@ struct NhwcArgs {
     const float* y_b;
     const float4* cf_b;
     void* dst_b;
+    int rows;              // (set by launch_to_nhwc) image rows per step
 };
 size_t nhwc_bytes(int B, int C, int H, int W);
 int launch_to_nhwc(NhwcArgs a, hipStream_t s);
