@@ -971,6 +971,10 @@ int launch_convg(ConvGArgs a, hipStream_t s) {
                   "convg: class-planar output only for the stride-2 data gradient (fp32 or channel-last)");
     if (a.mode == 1 && a.stride == 2) {
         for (int par = 0; par < 4; ++par) {  // each parity class of dx written exactly once
+            // a class no tap reaches (1x1 stride-2 shortcut: classes 1..3) adds nothing: skipped when
+            // accumulating (it used to re-read and re-write those class planes unchanged)
+            const int kh0 = ((par >> 1) + a.pad) & 1, kw0 = ((par & 1) + a.pad) & 1;
+            if (a.accumulate && ((a.KH - kh0 + 1) / 2) * ((a.KW - kw0 + 1) / 2) == 0) continue;
             ConvGArgs c = a;
             c.mode = 3;
             c.par = par;
