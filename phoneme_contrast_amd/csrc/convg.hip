@@ -1050,7 +1050,11 @@ int launch_convg(ConvGArgs a, hipStream_t s) {
 }
 
 int chan_slices(int B, int C, int* bps) {
-    int want = std::max(1, std::min(B, 2048 / std::max(C, 1)));
+    // ~16384 blocks per launch: each block's run of planes is short enough that the launch is not one
+    // long tail of latency-bound blocks (same-box B = 4096: deep fp32 125.2 -> 123.2 ms, bf16 51.0 ->
+    // 50.2 against 2048, profiles/r4_chan_slices.txt; PCX_CHAN_TARGET overrides)
+    static const int target = getenv("PCX_CHAN_TARGET") ? std::max(256, atoi(getenv("PCX_CHAN_TARGET"))) : 16384;
+    int want = std::max(1, std::min(B, target / std::max(C, 1)));
     *bps = ceil_div(B, want);
     return ceil_div(B, *bps);
 }
