@@ -39,7 +39,27 @@ __global__ __launch_bounds__(256) void head_pool_fwd_kernel(HeadPoolArgs a) {
     }
     __syncthreads();
     const float invp = 1.f / (float)a.P;
-    for (int c = wave; c < a.C; c += blockDim.x / 64) {
+    const int nw = blockDim.x / 64;
+    if (a.P <= 64) {  // short planes (3 x 13): 4 channels per step, their loads issued together
+        const float at = lane < a.P ? att[lane] : 0.f;
+        for (int c0 = wave; c0 < a.C; c0 += 4 * nw) {
+            float v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int c = c0 + j * nw;
+                v[j] = (c < a.C && lane < a.P) ? yb[(int64_t)c * a.P + lane] : 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int c = c0 + j * nw;
+                if (c >= a.C) break;
+                const float s = wave_sum(lane < a.P ? xval(v[j], scf[c], sdr[c]) * at : 0.f);
+                if (lane == 0) a.pooled[(int64_t)b * a.C + c] = s * invp;
+            }
+        }
+        return;
+    }
+    for (int c = wave; c < a.C; c += nw) {
         const float* yc = yb + (int64_t)c * a.P;
         float4 cf = scf[c];
         float d = sdr[c];
@@ -86,7 +106,40 @@ __global__ __launch_bounds__(256) void head_pool_bwd_kernel(HeadPoolArgs a) {
     if (lane == 0) red[wave] = dls;
     __syncthreads();
     if (tid == 0 && a.wa) a.p_dba[b] = red[0] + red[1] + red[2] + red[3];
-    for (int c = wave; c < a.C; c += blockDim.x / 64) {
+    const int nw = blockDim.x / 64;
+    if (a.P <= 64) {  // short planes: 4 channels per step, loads issued together
+        const bool on = lane < a.P;
+        const float atl = on ? att[lane] : 0.f, dll = on ? dl[lane] : 0.f;
+        for (int c0 = wave; c0 < a.C; c0 += 4 * nw) {
+            float yv[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int c = c0 + j * nw;
+                yv[j] = (c < a.C && on) ? yb[(int64_t)c * a.P + lane] : 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int c = c0 + j * nw;
+                if (c >= a.C) break;
+                const float4 cf = scf[c];
+                const float dr = sdr[c], g = sdp[c], wac = swa[c];
+                const float y = yv[j], z = fmaf(y, cf.x, cf.y);
+                const float dx = fmaf(g, atl, dll * wac);
+                const float dz = (on && z > 0.f) ? dx * dr : 0.f;
+                if (on) a.dz[((int64_t)b * a.C + c) * a.P + lane] = dz;
+                const float sdz = wave_sum(dz);
+                const float sdx = wave_sum(on ? dz * ((y - cf.z) * cf.w) : 0.f);
+                const float sdw = wave_sum(on ? dll * (dr * fmaxf(z, 0.f)) : 0.f);
+                if (lane == 0) {
+                    a.p_dz[(int64_t)c * a.B + b] = sdz;
+                    a.p_dzx[(int64_t)c * a.B + b] = sdx;
+                    if (a.wa) a.p_dwa[(int64_t)c * a.B + b] = sdw;
+                }
+            }
+        }
+        return;
+    }
+    for (int c = wave; c < a.C; c += nw) {
         const float* yc = yb + (int64_t)c * a.P;
         float* dzc = a.dz + ((int64_t)b * a.C + c) * a.P;
         const float4 cf = scf[c];
