@@ -223,8 +223,10 @@ __device__ __forceinline__ int64_t xcd_logical(int64_t nblocks) {
     return (bid & 7) * xcd_per(nblocks) + (bid >> 3);
 }
 
-template <int MODE, int WM, int KC>
-__global__ __launch_bounds__(256) void convn_kernel(ConvGArgs a) {
+// EP (mode 1 only): the producer BN's backward sums in the epilogue (a separate instantiation: its
+// registers held every data-gradient launch at 1-2 waves per SIMD)
+template <int MODE, int WM, int KC, bool EP = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void convn_kernel(ConvGArgs a) {
     constexpr int WN = 2;
     constexpr int BM = 64 * WM, BN = 64 * WN;
     constexpr int RB = 2 * KC, RPI = 1024 / RB, SPR = RB / 16;  // row bytes, rows per DMA instruction, runs per row
@@ -371,7 +373,7 @@ __global__ __launch_bounds__(256) void convn_kernel(ConvGArgs a) {
                 }
             }
     }
-    if (MODE == 1 && a.ep_pg != nullptr) {
+    if constexpr (MODE == 1 && EP) {
         // backward partials of the BN + ReLU (+ Dropout2d) that produced this conv's input (replaces
         // the bwd_prep pass over dx): producer values loaded for all of a row block first, per-row
         // sums over the lanes by the transposed butterfly, the two pixel halves added
@@ -393,31 +395,30 @@ __global__ __launch_bounds__(256) void convn_kernel(ConvGArgs a) {
         }
 #pragma unroll
         for (int mi = 0; mi < WM; ++mi) {
-            float yv[WN][16], dv[WN][16];
+            // one pixel column block at a time (16 y and 16 dropout values live, not 2 x 32), summed in
+            // the same order as before (ni ascending)
+            float sg[16], sx[16];
 #pragma unroll
-            for (int ni = 0; ni < WN; ++ni)
+            for (int r = 0; r < 16; ++r) sg[r] = sx[r] = 0.f;
+#pragma unroll
+            for (int ni = 0; ni < WN; ++ni) {
+                float yv[16], dv[16];
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int64_t rc = min(m0 + wr * 32 * WM + mi * 32 + acc_row(r, h), M - 1);
-                    yv[ni][r] = a.ep_y[yb[ni] + rc * IHWe];
-                    dv[ni][r] = a.ep_drop ? a.ep_drop[db[ni] + rc] : 1.f;
+                    yv[r] = a.ep_y[yb[ni] + rc * IHWe];
+                    dv[r] = a.ep_drop ? a.ep_drop[db[ni] + rc] : 1.f;
                 }
-            float sg[16], sx[16];
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int rl = wr * 32 * WM + mi * 32 + acc_row(r, h);
-                const float4 k = cfl[rl];
-                const bool rok = m0 + rl < M;
-                float tg = 0.f, tx = 0.f;
-#pragma unroll
-                for (int ni = 0; ni < WN; ++ni) {
-                    const float y = yv[ni][r];
-                    const float g = (valid[ni] && rok && fmaf(y, k.x, k.y) > 0.f) ? acc[mi][ni][r] * dv[ni][r] : 0.f;
-                    tg += g;
-                    tx = fmaf(g, (y - k.z) * k.w, tx);
+                for (int r = 0; r < 16; ++r) {
+                    const int rl = wr * 32 * WM + mi * 32 + acc_row(r, h);
+                    const float4 k = cfl[rl];
+                    const bool rok = m0 + rl < M;
+                    const float y = yv[r];
+                    const float g = (valid[ni] && rok && fmaf(y, k.x, k.y) > 0.f) ? acc[mi][ni][r] * dv[r] : 0.f;
+                    sg[r] += g;
+                    sx[r] = fmaf(g, (y - k.z) * k.w, sx[r]);
                 }
-                sg[r] = tg;
-                sx[r] = tx;
             }
             const float tg = xsum16(sg, l32), tx = xsum16(sx, l32);
             if (!(l32 & 1)) {
@@ -772,14 +773,17 @@ int launch_convn(const ConvGArgs& a, hipStream_t s) {
     const int64_t nblocks = ceil_div(M, 64 * wm) * ceil_div(N, 64 * wn);
     PCX_CHECK_ARG(nblocks < ((int64_t)1 << 31), "convn: grid too large");
     dim3 grid((unsigned)(8 * xcd_per(nblocks)));
-#define PCX_CN(MODE_, WM_, KC_)                                                                \
-    if (a.mode == MODE_ && wm == WM_ && kc == KC_) {                                           \
-        convn_kernel<MODE_, WM_, KC_><<<grid, 256, 0, s>>>(a);                                 \
+    const bool ep = a.ep_pg != nullptr;
+#define PCX_CN(MODE_, WM_, KC_, EP_)                                                           \
+    if (a.mode == MODE_ && wm == WM_ && kc == KC_ && ep == EP_) {                              \
+        convn_kernel<MODE_, WM_, KC_, EP_><<<grid, 256, 0, s>>>(a);                            \
         PCX_LAUNCH_CHECK("convn_kernel");                                                      \
         return PCX_OK;                                                                         \
     }
-    PCX_CN(0, 1, 32) PCX_CN(0, 2, 32) PCX_CN(1, 1, 32) PCX_CN(1, 2, 32) PCX_CN(3, 1, 32) PCX_CN(3, 2, 32)
-    PCX_CN(0, 1, 64) PCX_CN(0, 2, 64) PCX_CN(1, 1, 64) PCX_CN(1, 2, 64) PCX_CN(3, 1, 64) PCX_CN(3, 2, 64)
+    PCX_CN(0, 1, 32, false) PCX_CN(0, 2, 32, false) PCX_CN(3, 1, 32, false) PCX_CN(3, 2, 32, false)
+    PCX_CN(0, 1, 64, false) PCX_CN(0, 2, 64, false) PCX_CN(3, 1, 64, false) PCX_CN(3, 2, 64, false)
+    PCX_CN(1, 1, 32, false) PCX_CN(1, 2, 32, false) PCX_CN(1, 1, 64, false) PCX_CN(1, 2, 64, false)
+    PCX_CN(1, 1, 32, true) PCX_CN(1, 2, 32, true) PCX_CN(1, 1, 64, true) PCX_CN(1, 2, 64, true)
 #undef PCX_CN
     set_error("convn: mode %d unsupported", a.mode);
     return PCX_EINVAL;
