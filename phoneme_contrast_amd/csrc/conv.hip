@@ -494,7 +494,7 @@ __device__ __forceinline__ st_u32x2 st2_ld4(const __bf16* xs, int CP, int o) {
     return v;
 }
 
-__global__ __launch_bounds__(256) void stem_fwd_mfma_kernel(StemArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void stem_fwd_mfma_kernel(StemArgs a) {
     extern __shared__ __attribute__((aligned(16))) float xs_f[];  // two bf16 copies of (H + 7) rows (spare zero row)
     __bf16* xs = reinterpret_cast<__bf16*>(xs_f);
     __shared__ float red[2][64][2];
