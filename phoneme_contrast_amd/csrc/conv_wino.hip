@@ -15,7 +15,10 @@
 // Layout / staging (MI355X-first):
 //  * persistent workgroups (two per CU) walk units = (64 consecutive tiles of one sample in row-major
 //    tile order, 32 output channels); consecutive units (neighbouring rows, the other channel groups
-//    of the same tiles) run on one XCD, so the halo rows they share come from that XCD's L2;
+//    of the same tiles) run on one XCD, so the halo rows they share come from that XCD's L2 -- taken
+//    in order from a per-XCD work queue (ConvArgs::queue, round 4) so that the workgroups do not drift
+//    apart over a launch; narrow images (W < 31) use units of 64 consecutive tiles of the whole batch
+//    (SP: a wave's 16 tiles in up to 4 row segments of one or more samples);
 //  * wave w owns tiles 16 w .. 16 w + 15 of the unit: one or two row segments of one or two tile
 //    rows.  Its LDS slot holds, per input channel, the 4 input rows of those segments side by side
 //    (<= 36 columns), so every patch of the wave is a 4 x 4 window of one slot at a per-lane column;
