@@ -25,8 +25,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from phoneme_contrast_amd.costs import (BF16_PEAK_TFLOPS, DEEP_DIMS, FP32_PEAK_TFLOPS, HBM_PEAK_GBS,  # noqa: E402
-                                        deep_kernel_costs, deep_step_cost, executed_fraction,
-                                        kernel_costs, step_cost)
+                                        deep_executed_fraction, deep_kernel_costs, deep_step_cost,
+                                        executed_fraction, executed_step_flops, kernel_costs, step_cost)
 
 METRIC = "MFCC-samples/sec per train step (cnn_small, batch 4096) at 1/2/4/8 MI355X"
 
@@ -153,6 +153,39 @@ def load_pmc(model, precision, label):
         return None
 
 
+# ----------------------------------------------------------------------------- N-GPU launch
+def relaunch(n):
+    """`--gpus N > 1` without torch.distributed.run's environment: start the N ranks as children under
+    torch.distributed.run on this node (127.0.0.1, a free port) and return its exit code.  Runs before
+    anything touches the GPU; the parent never measures, so an N-GPU request cannot print a 1-rank line."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"bench: --gpus {n} without WORLD_SIZE: launching {n} ranks under torch.distributed.run")
+    return subprocess.run(cmd).returncode
+
+
+def launch_check(args):
+    """--launch-check: the launcher path alone (no model, no GPU): every rank joins the process group
+    and rank 0 prints the ranks it saw (tests/test_bench_launch.py runs it on CPU with gloo)."""
+    from phoneme_contrast_amd import distributed as ddp
+    rank, world, _ = ddp.init_from_env(backend="gloo")
+    seen = torch.distributed.get_world_size() if ddp.is_distributed() else 1
+    if ddp.is_distributed():
+        t = torch.ones(1)
+        torch.distributed.all_reduce(t)
+        seen = int(t.item())
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "dist_world_size": seen, "requested_gpus": args.gpus}), flush=True)
+    if ddp.is_distributed():
+        torch.distributed.destroy_process_group()
+    return 0 if world == args.gpus == seen else 1
+
+
 # ----------------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
@@ -176,7 +209,17 @@ def main():
     ap.add_argument("--table-steps", type=int, default=5,
                     help="untimed steps with every kernel event-timed (the per-kernel table)")
     ap.add_argument("--no-peaks", action="store_true", help="skip the measured-peak probes")
+    ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+
+    env_world = os.environ.get("WORLD_SIZE")
+    if args.gpus > 1 and env_world is None:
+        sys.exit(relaunch(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        log(f"error: --gpus {args.gpus} but WORLD_SIZE={env_world}: refusing to report a mismatched line")
+        sys.exit(2)
+    if args.launch_check:
+        sys.exit(launch_check(args))
 
     from phoneme_contrast_amd import distributed as ddp
     from phoneme_contrast_amd.losses import GlobalSupervisedContrastiveLoss, SupervisedContrastiveLoss
@@ -184,8 +227,6 @@ def main():
     from phoneme_contrast_amd.optim import FusedAdam
 
     rank, world, local = ddp.init_from_env()
-    if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}")
     local = local % max(1, torch.cuda.device_count())  # == LOCAL_RANK on a full node
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -283,49 +324,59 @@ def main():
         for lab, (tot, cnt) in sorted(table.items(), key=lambda kv: -kv[1][0]):
             kernels[lab] = {"avg_ms": round(tot / cnt, 4), "launches": cnt,
                             "share": round(tot / tsteps / ms_step, 4)}
+    xfrac = (lambda lab: deep_executed_fraction(lab, F, T, bf16)) if deep else (lambda lab: executed_fraction(lab, T))
     if dom is not None and prof.get(dom):
         # the dominant kernel: the costed label with the largest total time in the table steps (every
         # kernel that matters has a cost model; the labels without one are tiny finalisers /
-        # reductions), timed on its launch stream inside the timed region
+        # reductions), timed on its launch stream inside the timed region.  Its FLOPs are the ones it
+        # EXECUTES (a Winograd F(2x2,3x3) kernel performs 16 multiplies per 2x2 outputs, 4/9 of the
+        # direct conv's); the direct-conv-equivalent rate is reported beside it (alg_equiv_*).
         dom_any = max(table, key=lambda k: table[k][0])
         tot, cnt = prof[dom]
         avg_s = tot / cnt / 1000.0
         fl, by = costs[dom]
-        ai = fl / by
-        if ai > peak * 1e12 / (HBM_PEAK_GBS * 1e9):
-            ach = fl / avg_s / 1e12
+        xf = xfrac(dom)
+        xfl = fl * xf
+        if xfl / by > peak * 1e12 / (HBM_PEAK_GBS * 1e9):
+            ach = xfl / avg_s / 1e12
             roof = {"kernel": dom, "bound": "mfma", "achieved": sig(ach), "peak": peak,
-                    "unit": "TFLOP/s", "frac": sig(ach / peak)}
+                    "unit": "TFLOP/s", "frac": sig(ach / peak), "flops_counted": "executed"}
         else:
             ach = by / avg_s / 1e9
             roof = {"kernel": dom, "bound": "hbm", "achieved": sig(ach), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": sig(ach / HBM_PEAK_GBS)}
         roof["traffic"] = load_pmc(args.model, args.precision if deep else "fp32", dom)
+        roof["executed_flops_per_launch"] = int(xfl)
         roof["algorithmic_flops_per_launch"] = fl
         roof["algorithmic_bytes_per_launch"] = by
+        if xf != 1.0:
+            roof["alg_equiv_achieved"] = sig(fl / avg_s / 1e12)
+            roof["alg_equiv_frac"] = sig(fl / avg_s / 1e12 / peak)
+            roof["executed_per_algorithmic"] = round(xf, 6)
         roof["avg_launch_ms"] = round(avg_s * 1000.0, 4)
         roof["timed_launches"] = cnt
     if roof is not None:
         roof["largest_label_overall"] = dom_any
-        if not deep and roof["bound"] == "mfma":
-            # cnn_small's 3x3 convs run Winograd F(2x2,3x3): 4/9 of the direct multiplies are executed
-            xf = executed_fraction(dom, T)
-            roof["executed_flops_per_launch"] = int(fl * xf)
-            roof["executed_frac"] = sig(roof["frac"] * xf)
         for lab, rec in kernels.items():  # per-kernel achieved rates for every costed label
             if lab in costs:
                 f_, b_ = costs[lab]
                 t_ = rec["avg_ms"] / 1000.0
-                rec["alg_tflops"] = round(f_ / t_ / 1e12, 2) if f_ else None
+                if f_:
+                    rec["exec_tflops"] = round(f_ * xfrac(lab) / t_ / 1e12, 2)
+                    rec["exec_frac"] = round(f_ * xfrac(lab) / t_ / 1e12 / peak, 4)
+                    rec["alg_tflops"] = round(f_ / t_ / 1e12, 2)
                 rec["alg_gbps"] = round(b_ / t_ / 1e9, 1)
     # SURVEY 8(d)'s step byte model at the element size this path stores activations in (bf16 line:
     # e = 2, the survey's bf16 roof; fp32 lines: e = 4), and beside it the bytes the path actually
     # moves: the committed rocprofv3 PMC traffic per launch of every timed label x launches per step
     sf, sb = deep_step_cost(B, F, T, D, e=2 if bf16 else 4) if deep else step_cost(B, F, T, D)
     step_s = el / args.steps
-    step_roof = {"flops_per_step": sf, "bytes_per_step": sb,
+    xsf = executed_step_flops(B, F, T, D, deep=deep, bf16=bf16)
+    step_roof = {"flops_per_step": sf, "executed_flops_per_step": xsf, "bytes_per_step": sb,
                  "byte_model": "SURVEY 8(d), e=2 (bf16 activations)" if bf16 else "SURVEY 8(d), e=4 (fp32)",
-                 "mfma_fraction": round(sf / step_s / (peak * 1e12), 4),
+                 "mfma_fraction": round(xsf / step_s / (peak * 1e12), 4),
+                 "mfma_fraction_counts": "executed FLOPs (Winograd kernels at 16 multiplies per 2x2 outputs)",
+                 "alg_equiv_mfma_fraction": round(sf / step_s / (peak * 1e12), 4),
                  "hbm_fraction": round(sb / step_s / (HBM_PEAK_GBS * 1e9), 4)}
     if table:
         mkey = (args.model, args.precision if deep else "fp32")
@@ -379,6 +430,7 @@ def main():
                    "allreduce": None if bucketer is None else f"{nbuckets} {backend} buckets behind the backward",
                    "allreduce_buckets": nbuckets,
                    "dist_backend": backend,
+                   "dist_world_size": torch.distributed.get_world_size() if ddp.is_distributed() else 1,
                    "supcon": "global batch (embedding + coefficient all-gathers, anchor rows per rank)"
                              if args.global_supcon and world > 1 else "per rank (DDP-equivalent)"},
         "conv_algorithms": None if deep else {

@@ -79,6 +79,42 @@ def executed_fraction(label, T):
     return 1.0
 
 
+def deep_executed_fraction(label, F, T, bf16=False, h=DEEP_DIMS):
+    """Multiplies executed per algorithmic multiply for cnn_deep's kernels (deep.hip routing): in fp32
+    the stride-1 3x3 convs whose channel counts fit the cnn_small engines (block 0 conv1, every conv2)
+    run forward / data gradient on Winograd F(2x2,3x3) (conv_wino.hip: rows >= 31 columns, and the
+    batch-spanning units below that) and the weight gradient on wgrad_wino.hip at even widths; the
+    stem, the stride-2 convs, the 1x1 shortcuts and every bf16 conv are direct."""
+    if bf16:
+        return 1.0
+    routed = {}
+    for fl, wl, dl, ci, co, k, s, IH, IW, OH, OW in deep_convs(F, T, h):
+        fits = (co == 32 or co % 64 == 0) and (ci == 32 or ci % 64 == 0)
+        if k == 3 and s == 1 and fits:
+            routed[fl] = routed[dl] = 4 / 9
+            routed[wl] = 4 / 9 if OW % 2 == 0 else 1.0
+    return routed.get(label, 1.0)
+
+
+def executed_step_flops(B, F, T, D=128, deep=False, bf16=False):
+    """FLOPs the step executes: the algorithmic step FLOPs with every Winograd kernel's convolution
+    counted at the multiplies it performs (16 per 2x2 outputs instead of 36)."""
+    if deep:
+        total, _ = deep_step_cost(B, F, T, D, e=2 if bf16 else 4)
+        costs = deep_kernel_costs(B, F, T, bf16, D)
+        frac = lambda lab: deep_executed_fraction(lab, F, T, bf16)  # noqa: E731
+        labels = [lab for c in deep_convs(F, T) for lab in c[:3] if lab]
+    else:
+        total, _ = step_cost(B, F, T, D)
+        costs = kernel_costs(B, F, T, D)
+        frac = lambda lab: executed_fraction(lab, T)  # noqa: E731
+        # (at even widths layer 2's data gradient and weight gradient run as one kernel, wgbd_L2, with the
+        # same executed fraction as the two it replaces)
+        labels = [f"{p}{l}" for l in range(2, 7) for p in ("conv_fwd_L", "conv_dgrad_L", "wgrad_L")]
+    saved = sum(costs[lab][0] * (1.0 - frac(lab)) for lab in labels if lab in costs)
+    return int(total - saved)
+
+
 def deep_convs(F, T, h=DEEP_DIMS):
     """(fwd label, wgrad label, dgrad label or None, cin, cout, k, stride, IH, IW, OH, OW) of every
     conv of cnn_deep, labelled as deep.hip profiles them."""
@@ -177,8 +213,20 @@ def deep_step_cost(B, F, T, D=128, e=4, h=DEEP_DIMS, nparams=4968833):
     return flops, act + 40 * nparams + 12 * B * D
 
 
-def step_cost(B, F, T, D=128):
-    """Algorithmic FLOPs and bytes of one whole train step."""
+def small_nparams(D=128, use_attention=True):
+    """Parameter count of cnn_small (PhonemeNet, reference src/models/phoneme_cnn.py:31-80): convs
+    1->32->32, 32->64->64, 64->128->128 with BN, the 1x1 attention conv, Linear(128, D) + BN1d(D)."""
+    n = 0
+    for ci, co in ((1, 32), (32, 32), (32, 64), (64, 64), (64, 128), (128, 128)):
+        n += co * ci * 9 + co + 2 * co
+    if use_attention:
+        n += 128 + 1
+    return n + 128 * D + D + 2 * D
+
+
+def step_cost(B, F, T, D=128, nparams=None):
+    """Algorithmic FLOPs and bytes of one whole train step; nparams defaults
+    to cnn_small's own count at this D (304,225 at D = 128 with attention)."""
     flops = 0
     act_bytes = 4 * 2 * B * F * T  # input read twice
     for l, ci, co, h, w in small_layers(B, F, T):
@@ -186,21 +234,24 @@ def step_cost(B, F, T, D=128):
         flops += 2 * macs * (2 if l == 1 else 3)
         act_bytes += 4 * 5 * B * co * h * w
     flops += 4 * B * B * D + 3 * 2 * B * 128 * D
-    params = 304225
+    params = small_nparams(D) if nparams is None else nparams
     return flops, act_bytes + 40 * params + 12 * B * D
 
 
 def model_step_cost(model, B, F, T):
-    """(FLOPs, bytes, peak TFLOP/s) of one train step of `model` (a PhonemeNet / PhonemeNetDeep)
-    at per-rank batch B and input [B, 1, F, T] under this cost model, or None for other models."""
+    """(FLOPs, bytes, peak TFLOP/s, executed FLOPs) of one train step of `model` (a PhonemeNet /
+    PhonemeNetDeep) at per-rank batch B and input [B, 1, F, T] under this cost model, or None for
+    other models.  Executed FLOPs count the Winograd kernels at the multiplies they perform."""
     name = type(model).__name__
     D = getattr(model, "embedding_dim", 128)
     if name == "PhonemeNet":
-        fl, by = step_cost(B, F, T, D)
-        return fl, by, FP32_PEAK_TFLOPS
+        fl, by = step_cost(B, F, T, D, nparams=sum(p.numel() for p in model.parameters()))
+        return fl, by, FP32_PEAK_TFLOPS, fl - (step_cost(B, F, T, D)[0] - executed_step_flops(B, F, T, D))
     if name == "PhonemeNetDeep":
         bf16 = getattr(model, "precision", "fp32") == "bf16"
         n = sum(p.numel() for p in model.parameters())
-        fl, by = deep_step_cost(B, F, T, D, e=2 if bf16 else 4, h=list(model.hidden_dims), nparams=n)
-        return fl, by, BF16_PEAK_TFLOPS if bf16 else FP32_PEAK_TFLOPS
+        h = list(model.hidden_dims)
+        fl, by = deep_step_cost(B, F, T, D, e=2 if bf16 else 4, h=h, nparams=n)
+        xfl = fl if (bf16 or h != DEEP_DIMS) else executed_step_flops(B, F, T, D, deep=True)
+        return fl, by, BF16_PEAK_TFLOPS if bf16 else FP32_PEAK_TFLOPS, xfl
     return None

@@ -173,11 +173,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
     // (no global load inside the row loop: a vmcnt wait there would also wait for the next row's staging
     // loads), so mask = [x > 0] (exactly [s yp + t > 0]) and, where the mask is on, x = s yp + t, hence
     // xhat = (yp - mean) invstd = x r1 + r0 with r1 = invstd / s, r0 = -(t / s + mean) invstd
+    // That recovery loses ~eps |t / s| invstd of xhat and cannot work at s == 0 (BN_prev gamma 0: x is the
+    // constant relu(t)); such channels (|t| invstd > 16 |s|, NaN-safe) read yp itself in the epilogue: a
+    // block-uniform slow path (flag `rare`), so the common path keeps its loop free of global loads.
+    // (rare channels: ecf = {0, 0}, ecf_yp = {invstd, -mean invstd}, applied to yp)
     float2* const ecf = reinterpret_cast<float2*>(xb + 2 * 4096 + 2048);
+    float2* const ecf_yp = ecf + CH;
+    int* const rare = reinterpret_cast<int*>(ecf_yp + CH);
+    if (tid == 0) *rare = 0;
+    __syncthreads();
     if (tid < CH) {
         const float4 k = a.cf_x[tid];
-        const float r1 = k.x != 0.f ? k.w / k.x : 0.f;
-        ecf[tid] = make_float2(r1, -(k.y * r1) - k.z * k.w);
+        const bool ok = fabsf(k.x) * 16.f >= fabsf(k.y) * k.w && k.x != 0.f;
+        const float r1 = ok ? k.w / k.x : 0.f;
+        ecf[tid] = ok ? make_float2(r1, -(k.y * r1) - k.z * k.w) : make_float2(0.f, 0.f);
+        ecf_yp[tid] = ok ? make_float2(0.f, 0.f) : make_float2(k.w, -k.z * k.w);
+        if (!ok) atomicOr(rare, 1);
     }
 
     // the task loop is instantiated once per wave role (the weight-gradient and the data-gradient code
@@ -428,13 +439,24 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
                         const int64_t o = pb + (int64_t)c * HW + h0 * W + 2 * (t0 + tile);
                         const float2 k = ecf[c];
                         const float gv[4] = {y00, y01, y10, y11};
-                        float dz[4];
+                        float dz[4], xh[4];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) xh[e] = fmaf(ex[k2][e], k.x, k.y);
+                        if (__builtin_amdgcn_readfirstlane(*rare)) {  // block-uniform: some channel's BN_prev scale is (near) zero
+                            const float2 kr = ecf_yp[c];
+                            if (kr.x != 0.f) {
+                                const float* yq = a.yp + o;
+#pragma unroll
+                                for (int e = 0; e < 4; ++e)
+                                    xh[e] = (e < 2 || r1ok) ? fmaf(yq[(e >> 1) * W + (e & 1)], kr.x, kr.y) : 0.f;
+                            }
+                        }
 #pragma unroll
                         for (int e = 0; e < 4; ++e) {
                             const float xe = ex[k2][e];  // 0 outside the image (row H of an odd H)
                             dz[e] = xe > 0.f ? gv[e] : 0.f;
                             rz[k2] += dz[e];
-                            rx_[k2] = fmaf(dz[e], fmaf(xe, k.x, k.y), rx_[k2]);
+                            rx_[k2] = fmaf(dz[e], xh[e], rx_[k2]);
                         }
                         *reinterpret_cast<float2*>(a.dzp + o) = make_float2(dz[0], dz[1]);
                         if (r1ok) *reinterpret_cast<float2*>(a.dzp + o + W) = make_float2(dz[2], dz[3]);
@@ -515,7 +537,7 @@ bool wgbd_wino_geometry(int B, int H, int W, int C, WinoBwdArgs* a) {
     if (nx > 16 * 2) return false;  // 16 threads x NIR = 2 items per row and channel
     const int XCS = smallest_2odd(std::max(V * kmax + 1, 2 * smax + 5));
     // rings, exchange buffer, the lanes' float64 sums, the epilogue coefficients
-    const size_t lds = ((size_t)4 + 8 * CH * XCS + 2 * 4096) * 4 + 256 * 4 * 8 + CH * 8;
+    const size_t lds = ((size_t)4 + 8 * CH * XCS + 2 * 4096) * 4 + 256 * 4 * 8 + 2 * CH * 8 + 16;
     if (lds > 160 * 1024) return false;
     if ((int64_t)CH * H * W * 4 >= OOB) return false;
     if (a) {

@@ -255,10 +255,13 @@ class ContrastiveTrainer:
             rec["samples_per_s"] = round(self.world_size * samples / seconds, 1)
             cost = model_step_cost(self.model, shape[0], shape[-2], shape[-1]) if shape and len(shape) == 4 else None
             if cost is not None:
-                fl, by, peak = cost
+                fl, by, peak, xfl = cost
                 per = seconds / steps
-                rec.update({"step_tflops": round(fl / per / 1e12, 2), "step_gbps": round(by / per / 1e9, 1),
-                            "mfma_fraction": round(fl / per / (peak * 1e12), 4),
+                # mfma_fraction on the FLOPs the step executes (Winograd kernels: 16 multiplies per 2x2
+                # outputs); the direct-conv-equivalent rate beside it
+                rec.update({"step_tflops": round(xfl / per / 1e12, 2), "step_gbps": round(by / per / 1e9, 1),
+                            "mfma_fraction": round(xfl / per / (peak * 1e12), 4),
+                            "alg_equiv_mfma_fraction": round(fl / per / (peak * 1e12), 4),
                             "hbm_fraction": round(by / per / (HBM_PEAK_GBS * 1e9), 4),
                             "cost_model": "phoneme_contrast_amd/costs.py (SURVEY 8(d)); last batch shape "
                                           f"{list(shape)}"})

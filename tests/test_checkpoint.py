@@ -89,7 +89,8 @@ def test_metrics_json_layout():
 
 def test_perf_json_layout():
     """perf.json: one record per epoch with samples/s and the step's roofline
-    fractions from phoneme_contrast_amd.costs (cnn_small at B = 4096, T = 200: 7.29 TFLOP, 73.7 GB)."""
+    fractions from phoneme_contrast_amd.costs (cnn_small at B = 4096, T = 200: 3.27 TFLOP executed, 7.29
+    TFLOP direct-conv equivalent, 73.7 GB)."""
     m = model_registry.create("phoneme_cnn", {"embedding_dim": 128})
     out = Path(tempfile.mkdtemp())
     t = _trainer(m, torch.optim.SGD(m.parameters(), 0.1), None, {}, out)
@@ -101,8 +102,10 @@ def test_perf_json_layout():
     e0 = got["epochs"][0]
     assert got["world_size"] == 1 and len(got["epochs"]) == 2 and got["epochs"][1]["steps"] == 0
     assert e0["ms_per_step"] == 50.0 and e0["samples_per_s"] == 81920.0
-    assert abs(e0["step_tflops"] - 7294498635776 / 0.05 / 1e12) < 0.01
-    assert abs(e0["mfma_fraction"] - 7294498635776 / 0.05 / 157.3e12) < 1e-4
+    # executed FLOPs: the Winograd convs of layers 2-6 at 4/9 of their direct-conv count
+    assert abs(e0["step_tflops"] - 3267966795776 / 0.05 / 1e12) < 0.01
+    assert abs(e0["mfma_fraction"] - 3267966795776 / 0.05 / 157.3e12) < 1e-4
+    assert abs(e0["alg_equiv_mfma_fraction"] - 7294498635776 / 0.05 / 157.3e12) < 1e-4
     assert 0 < e0["hbm_fraction"] < 1
 
 

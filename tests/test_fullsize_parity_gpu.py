@@ -9,14 +9,14 @@ split-K reductions and the BatchNorm statistics over 4096 x H x W are all exerci
 BASELINE size.  Reference: /root/reference/src/models/phoneme_cnn.py:98-126 (cnn_small),
 :274-304 (cnn_deep), src/training/losses.py:41-86 (SupCon).
 
-Tolerances (stated contract): embeddings 1e-5 abs, loss 1e-4 abs, gradients
-2e-3 x max|g| per tensor (biases feeding a train-mode BN: 1e-4 abs, their exact gradient is 0),
-running statistics 1e-5 rel (cnn_deep fp32 embeddings too: 4.5e-6 measured, round 4).  Both
-models' gradients are also compared with torch's own float32 evaluation of the same step (the
-reference's arithmetic): cnn_small's layer-1 gradients are 33 M-term sums at the end of a 6-layer
-backward (~1e-3 of max|g| in any float32 evaluation), and cnn_deep's ReLU / max-pool kinks move
-float32 gradients by up to ~1e-2 of max|g| in any float32 evaluation (tools/wgrad_probe.py: the weight-gradient engines alone are at 1e-6 at these
-shapes), so each tensor passes within 3x the yardstick's largest error.  Every test prints its
+Tolerances (stated contract): embeddings 1e-5 abs, loss 1e-4 abs, gradients per
+tensor max(2e-3, 3 x that tensor's own float32-yardstick error) x max|g| (max-abs and L2; biases feeding
+a train-mode BN: 1e-4 abs, their exact gradient is 0), running statistics 1e-5 rel (cnn_deep fp32
+embeddings too: 4.5e-6 measured, round 4).  The yardstick is torch's own float32 evaluation of the same
+step (the reference's arithmetic): cnn_small's layer-1 gradients are 33 M-term sums at the end of a
+6-layer backward (~1e-3 of max|g| in any float32 evaluation), and cnn_deep's ReLU / max-pool kinks move
+float32 gradients by up to ~1e-2 of max|g| in any float32 evaluation (tools/wgrad_probe.py: the
+weight-gradient engines alone are at 1e-6 at these shapes).  Every test prints its
 per-tensor max-abs and L2 errors (FULLSIZE lines) and records them, with the tolerances they were
 held to, in gpurun_out/fullsize_parity.json (PCX_FULLSIZE_JSON overrides the path; the round's copy
 is committed under profiles/).
@@ -87,38 +87,44 @@ def _run_oracle(sd64, x, labels, masks, temperature, dtype=torch.float64):
 
 def _grad_errors(got, ref):
     """per tensor: ("abs" | "rel", max-abs error (relative to max|ref| unless a BN-fed bias),
-    relative L2 error)"""
+    relative L2 error, or None for a BN-fed bias: its exact gradient is 0, so norm(g - r) / norm(r)
+    would divide float noise by float noise)"""
     out = {}
     for k, r in ref["grads"].items():
         g = got["grads"][k]
-        l2 = (torch.linalg.vector_norm(g - r) / max(torch.linalg.vector_norm(r).item(), 1e-300)).item()
         if bn_fed_bias(k, None):
-            out[k] = ("abs", max(g.abs().max().item(), r.abs().max().item()), l2)
+            out[k] = ("abs", max(g.abs().max().item(), r.abs().max().item()), None)
         else:
+            l2 = (torch.linalg.vector_norm(g - r) / max(torch.linalg.vector_norm(r).item(), 1e-300)).item()
             out[k] = ("rel", ((g - r).abs().max() / max(r.abs().max().item(), 1e-30)).item(), l2)
     return out
 
 
 def _compare(got, ref, emb_tol, name, yardstick=None):
     """yardstick: the reference's own float32 arithmetic (the same restatement evaluated by torch in
-    float32) against the same float64 values.  cnn_deep's ReLU / max-pool kinks make its float32
-    gradients leave the float64 ones by up to ~1e-2 in ANY float32 evaluation (a kink that flips
-    under float32 rounding reroutes a gradient): there a tensor passes within 3x the largest error
-    the yardstick shows on any tensor (max-abs and L2), else at the 2e-3 contract."""
+    float32) against the same float64 values.  Layer-1 gradients (33 M-term sums at the end of the
+    backward) and cnn_deep's ReLU / max-pool kinks move ANY float32 evaluation's gradients away from the
+    float64 ones by up to ~1e-2 of max|g| (a kink that flips under float32 rounding reroutes a gradient).
+    Contract, per tensor: max-abs and L2 errors each below
+    max(2e-3, 3 x THAT tensor's own yardstick error) -- a tensor the yardstick reproduces to 1e-7 is
+    still held to 2e-3, never to another tensor's noise."""
     de = (got["emb"] - ref["emb"]).abs().max().item()
     dl = abs(got["loss"] - ref["loss"])
     errs = _grad_errors(got, ref)
     ys = _grad_errors(yardstick, ref) if yardstick is not None else {}
+    tol_m = {k: max(2e-3, 3.0 * ys[k][1]) if k in ys else 2e-3 for k, v in errs.items() if v[0] == "rel"}
+    tol_l = {k: max(2e-3, 3.0 * ys[k][2]) if k in ys else 2e-3 for k, v in errs.items() if v[0] == "rel"}
     rec = {"emb": de, "loss": dl, "grads_maxrel": {k: v[1] for k, v in errs.items()},
            "grads_l2rel": {k: v[2] for k, v in errs.items()},
            "float32_yardstick_maxrel": {k: v[1] for k, v in ys.items()},
-           "float32_yardstick_l2rel": {k: v[2] for k, v in ys.items()}}
-    ymax = max((v[1] for v in ys.values() if v[0] == "rel"), default=0.0)
-    yl2 = max((v[2] for v in ys.values() if v[0] == "rel"), default=0.0)
-    rec["tolerances"] = {"emb": emb_tol, "loss": 1e-4, "grad_maxrel": max(2e-3, 3.0 * ymax),
-                         "grad_l2rel": max(2e-3, 3.0 * yl2), "bn_fed_bias_abs": 1e-4}
+           "float32_yardstick_l2rel": {k: v[2] for k, v in ys.items()},
+           "grad_maxrel_bound": tol_m, "grad_l2rel_bound": tol_l}
+    rec["tolerances"] = {"emb": emb_tol, "loss": 1e-4, "grad": "per tensor max(2e-3, 3 x its float32 yardstick)",
+                         "bn_fed_bias_abs": 1e-4}
     rec["worst_grad_maxrel"] = max((v[1] for v in errs.values() if v[0] == "rel"), default=0.0)
     rec["worst_grad_l2rel"] = max((v[2] for v in errs.values() if v[0] == "rel"), default=0.0)
+    rec["worst_margin"] = max((max(v[1] / tol_m[k], v[2] / tol_l[k]) for k, v in errs.items() if v[0] == "rel"),
+                              default=0.0)
     print(f"\nFULLSIZE {name} " + json.dumps(rec, sort_keys=True))
     _record(name, rec)
     assert de < emb_tol, de
@@ -128,8 +134,8 @@ def _compare(got, ref, emb_tol, name, yardstick=None):
         if kind == "abs":
             if not err < 1e-4:
                 bad[k] = (err, 1e-4)
-        elif not (err < max(2e-3, 3.0 * ymax) and l2 < max(2e-3, 3.0 * yl2)):
-            bad[k] = (err, l2, max(2e-3, 3.0 * ymax), max(2e-3, 3.0 * yl2))
+        elif not (err < tol_m[k] and l2 < tol_l[k]):
+            bad[k] = (err, l2, tol_m[k], tol_l[k])
     assert not bad, json.dumps(bad, sort_keys=True)
     for k, r in ref["state"].items():
         assert torch.allclose(got["state"][k], r, rtol=1e-5, atol=1e-6), k

@@ -20,3 +20,12 @@ def test_no_packed_valu_overwrites_wide_store_data():
                        capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout[-4000:] + p.stderr[-2000:]
     assert "0 hazard(s)" in p.stdout
+
+
+def test_no_bitcast_of_vector_lane_lvalues():
+    """ROCm 7.2's clang reads element 0 for `__builtin_bit_cast(T, v[i])` on an ext_vector_type lvalue (the
+    root cause of round 4's wrong pooled-dz dy, tools/bitcast_lane_probe.cpp): no source may contain one."""
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "isa_hazard_check.py"), "--bitcast-lanes"],
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stdout[-4000:]
+    assert "0 bit_cast lane finding(s)" in p.stdout

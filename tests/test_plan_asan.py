@@ -11,9 +11,9 @@ BIN = os.path.join(ROOT, "tools", "plan_check_asan")
 
 
 def test_plan_builders_clean_under_asan_ubsan():
-    if not os.path.exists(BIN):
-        r = subprocess.run(["make", "-j8", "asan"], cwd=ROOT, capture_output=True, text=True, timeout=900)
-        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    # always through make (incremental): a sanitizer binary older than the plan builders would test old code
+    r = subprocess.run(["make", "-j8", "asan"], cwd=ROOT, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
     r = subprocess.run([BIN], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]

@@ -60,6 +60,8 @@ WB_CASES = [  # H, W, B, reps [, pooled dz]: the fused layer-2 backward (wgbd_wi
     (21, 56, 16, 1),    # odd H (a half tile row at the bottom), one 28-tile strip
     (40, 200, 48, 1, 1),  # dz as layer 3's pooled gradient + window selection (EPI_BWD_POOLSELP's output)
     (20, 100, 24, 1, 1),
+    (40, 200, 16, 1, 1, 1),  # producer BN scale 0 / tiny on three channels: xhat from yp itself
+    (20, 100, 8, 1, 0, 1),
 ]
 
 

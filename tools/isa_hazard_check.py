@@ -11,6 +11,14 @@ data registers (the hazard needs one wait state: flagged when the v_pk_* is the 
 instruction; the store data of a 4-dword store is read a cycle after its issue).
 
     python tools/isa_hazard_check.py [build_dir]      (exit 1 on findings)
+
+Second guard (--bitcast-lanes [src dirs]): ROCm 7.2's clang lowers `__builtin_bit_cast(T, v[i])`, with v an
+ext_vector_type value and v[i] an element lvalue, to a load of the VECTOR's address: it returns element 0's
+bits whatever i is (host and device alike; tools/bitcast_lane_probe.cpp shows it).  That was the round-4
+"wrong dy" of the pooled-dz weight gradient (commit d4d63c9): the selection bytes held in lane 2 of the dz
+vector were read back as `__builtin_bit_cast(unsigned, dzv[m][2])`, i.e. as the bits of the first pooled
+gradient in lane 0 -- no FTZ or other float op touched them.  The guard flags every bit_cast whose operand is
+a subscripted lvalue (`x[...]`); bit-cast a scalar temporary instead (`float t = v[i];`).
 """
 import glob
 import os
@@ -68,7 +76,34 @@ def scan(lines):
     return found
 
 
+BITCAST_SUB = re.compile(r"__builtin_bit_cast\s*\(\s*[^,()]+(?:\([^()]*\))?\s*,\s*([A-Za-z_][\w.]*\s*(?:\[[^\]]*\]\s*)+)\)")
+
+
+def scan_bitcast_lanes(dirs):
+    """(file, line, text) of every __builtin_bit_cast whose operand is a subscripted lvalue."""
+    found = []
+    for d in dirs:
+        for path in sorted(glob.glob(os.path.join(d, "*.hip")) + glob.glob(os.path.join(d, "*.h")) +
+                           glob.glob(os.path.join(d, "*.cpp"))):
+            if os.path.basename(path) == "bitcast_lane_probe.cpp":  # the defect's demonstration
+                continue
+            with open(path) as f:
+                for n, line in enumerate(f, 1):
+                    code = line.split("//")[0]
+                    if BITCAST_SUB.search(code):
+                        found.append((path, n, line.strip()))
+    return found
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "--bitcast-lanes":
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        dirs = sys.argv[2:] or [os.path.join(root, "phoneme_contrast_amd", "csrc"), os.path.join(root, "tools")]
+        bad = scan_bitcast_lanes(dirs)
+        for path, n, text in bad:
+            print(f"{os.path.relpath(path)}:{n}: bit_cast of a subscripted lvalue: {text}")
+        print(f"{len(bad)} bit_cast lane finding(s)")
+        return 1 if bad else 0
     bdir = sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(os.path.dirname(
         os.path.abspath(__file__))), "build")
     objs = sorted(glob.glob(os.path.join(bdir, "*.o")))

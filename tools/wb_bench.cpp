@@ -65,10 +65,13 @@ static double maxrel(const std::vector<float>& a, const std::vector<float>& b) {
 }
 
 int main(int argc, char** argv) {
-    if (argc < 3) { printf("usage: wb_bench H W [B] [reps]\n"); return 2; }
+    if (argc < 3) { printf("usage: wb_bench H W [B] [reps] [pooled dz] [rare gammas]\n"); return 2; }
     const int H = atoi(argv[1]), W = atoi(argv[2]);
     const int B = argc > 3 ? atoi(argv[3]) : 4096, reps = argc > 4 ? atoi(argv[4]) : 5;
     const bool pd = argc > 5 && atoi(argv[5]) != 0;
+    // rare: the producer BN's scale s = gamma invstd is 0 on channel 3 (t > 0: every pixel unmasked) and tiny
+    // on channels 7 / 11, where the kernel cannot rebuild xhat from the staged relu(s yp + t)
+    const bool rare = argc > 6 && atoi(argv[6]) != 0;
     const int C = 32;
     pcx::WinoBwdArgs f{};
     pcx::WinoWgradArgs w{};
@@ -90,6 +93,14 @@ int main(int argc, char** argv) {
     fill<<<4096, 256>>>(dz, n, 1, 2.f, 0.f); fill<<<4096, 256>>>(y, n, 2, 2.f, 0.f); fill<<<4096, 256>>>(yp, n, 3, 2.f, 0.f);
     fill<<<1, 256>>>(cfd, C * 4, 4, 0.5f, 1.f); fill<<<1, 256>>>(cfx, C * 4, 5, 0.5f, 0.5f);
     fill<<<1, 256>>>(wt, nw, 6, 0.4f, 0.f);
+    if (rare) {
+        std::vector<float> h(C * 4);
+        (void)hipMemcpy(h.data(), cfx, C * 16, hipMemcpyDeviceToHost);
+        h[3 * 4 + 0] = 0.f; h[3 * 4 + 1] = 0.3f;
+        h[7 * 4 + 0] = 1e-6f; h[7 * 4 + 1] = -0.2f;
+        h[11 * 4 + 0] = -3e-7f; h[11 * 4 + 1] = 0.4f;
+        (void)hipMemcpy(cfx, h.data(), C * 16, hipMemcpyHostToDevice);
+    }
     (void)hipMemset(dzp1, 0, n * 4); (void)hipMemset(dzp2, 0, n * 4);
     check(pcx::launch_wino_pack(wt, up, C, C, 1, 0), "wino_pack");
     float* dpool = nullptr;
@@ -168,8 +179,8 @@ int main(int argc, char** argv) {
     for (int i = 0; i < reps; ++i) twok();
     (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
     (void)hipEventElapsedTime(&tr, e0, e1);
-    printf("wgbd%s H=%d W=%d B=%d strips=%d (%d,%d) nslice=%d: fused %.3f ms, two-kernel %.3f ms; "
-           "dW rel %.2e, dz_prev rel %.2e, BN sums rel %.2e\n", pd ? " (pooled dz)" : "", H, W, B, f.nseg, f.seg_S[0], f.seg_S[1], f.nslice,
+    printf("wgbd%s%s H=%d W=%d B=%d strips=%d (%d,%d) nslice=%d: fused %.3f ms, two-kernel %.3f ms; "
+           "dW rel %.2e, dz_prev rel %.2e, BN sums rel %.2e\n", pd ? " (pooled dz)" : "", rare ? " (zero / tiny BN scales)" : "", H, W, B, f.nseg, f.seg_S[0], f.seg_S[1], f.nslice,
            tf / reps, tr / reps, ew, ed, eb);
     return (ew < 2e-5 && ed < 2e-5 && eb < 2e-5) ? 0 : 2;
 }
