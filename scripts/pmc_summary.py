@@ -223,6 +223,16 @@ def label_stalls(rename_trace, csv_path, out_json, key):
             d["trace_ms"] = round(dv[len(dv) // 2], 4)
             if d.get("GRBM_GUI_ACTIVE"):
                 d["clock_ghz"] = round(d["GRBM_GUI_ACTIVE"] / 8.0 / (d["trace_ms"] * 1e6), 3)
+            if d.get("SQ_INSTS_VALU_MFMA_MOPS_F32"):
+                # fp32 MFMA work the hardware counted (units of 512 FLOPs): the executed FLOPs of the launch,
+                # independent of the cost model, and their rate against the 157.3 TFLOP/s fp32 peak
+                fl = d["SQ_INSTS_VALU_MFMA_MOPS_F32"] * 512.0
+                d["mops_f32_flops"] = fl
+                d["mops_f32_frac"] = round(fl / (d["trace_ms"] * 1e-3) / 157.3e12, 4)
+            if d.get("SQ_INSTS_VALU_MFMA_MOPS_BF16"):
+                fl = d["SQ_INSTS_VALU_MFMA_MOPS_BF16"] * 512.0
+                d["mops_bf16_flops"] = fl
+                d["mops_bf16_frac"] = round(fl / (d["trace_ms"] * 1e-3) / 2500e12, 4)
     try:
         with open(out_json) as fi:
             allres = json.load(fi)

@@ -150,3 +150,92 @@ def test_deep_bf16_full_size_properties():
     assert torch.isfinite(torch.tensor(l)) and all(torch.isfinite(t).all() for t in g)
     e2, l2, g2 = outs[1]
     assert torch.equal(e, e2) and l == l2 and all(torch.equal(a, b) for a, b in zip(g, g2))
+
+
+@pytest.mark.parametrize("T", [200, 201])
+def test_deep_bf16_b512_full_width_matches_rounded_f64(T):
+    """cnn_deep bf16 (config 5's model, full widths 64..512) at B = 512, against the rounded-operand
+    float64 reference evaluated on the GPU (torch im2col + rocBLAS in float64, MIOpen off): the
+    persistent channel-last engine, its epilogue BN partials (forward mode 0, data-gradient mode 1) and
+    the multi-block channel reductions at a batch where every grid runs many rounds.  Same tolerances as
+    the small-batch cases above; the measured margins go to the full-size JSON record (profiles/).
+    Reference: src/models/phoneme_cnn.py:146-216, 274-304; T = 201: src/datasets/dataset.py:50."""
+    import gc
+    import json
+    import os
+    from oracle import torch_port as tp
+    from phoneme_contrast_amd.losses import SupervisedContrastiveLoss
+    from phoneme_contrast_amd.models import PhonemeNetDeep
+    B = 512
+    torch.manual_seed(23)
+    cfg = dict(DEEP, hidden_dims=FULL, precision="bf16")
+    m = PhonemeNetDeep(cfg)
+    sd = m.state_dict()
+    m = m.cuda().train()
+    g = torch.Generator().manual_seed(77)
+    x = torch.randn(B, 1, 40, T, generator=g)
+    labels = torch.arange(B) // 4
+    masks = [(torch.rand(B, c, generator=g) > 0.2).float() / 0.8 for c in FULL]
+    m.set_dropout_masks(masks)
+    e = m(x.cuda())
+    loss = SupervisedContrastiveLoss(temperature=0.15)(e, labels.cuda())
+    loss.backward()
+    got = {k: p.grad.detach().double().cpu() for k, p in m.named_parameters()}
+    e64 = e.detach().double().cpu()
+    lgot = loss.item()
+    run_stats = {k: v.detach().double().cpu() for k, v in m.state_dict().items() if "running" in k}
+    del m, e, loss
+    gc.collect()
+    torch.cuda.empty_cache()
+    with torch.backends.cudnn.flags(enabled=False):
+        dev = torch.device("cuda")
+        out = {}
+        for kind in ("rnd", "exact"):
+            r = PhonemeNetDeep(dict(cfg, precision="fp32")).double()
+            r.load_state_dict(sd)
+            if kind == "rnd":
+                _round_conv_operands(r)
+            r = r.to(dev).train()
+            er = _torch_reference(r, x.double().to(dev), [k.double().to(dev) for k in masks])
+            lr_ = tp.supcon(er, labels.to(dev), 0.15, 0.07)
+            lr_.backward()
+            out[kind] = (er.detach().cpu(), lr_.item(), {k: p.grad.detach().cpu() for k, p in r.named_parameters()},
+                         {k: v.detach().cpu() for k, v in r.state_dict().items() if "running" in k})
+            del r, er, lr_
+            gc.collect()
+            torch.cuda.empty_cache()
+    e_rnd, l_rnd, g_rnd, s_rnd = out["rnd"]
+    e_ref, l_ref, _, _ = out["exact"]
+    exact = (e64 - e_rnd).abs().max().item()
+    vs_f64 = (e64 - e_ref).abs().max().item()
+    cos = {}
+    for k, gg in got.items():
+        if bn_fed_bias(k, None) or k.startswith("attention"):
+            continue
+        a, b = gg.flatten(), g_rnd[k].flatten()
+        cos[k] = (a @ b / (a.norm() * b.norm() + 1e-300)).item()
+    worst = min(cos, key=cos.get)
+    rstat = max(((run_stats[k] - s_rnd[k]).abs() / (s_rnd[k].abs() + 1e-3)).max().item() for k in s_rnd)
+    rec = {"B": B, "T": T, "emb_vs_rounded_f64": exact, "emb_vs_f64": vs_f64, "loss_vs_f64": abs(lgot - l_ref),
+           "loss_vs_rounded_f64": abs(lgot - l_rnd), "min_grad_cosine": cos[worst], "min_grad_cosine_tensor": worst,
+           "grad_cosine": cos, "running_stats_maxrel": rstat,
+           "tolerances": {"emb_vs_rounded_f64": 1e-2, "emb_vs_f64": 5e-2, "loss_vs_f64": 5e-2, "grad_cosine": 0.98,
+                          "running_stats": "rtol 1e-2, atol 1e-3"}}
+    print(f"\nFULLSIZE cnn_deep_bf16_B512_T{T} " + json.dumps(rec, sort_keys=True))
+    path = os.environ.get("PCX_FULLSIZE_JSON", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                              "gpurun_out", "fullsize_parity.json"))
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    try:
+        with open(path) as f:
+            allrec = json.load(f)
+    except (OSError, ValueError):
+        allrec = {}
+    allrec[f"cnn_deep_bf16_B512_T{T}"] = rec
+    with open(path, "w") as f:
+        json.dump(allrec, f, indent=1, sort_keys=True)
+    assert exact < 1e-2
+    assert vs_f64 < 5e-2
+    assert abs(lgot - l_ref) < 5e-2
+    assert cos[worst] > 0.98, (worst, cos[worst])
+    for k in s_rnd:
+        assert torch.allclose(run_stats[k], s_rnd[k], rtol=1e-2, atol=1e-3), k
