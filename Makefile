@@ -8,12 +8,17 @@ OBJ = $(patsubst phoneme_contrast_amd/csrc/%.hip,build/%.o,$(SRC))
 HDR = $(wildcard phoneme_contrast_amd/csrc/*.h) include/pcx.h
 LIB = phoneme_contrast_amd/libpcx.so
 
-TOOLS = tools/wino_bench tools/ww_bench tools/stem_bench tools/wb_bench tools/ws_bench
+TOOLS = tools/wino_bench tools/ww_bench tools/stem_bench tools/wb_bench tools/ws_bench tools/wino4_bench
 
 all: $(LIB) $(TOOLS)
 
 # engine cross-check / micro-benchmark (tests/test_wino_engine_gpu.py runs it)
 tools/wino_bench: tools/wino_bench.cpp $(LIB) $(HDR)
+	$(HIPCC) -O2 -std=c++17 --offload-arch=$(ARCH) -Iinclude $< -Lphoneme_contrast_amd -lpcx \
+	    -Wl,-rpath,'$$ORIGIN/../phoneme_contrast_amd' -o $@
+
+# F(4x3) Winograd conv vs the F(2x2) one (tests/test_wino_engine_gpu.py runs it)
+tools/wino4_bench: tools/wino4_bench.cpp $(LIB) $(HDR)
 	$(HIPCC) -O2 -std=c++17 --offload-arch=$(ARCH) -Iinclude $< -Lphoneme_contrast_amd -lpcx \
 	    -Wl,-rpath,'$$ORIGIN/../phoneme_contrast_amd' -o $@
 
@@ -45,6 +50,7 @@ build/%.o: phoneme_contrast_amd/csrc/%.hip $(HDR)
 build/conv_wino.o: CXXFLAGS += -fno-slp-vectorize
 build/wgrad_wino.o: CXXFLAGS += -fno-slp-vectorize
 build/wgbd_wino.o: CXXFLAGS += -fno-slp-vectorize
+build/conv_wino4.o: CXXFLAGS += -fno-slp-vectorize
 
 $(LIB): $(OBJ)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJ)

@@ -771,7 +771,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
 #pragma unroll
                     for (int q = 0; q < 4; ++q)
                         av[mi][q] = *reinterpret_cast<const f32x4*>(bw + (((cl * 4 + q) * 32) + 16 * mi + n) * 4);
+#if defined(WINO_KO) && (WINO_KO & 8)  // analysis builds only: no BN + ReLU prologue arithmetic
+                if (false) {
+#else
                 if (PRO != PRO_RAW) {
+#endif
                     const f2 st = *reinterpret_cast<const f2*>(cft + 2 * (c0 + cl));
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
