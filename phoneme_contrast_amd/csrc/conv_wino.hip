@@ -133,6 +133,35 @@ __device__ __forceinline__ float row16_xsel8(const float (&v)[8], int n) {
 __device__ __forceinline__ void st2(float* p, float x, float y) { *reinterpret_cast<float2*>(p) = make_float2(x, y); }
 __device__ __forceinline__ float2 ld2(const float* p) { return *reinterpret_cast<const float2*>(p); }
 
+// Branch-free epilogue stores (round 5): a guarded global store (`if (ok) p[i] = v`) compiles to an exec-mask
+// branch per store -- 16 to 64 per unit, ~11-40 % of the conv's time in the epilogue knock-outs
+// (profiles/r5_wino_knockouts.txt).  Instead every store is a buffer store relative to the wave's first
+// output plane: lanes keep byte offsets, an element outside the image gets an offset past num_records (the
+// hardware drops the store), the channel's plane offset rides in soffset.
+constexpr unsigned WOOB = 0x80000000u;  // masked element offset (> every num_records used)
+typedef unsigned u32x2w __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4w __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void bst1(__amdgpu_buffer_rsrc_t r, unsigned vo, int so, float x) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), r, vo, so, 0);
+}
+__device__ __forceinline__ void bst2(__amdgpu_buffer_rsrc_t r, unsigned vo, int so, float x, float y) {
+    __builtin_amdgcn_raw_buffer_store_b64(u32x2w{__builtin_bit_cast(unsigned, x), __builtin_bit_cast(unsigned, y)}, r,
+                                          vo, so, 0);
+}
+__device__ __forceinline__ void bst4(__amdgpu_buffer_rsrc_t r, unsigned vo, int so, float x, float y, float z, float w) {
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4w{__builtin_bit_cast(unsigned, x), __builtin_bit_cast(unsigned, y),
+                                                  __builtin_bit_cast(unsigned, z), __builtin_bit_cast(unsigned, w)},
+                                           r, vo, so, 0);
+}
+__device__ __forceinline__ float2 bld2(__amdgpu_buffer_rsrc_t r, unsigned vo, int so) {
+    const u32x2w t = __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0);
+    const unsigned t0 = t.x, t1 = t.y;  // (named copies: no bit_cast of a vector-lane lvalue)
+    return make_float2(__builtin_bit_cast(float, t0), __builtin_bit_cast(float, t1));
+}
+__device__ __forceinline__ float bld1(__amdgpu_buffer_rsrc_t r, unsigned vo, int so) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
+}
+
 // Epilogue of one unit.  Lane (n, kq) holds output channels n0 + 16 mi + 4 kq + i (j = 4 mi + i < 8)
 // of its tile (outputs y[j][e] at (2 tr + (e >> 1), 2 tc + (e & 1))).  The 16 lanes of a row hold
 // 16 consecutive tiles of one or two tile rows, so a store of one output row is a 128-byte run.
@@ -154,25 +183,39 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
     const int poff[4] = {0, 1, a.W, a.W + 1};
     const int jsel = (n >> 1) & 7;                               // channel this lane reduces
     const int cosel = 16 * (jsel >> 2) + 4 * kq + (jsel & 3);
+    // store bases: the wave's first sample bw (lane 0 holds the wave's first tile; host-checked 32-bit offsets)
+    const int bw = __builtin_amdgcn_readfirstlane(b);
+    const int lpl = (b - bw) * a.cout + 4 * kq;  // the lane's channel-4kq plane relative to the wave's first
+    auto wrs = [&](const void* base, int hw, int esz) {  // tensor [B][cout][hw] of esz-byte elements
+        const int64_t rest = ((int64_t)(a.B - bw) * a.cout - n0) * hw * esz;
+        const int nrec = rest <= 0 ? 0 : (int)(rest < 0x7ffffff0 ? rest : 0x7ffffff0);
+        const float* p = reinterpret_cast<const float*>(static_cast<const char*>(base) +
+                                                        ((int64_t)bw * a.cout + n0) * hw * esz);
+        return wrsrc(wuniform(p), __builtin_amdgcn_readfirstlane(nrec));
+    };
+    // channel j's plane offset (bytes, uniform)
+    auto chs = [&](int j, int hwb) { return __builtin_amdgcn_readfirstlane((16 * (j >> 2) + (j & 3)) * hwb); };
+    unsigned oe[4];  // conv-resolution byte offsets of the lane's 4 outputs (channel 4 kq), masked
+#pragma unroll
+    for (int e = 0; e < 4; ++e) oe[e] = ok[e] ? 4u * (unsigned)(lpl * HW + pix0 + poff[e]) : WOOB;
     if (EPI == EPI_FWD) {
         // store y; per channel Chan statistics of the block: each wave sums about a shift K (the
         // channel's first output in its row of lanes), reduced with the transposed butterfly
-        float* ob = a.out + ((int64_t)b * a.cout + n0) * HW + pix0;
+        const __amdgpu_buffer_rsrc_t rs = wrs(a.out, HW, 4);
         float cnt = 0.f;
 #pragma unroll
         for (int e = 0; e < 4; ++e) cnt += ok[e] ? 1.f : 0.f;
         float s1[8], s2[8], kv[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            float* o = ob + (int64_t)(16 * (j >> 2) + 4 * kq + (j & 3)) * HW;
+            const int so = chs(j, 4 * HW);
             const float* v = y[j];
             if (vec) {
-                if (ok[0]) st2(o, v[0], v[1]);
-                if (ok[2]) st2(o + a.W, v[2], v[3]);
+                bst2(rs, oe[0], so, v[0], v[1]);
+                bst2(rs, oe[2], so, v[2], v[3]);
             } else {
 #pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    if (ok[e]) o[poff[e]] = v[e];
+                for (int e = 0; e < 4; ++e) bst1(rs, oe[e], so, v[e]);
             }
             kv[j] = __shfl(v[0], lane & 48, 64);
             float t1 = 0.f, t2 = 0.f;
@@ -214,31 +257,25 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
             if (tid == 0 && n0 == 0) a.partn[tb] = nn;
         }
     } else if (EPI == EPI_BWD_STORE) {
-        float* ob = a.out + ((int64_t)b * a.cout + n0) * HW + pix0;
+        const __amdgpu_buffer_rsrc_t rs = wrs(a.out, HW, 4);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            float* o = ob + (int64_t)(16 * (j >> 2) + 4 * kq + (j & 3)) * HW;
+            const int so = chs(j, 4 * HW);
             const float* v = y[j];
             if (vec) {
 #pragma unroll
-                for (int rr = 0; rr < 2; ++rr)
-                    if (ok[2 * rr]) {
-                        float* q = o + rr * a.W;
-                        float2 t = make_float2(v[2 * rr], v[2 * rr + 1]);
-                        if (a.accumulate) {
-                            const float2 p = ld2(q);
-                            t.x += p.x;
-                            t.y += p.y;
-                        }
-                        st2(q, t.x, t.y);
+                for (int rr = 0; rr < 2; ++rr) {
+                    float2 t = make_float2(v[2 * rr], v[2 * rr + 1]);
+                    if (a.accumulate) {  // (masked loads read 0)
+                        const float2 p = bld2(rs, oe[2 * rr], so);
+                        t.x += p.x;
+                        t.y += p.y;
                     }
+                    bst2(rs, oe[2 * rr], so, t.x, t.y);
+                }
             } else {
 #pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    if (ok[e]) {
-                        float* q = o + poff[e];
-                        *q = a.accumulate ? *q + v[e] : v[e];
-                    }
+                for (int e = 0; e < 4; ++e) bst1(rs, oe[e], so, a.accumulate ? bld1(rs, oe[e], so) + v[e] : v[e]);
             }
         }
     } else {
@@ -246,31 +283,28 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
         // producer BN's backward sums (dz, dz * xhat) per channel
         float sz[8], sx[8];
         if (EPI == EPI_BWD_RELU) {
-            // all loads first (addresses clamped in bounds), then the arithmetic and the stores: one
-            // memory round trip per unit instead of one per channel
-            const int pixc = tvalid ? pix0 : 0;
-            const int row1 = ok[2] ? a.W : 0;
-            const float* yb = a.yprev + ((int64_t)b * a.cout + n0) * HW + pixc;
-            float* ob = a.out + ((int64_t)b * a.cout + n0) * HW + pix0;
+            // all loads first (masked elements read 0), then the arithmetic and the stores: one memory
+            // round trip per unit instead of one per channel
+            const __amdgpu_buffer_rsrc_t ry = wrs(a.yprev, HW, 4);
             float4 cf[8];
             float yy[8][4];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int co = 16 * (j >> 2) + 4 * kq + (j & 3);
+                const int so = chs(j, 4 * HW);
                 cf[j] = a.cf_out[n0 + co];
-                const float* yp = yb + (int64_t)co * HW;
                 if (vec) {
-                    const float2 p0 = ld2(yp), p1 = ld2(yp + row1);
+                    const float2 p0 = bld2(ry, oe[0], so), p1 = bld2(ry, oe[2], so);
                     yy[j][0] = p0.x; yy[j][1] = p0.y; yy[j][2] = p1.x; yy[j][3] = p1.y;
                 } else {
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) yy[j][e] = yp[ok[e] ? poff[e] : 0];
+                    for (int e = 0; e < 4; ++e) yy[j][e] = bld1(ry, oe[e], so);
                 }
             }
+            const __amdgpu_buffer_rsrc_t rs = wrs(a.out, HW, 4);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const int co = 16 * (j >> 2) + 4 * kq + (j & 3);
-                float* op = ob + (int64_t)co * HW;
+                const int so = chs(j, 4 * HW);
                 float dz[4], s_z = 0.f, s_x = 0.f;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
@@ -279,12 +313,11 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
                     s_x = fmaf(dz[e], (yy[j][e] - cf[j].z) * cf[j].w, s_x);
                 }
                 if (vec) {
-                    if (ok[0]) st2(op, dz[0], dz[1]);
-                    if (ok[2]) st2(op + a.W, dz[2], dz[3]);
+                    bst2(rs, oe[0], so, dz[0], dz[1]);
+                    bst2(rs, oe[2], so, dz[2], dz[3]);
                 } else {
 #pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        if (ok[e]) op[poff[e]] = dz[e];
+                    for (int e = 0; e < 4; ++e) bst1(rs, oe[e], so, dz[e]);
                 }
                 sz[j] = s_z;
                 sx[j] = s_x;
@@ -295,11 +328,14 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
             // element and its index (bn_relu_pool_kernel), read at the conv's (pooled) resolution -- a
             // quarter of the full-resolution window reads; dz written at Hs x Ws as EPI_BWD_POOL does
             const int HWs = a.Hs * a.Ws;
-            const int pixc = tvalid ? pix0 : 0;
-            const int row1 = ok[2] ? a.W : 0;
-            const float* ysb = a.ysel + ((int64_t)b * a.cout + n0) * HW + pixc;
-            const uint8_t* pab = a.parg + ((int64_t)b * a.cout + n0) * HW + pixc;
-            float* ob = a.out + ((int64_t)b * a.cout + n0) * HWs + (2 * h0) * a.Ws + 2 * w0;
+            const __amdgpu_buffer_rsrc_t ry = wrs(a.ysel, HW, 4), ra = wrs(a.parg, HW, 1);
+            const __amdgpu_buffer_rsrc_t ro = wrs(PO ? static_cast<const void*>(a.dpool) : a.out, PO ? HW : HWs, 4);
+            unsigned ob[4], os[4];  // parg byte offsets; full-resolution window offsets (row r0, column c0)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                ob[e] = ok[e] ? (unsigned)(lpl * HW + pix0 + poff[e]) : WOOB;
+                os[e] = ok[e] ? 4u * (unsigned)(lpl * HWs + (2 * h0 + 2 * (e >> 1)) * a.Ws + 2 * w0 + 2 * (e & 1)) : WOOB;
+            }
 #pragma unroll
             for (int half = 0; half < 2; ++half) {
                 // four channels' loads together (one round trip per batch; registers)
@@ -310,29 +346,26 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
                 for (int jj = 0; jj < 4; ++jj) {
                     const int j = 4 * half + jj;
                     const int co = 16 * (j >> 2) + 4 * kq + (j & 3);
+                    const int so = chs(j, 4 * HW), sb = chs(j, HW);
                     cf[jj] = a.cf_out[n0 + co];
                     dv[jj] = a.drop_out ? a.drop_out[(int64_t)b * a.cout + n0 + co] : 1.f;
-                    const float* yp = ysb + (int64_t)co * HW;
-                    const uint8_t* pp = pab + (int64_t)co * HW;
                     if (vec) {
-                        const float2 p0 = ld2(yp), p1 = ld2(yp + row1);
+                        const float2 p0 = bld2(ry, oe[0], so), p1 = bld2(ry, oe[2], so);
                         ys[jj][0] = p0.x; ys[jj][1] = p0.y; ys[jj][2] = p1.x; ys[jj][3] = p1.y;
-                        ag[jj] = (unsigned)*reinterpret_cast<const uint16_t*>(pp) |
-                                 ((unsigned)*reinterpret_cast<const uint16_t*>(pp + row1) << 16);
+                        ag[jj] = (unsigned)__builtin_amdgcn_raw_buffer_load_b16(ra, ob[0], sb, 0) |
+                                 ((unsigned)__builtin_amdgcn_raw_buffer_load_b16(ra, ob[2], sb, 0) << 16);
                     } else {
                         ag[jj] = 0;
 #pragma unroll
                         for (int e = 0; e < 4; ++e) {
-                            ys[jj][e] = yp[ok[e] ? poff[e] : 0];
-                            ag[jj] |= (unsigned)pp[ok[e] ? poff[e] : 0] << (8 * e);
+                            ys[jj][e] = bld1(ry, oe[e], so);
+                            ag[jj] |= (unsigned)__builtin_amdgcn_raw_buffer_load_b8(ra, ob[e], sb, 0) << (8 * e);
                         }
                     }
                 }
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj) {
                     const int j = 4 * half + jj;
-                    const int co = 16 * (j >> 2) + 4 * kq + (j & 3);
-                    float* op = ob + (int64_t)co * HWs;
                     const float4 k = cf[jj];
                     float dzw[4][4], dde[4];
                     float s_z = 0.f, s_x = 0.f;
@@ -356,31 +389,32 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
                     if constexpr (PO) {
                         // EPI_BWD_POOLSELP: the consumer rebuilds the windows from parg -- the routed
                         // gradient at the pooled resolution only (a quarter of the full-resolution writes)
-                        float* pq = a.dpool + ((int64_t)b * a.cout + n0 + co) * HW + pix0;
+                        const int so = chs(j, 4 * HW);
                         if (vec) {
-                            if (ok[0]) st2(pq, dde[0], dde[1]);
-                            if (ok[2]) st2(pq + a.W, dde[2], dde[3]);
+                            bst2(ro, oe[0], so, dde[0], dde[1]);
+                            bst2(ro, oe[2], so, dde[2], dde[3]);
                         } else {
 #pragma unroll
-                            for (int e = 0; e < 4; ++e)
-                                if (ok[e]) pq[poff[e]] = dde[e];
+                            for (int e = 0; e < 4; ++e) bst1(ro, oe[e], so, dde[e]);
                         }
-                    } else if constexpr (V4) {
-                        if (tvalid)
+                    } else {
+                        const int so = chs(j, 4 * HWs);
+                        if constexpr (V4) {  // (H, W even: ok[e] == tvalid; the window rows are 16-byte runs)
 #pragma unroll
                             for (int r = 0; r < 4; ++r)
-                                st4(op + r * a.Ws, make_float4(dzw[r][0], dzw[r][1], dzw[r][2], dzw[r][3]));
-                    } else {
+                                bst4(ro, os[0] + (r == 0 ? 0u : 4u * (unsigned)(r * a.Ws)), so, dzw[r][0], dzw[r][1],
+                                     dzw[r][2], dzw[r][3]);
+                        } else {
 #pragma unroll
-                        for (int e = 0; e < 4; ++e)
-                            if (ok[e]) {
+                            for (int e = 0; e < 4; ++e) {  // (dword stores: odd Ws leaves rows 4-byte aligned)
                                 const int r0 = 2 * (e >> 1), c0 = 2 * (e & 1);
-                                float* q = op + r0 * a.Ws + c0;
-                                q[0] = dzw[r0][c0];
-                                q[1] = dzw[r0][c0 + 1];
-                                q[a.Ws] = dzw[r0 + 1][c0];
-                                q[a.Ws + 1] = dzw[r0 + 1][c0 + 1];
+                                const unsigned o1 = os[e] + 4u * (unsigned)a.Ws;
+                                bst1(ro, os[e], so, dzw[r0][c0]);
+                                bst1(ro, os[e] + 4u, so, dzw[r0][c0 + 1]);
+                                bst1(ro, o1, so, dzw[r0 + 1][c0]);
+                                bst1(ro, o1 + 4u, so, dzw[r0 + 1][c0 + 1]);
                             }
+                        }
                     }
                     sz[j] = s_z;
                     sx[j] = s_x;
@@ -391,7 +425,11 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
             constexpr int PB = V4 ? 1 : 2;  // channels per batch of window loads (registers)
             const int soff0 = tvalid ? (2 * h0) * a.Ws + 2 * w0 : 0;  // loads clamped in bounds
             const float* yb = a.yprev + ((int64_t)b * a.cout + n0) * HWs + soff0;
-            float* ob = a.out + ((int64_t)b * a.cout + n0) * HWs + (2 * h0) * a.Ws + 2 * w0;
+            const __amdgpu_buffer_rsrc_t ro = wrs(a.out, HWs, 4);
+            unsigned os[4];  // full-resolution window offsets (row r0, column c0), masked
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                os[e] = ok[e] ? 4u * (unsigned)(lpl * HWs + (2 * h0 + 2 * (e >> 1)) * a.Ws + 2 * w0 + 2 * (e & 1)) : WOOB;
 #pragma unroll
             for (int half = 0; half < 8 / PB; ++half) {
                 // PB channels' windows loaded together (one round trip per batch; registers)
@@ -428,7 +466,6 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
                 for (int jj = 0; jj < PB; ++jj) {
                     const int j = PB * half + jj;
                     const int co = 16 * (j >> 2) + 4 * kq + (j & 3);
-                    float* op = ob + (int64_t)co * HWs;
                     float dzw[4][4];
                     float s_z = 0.f, s_x = 0.f;
 #pragma unroll
@@ -453,22 +490,22 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
                         s_z += dd;
                         s_x = fmaf(dd, (ya - k.z) * k.w, s_x);
                     }
+                    const int so = chs(j, 4 * HWs);
                     if (V4) {
-                        if (tvalid)
 #pragma unroll
-                            for (int r = 0; r < 4; ++r)
-                                st4(op + r * a.Ws, make_float4(dzw[r][0], dzw[r][1], dzw[r][2], dzw[r][3]));
+                        for (int r = 0; r < 4; ++r)
+                            bst4(ro, os[0] + (r == 0 ? 0u : 4u * (unsigned)(r * a.Ws)), so, dzw[r][0], dzw[r][1],
+                                 dzw[r][2], dzw[r][3]);
                     } else {
 #pragma unroll
-                        for (int e = 0; e < 4; ++e)
-                            if (ok[e]) {
-                                const int r0 = 2 * (e >> 1), c0 = 2 * (e & 1);
-                                float* q = op + r0 * a.Ws + c0;
-                                q[0] = dzw[r0][c0];
-                                q[1] = dzw[r0][c0 + 1];
-                                q[a.Ws] = dzw[r0 + 1][c0];
-                                q[a.Ws + 1] = dzw[r0 + 1][c0 + 1];
-                            }
+                        for (int e = 0; e < 4; ++e) {
+                            const int r0 = 2 * (e >> 1), c0 = 2 * (e & 1);
+                            const unsigned o1 = os[e] + 4u * (unsigned)a.Ws;
+                            bst1(ro, os[e], so, dzw[r0][c0]);
+                            bst1(ro, os[e] + 4u, so, dzw[r0][c0 + 1]);
+                            bst1(ro, o1, so, dzw[r0 + 1][c0]);
+                            bst1(ro, o1 + 4u, so, dzw[r0 + 1][c0 + 1]);
+                        }
                     }
                     sz[j] = s_z;
                     sx[j] = s_x;
@@ -1036,6 +1073,13 @@ int launch_conv3x3_wino(int pro, int epi, ConvArgs a, hipStream_t s) {
     PCX_CHECK_ARG(!sp || (pro == PRO_RAW && (epi == EPI_FWD || epi == EPI_BWD_STORE) && a.src_guard),
                   "conv3x3_wino: %dx%d images need PRO_RAW, EPI_FWD / EPI_BWD_STORE and src_guard", a.H, a.W);
     PCX_CHECK_ARG(a.nblk == g.nblk, "conv3x3_wino: partial buffer sized for %d tiles, need %d", a.nblk, g.nblk);
+    {  // the epilogue's 32-bit buffer offsets span the samples of one wave's tiles x cout output planes
+        const int64_t ns = sp ? (64 + g.NTS - 1) / g.NTS + 1 : 1;
+        const int64_t hwo = std::max<int64_t>((int64_t)a.H * a.W, (epi == EPI_BWD_POOL || epi == EPI_BWD_POOLSEL)
+                                                                      ? (int64_t)a.Hs * a.Ws : 0);
+        PCX_CHECK_ARG(4 * ns * a.cout * hwo < 0x7ffffff0, "conv3x3_wino: %d x %lld outputs per sample exceed the "
+                      "epilogue's 32-bit offsets", a.cout, (long long)hwo);
+    }
     PCX_CHECK_ARG(pro == PRO_RAW || pro == PRO_BNRELU, "conv3x3_wino: prologue %d", pro);
     if (epi == EPI_BWD_POOL || epi == EPI_BWD_POOLSEL)
         PCX_CHECK_ARG(a.Hs >= 2 * a.H && a.Ws >= 2 * a.W, "conv3x3_wino: pooled source %dx%d for %dx%d", a.Hs, a.Ws,

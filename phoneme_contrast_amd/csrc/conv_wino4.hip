@@ -243,15 +243,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         const int nrec = rest < 1 ? 1 : (int)min(rest, (int64_t)(a.cin + W4_CK) * HW + 1);
         const __amdgpu_buffer_rsrc_t r = w4_rsrc(sb, __builtin_amdgcn_readfirstlane(4 * nrec));
         const unsigned sl = lds0 + 4u * (unsigned)(buf * W4_BUFF + wave * W4_WSLOT);
+#if !(defined(WINO4_KO) && (WINO4_KO & 1))  // analysis builds only (tools/wino4_kx.sh): no input copies
 #pragma unroll
         for (int j = 0; j < W4_NCP; ++j) w4_bdma(r, voff[j], sl + 1024u * (unsigned)j);
+#endif
         const float* sw = w4_uniform(a.wpack + ((int64_t)x.cg * a.cin + c0) * (32 * W4_XS));
         const unsigned wl = lds0 + 4u * (unsigned)(buf * W4_BUFF + W4_INF);
+#if !(defined(WINO4_KO) && (WINO4_KO & 2))  // analysis builds only: no weight copies
 #pragma unroll
         for (int j = 0; j < (W4_WDMA + 3) / 4; ++j) {
             const int jj = 4 * j + wave;
             if (jj < W4_WDMA) w4_gdma(sw, 16u * (unsigned)(64 * jj + lane), wl + 1024u * (unsigned)jj);
         }
+#endif
     };
 
     const int nchunk = a.cin / W4_CK;
@@ -309,10 +313,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                 }
                 float d[6][5];
                 const float* pp = bi + pbase;
+#if defined(WINO4_KO) && (WINO4_KO & 8)  // analysis builds only: the patch as 8 aligned 16-byte reads (wrong values)
+                {
+                    const float* pq = bi + wave * W4_WSLOT + 4 * lane;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const f32x4 t = *reinterpret_cast<const f32x4*>(pq + 256 * (k & 3) + 8 * (k >> 2));
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            if (4 * k + e < 30) d[(4 * k + e) / 5][(4 * k + e) % 5] = t[e];
+                    }
+                }
+#else
 #pragma unroll
                 for (int r = 0; r < 6; ++r)
 #pragma unroll
                     for (int c = 0; c < 5; ++c) d[r][c] = pp[r * W4_ROW + c];
+#endif
                 if (PRO != PRO_RAW) {
                     const f2v st = *reinterpret_cast<const f2v*>(cft + 2 * (c0 + kq));
 #pragma unroll
@@ -365,7 +382,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             auto chunk = [&](int k, auto ftag) {
                 const int c0 = k * W4_CK;
                 if (a.queue && tid == 0 && k + 1 == nchunk) qsl[par ^ 1] = qv;
+#if !(defined(WINO4_KO) && (WINO4_KO & 4))  // analysis builds only: no wait for the chunk copies
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
                 __syncthreads();  // chunk k visible to every wave; chunk k - 1 consumed
                 const bool more = k + 1 < nchunk;
                 if (!more && a.queue) {
@@ -396,24 +415,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         const int cosel = 16 * (jsel >> 2) + 4 * kq + (jsel & 3);
         float s1[8], s2[8], kv[8];
         const float cntl = (float)(nrow * ncol);
+        // branch-free stores and producer reads: buffer accesses relative to the wave's first plane (sample ba,
+        // channel n0); an element outside the tile's image part gets an offset past num_records (store dropped,
+        // load 0), the channel's plane offset rides in soffset
+        const int64_t orest = ((int64_t)(a.B - cur.ba) * a.cout - n0) * HW;
+        const int onrec = __builtin_amdgcn_readfirstlane(
+            4 * (int)(orest < 0 ? 0 : min(orest, (int64_t)2 * a.cout * HW)));
+        const int64_t obase = ((int64_t)cur.ba * a.cout + n0) * HW;
+        const int lofs = ((b - cur.ba) * a.cout + 4 * kq) * HW + pix0;
+        unsigned eoff[4][3];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+                eoff[r][c] = (full || (r < nrow && c < ncol)) ? 4u * (unsigned)(lofs + r * a.W + c) : 0x80000000u;
+        const __amdgpu_buffer_rsrc_t rs_o =
+            w4_rsrc(w4_uniform((EPI == EPI_FWD || EPI == EPI_BWD_RELU ? a.out : a.dpool) + obase), onrec);
+        const __amdgpu_buffer_rsrc_t rs_y =
+            w4_rsrc(w4_uniform((EPI == EPI_BWD_RELU ? a.yprev : EPI == EPI_FWD ? a.out : a.ysel) + obase), onrec);
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 __builtin_amdgcn_sched_barrier(0);  // one channel at a time: its 30 accumulators leave the AGPRs here
                 const int j = 4 * mi + i, co = 16 * mi + 4 * kq + i;
-                const int64_t plane = ((int64_t)b * a.cout + n0 + co) * HW;
+                const int soff = __builtin_amdgcn_readfirstlane(4 * (16 * mi + i) * HW);
                 // (data gradient: the producer's values first, so their latency runs under the transform)
                 float yy[4][3];
                 float4 k4 = make_float4(0.f, 0.f, 0.f, 0.f);
                 float dv = 1.f;
                 if (EPI != EPI_FWD) {
                     k4 = a.cf_out[n0 + co];
-                    const float* yq = (EPI == EPI_BWD_RELU ? a.yprev : a.ysel) + plane + pix0;
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
 #pragma unroll
-                        for (int c = 0; c < 3; ++c) yy[r][c] = yq[(full || (r < nrow && c < ncol)) ? r * a.W + c : 0];
+                        for (int c = 0; c < 3; ++c)
+                            yy[r][c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_y, eoff[r][c], soff, 0));
                     if (EPI == EPI_BWD_POOLSELP && a.drop_out) dv = a.drop_out[(int64_t)b * a.cout + n0 + co];
                 }
                 // Y = Ar^T M Ac
@@ -430,12 +467,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
                 for (int r = 0; r < 4; ++r) at5(t[r][0], t[r][1], t[r][2], t[r][3], t[r][4], y[r]);
                 if (EPI == EPI_FWD) {
-                    float* o = a.out + plane + pix0;
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
 #pragma unroll
                         for (int c = 0; c < 3; ++c)
-                            if (full || (r < nrow && c < ncol)) o[r * a.W + c] = y[r][c];
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(y[r][c]), rs_o, eoff[r][c], soff, 0);
                     kv[j] = __shfl(y[0][0], lane & 48, 64);
                     float t1 = 0.f, t2 = 0.f;
 #pragma unroll
@@ -452,7 +488,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                     // dz = dx through the producer's ReLU(BN) (EPI_BWD_RELU: y_prev; EPI_BWD_POOLSELP: y at each 2x2
                     // window's selected element, dropout; the routed gradient stored at the conv's (pooled)
                     // resolution into dpool) + the producer BN's backward sums
-                    float* o = (EPI == EPI_BWD_RELU ? a.out : a.dpool) + plane + pix0;
                     float s_z = 0.f, s_x = 0.f;
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
@@ -460,7 +495,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                         for (int c = 0; c < 3; ++c) {
                             const bool ok = full || (r < nrow && c < ncol);
                             const float dz = (ok && fmaf(yy[r][c], k4.x, k4.y) > 0.f) ? y[r][c] * dv : 0.f;
-                            if (ok) o[r * a.W + c] = dz;
+                            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dz), rs_o, eoff[r][c], soff, 0);
                             s_z += dz;
                             s_x = fmaf(dz, (yy[r][c] - k4.z) * k4.w, s_x);
                         }
@@ -568,6 +603,7 @@ bool wino4_geometry(int B, int H, int W, int cin, int cout, Wino4Geo* g) {
     r.TR = (H + 3) / 4;
     r.TC = (W + 2) / 3;
     if (r.TC < 16) return false;  // the 16 tiles of a wave span at most two tile rows
+    if ((int64_t)8 * (cin > cout ? cin : cout) * H * W >= ((int64_t)1 << 31)) return false;  // 32-bit buffer offsets
     r.NTS = r.TR * r.TC;
     if ((int64_t)B * r.NTS >= ((int64_t)1 << 22)) return false;  // batch-wide tile indices (float division)
     r.NTOT = B * r.NTS;
