@@ -130,8 +130,6 @@ __device__ __forceinline__ float row16_xsel8(const float (&v)[8], int n) {
     return b1 ? w2[1] : w2[0];
 }
 
-__device__ __forceinline__ void st2(float* p, float x, float y) { *reinterpret_cast<float2*>(p) = make_float2(x, y); }
-__device__ __forceinline__ float2 ld2(const float* p) { return *reinterpret_cast<const float2*>(p); }
 
 // Branch-free epilogue stores (round 5): a guarded global store (`if (ok) p[i] = v`) compiles to an exec-mask
 // branch per store -- 16 to 64 per unit, ~11-40 % of the conv's time in the epilogue knock-outs
@@ -465,7 +463,6 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
 #pragma unroll
                 for (int jj = 0; jj < PB; ++jj) {
                     const int j = PB * half + jj;
-                    const int co = 16 * (j >> 2) + 4 * kq + (j & 3);
                     float dzw[4][4];
                     float s_z = 0.f, s_x = 0.f;
 #pragma unroll

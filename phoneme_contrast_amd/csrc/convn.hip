@@ -223,6 +223,168 @@ __device__ __forceinline__ int64_t xcd_logical(int64_t nblocks) {
     return (bid & 7) * xcd_per(nblocks) + (bid >> 3);
 }
 
+// Epilogue of the forward / data-gradient kernels: planar NCHW float32 stores (columns = pixels:
+// 128-byte rows per MFMA output row), optionally the producer BN's backward sums (EP, mode 1) or the BN
+// forward partials (mode 0).  col[ni]: the flattened pixel of the lane's column (a valid pixel even where
+// valid[ni] is false), cnt_w: valid pixels among the wave's 32 WN columns, tn of ntile: the partials' tile.
+template <int MODE, int WM, int WN, bool EP>
+__device__ __forceinline__ void convn_epilogue(const ConvGArgs& a, const f32x16 (&acc)[WM][WN], char* smem, int64_t m0,
+                                               int64_t M, const int64_t (&col)[WN], const bool (&valid)[WN], int cnt_w,
+                                               int64_t ntile, int64_t tn, int64_t tm) {
+    constexpr int BM = 64 * WM;
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+    const int wave = tid >> 6, wr = wave >> 1, wc = wave & 1;
+    const int ph = a.par >> 1, pw = a.par & 1;
+    const int64_t OHW = (int64_t)a.OH * a.OW, IHW = (int64_t)a.IH * a.IW;
+    const int IHc = (a.IH - ph + 1) / 2, IWc = (a.IW - pw + 1) / 2;
+    const int64_t CHW = (int64_t)IHc * IWc;
+#pragma unroll
+    for (int ni = 0; ni < WN; ++ni) {
+        if (!valid[ni]) continue;
+        const int64_t cl = col[ni];
+        int64_t obase, ostride;
+        float* dst = a.out;
+        if (MODE == 0) {
+            const int64_t b = cl / OHW;
+            obase = b * a.cout * OHW + (cl - b * OHW);
+            ostride = OHW;
+        } else if (MODE == 1) {
+            const int64_t b = cl / IHW;
+            obase = b * a.cin * IHW + (cl - b * IHW);
+            ostride = IHW;
+        } else {
+            const int64_t b = cl / CHW, p = cl - b * CHW;
+            if (a.par_out) {  // dense class planes (contiguous 128-byte rows)
+                dst = a.par_out;
+                obase = b * a.cin * CHW + p;
+                ostride = CHW;
+            } else {
+                const int ihc = (int)(p / IWc), iwc = (int)(p - (int64_t)(p / IWc) * IWc);
+                obase = b * a.cin * IHW + (int64_t)(2 * ihc + ph) * a.IW + 2 * iwc + pw;
+                ostride = IHW;
+            }
+        }
+#pragma unroll
+        for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int64_t row = m0 + wr * 32 * WM + mi * 32 + acc_row(r, h);
+                if (row < M) {
+                    float* o = dst + obase + row * ostride;
+                    if (MODE != 0 && a.accumulate) *o += acc[mi][ni][r];
+                    else *o = acc[mi][ni][r];
+                }
+            }
+    }
+    if constexpr (MODE == 1 && EP) {
+        // backward partials of the BN + ReLU (+ Dropout2d) that produced this conv's input (replaces
+        // the bwd_prep pass over dx): producer values loaded for all of a row block first, per-row
+        // sums over the lanes by the transposed butterfly, the two pixel halves added
+        __syncthreads();  // operand stages consumed
+        float* red = reinterpret_cast<float*>(smem);                   // [2 (wc)][BM][2]
+        float4* cfl = reinterpret_cast<float4*>(red + 4 * BM);        // [BM]
+        if (tid < BM) cfl[tid] = a.ep_cf[min(m0 + tid, M - 1)];
+        __syncthreads();
+        const int64_t IHWe = (int64_t)a.IH * a.IW;
+        int64_t yb[WN], db[WN];
+#pragma unroll
+        for (int ni = 0; ni < WN; ++ni) {
+            const int64_t cc = col[ni], b = cc / IHWe;
+            yb[ni] = b * a.cin * IHWe + (cc - b * IHWe);
+            db[ni] = b * a.cin;
+        }
+#pragma unroll
+        for (int mi = 0; mi < WM; ++mi) {
+            // one pixel column block at a time (16 y and 16 dropout values live, not 2 x 32), summed in
+            // the same order as before (ni ascending)
+            float sg[16], sx[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sg[r] = sx[r] = 0.f;
+#pragma unroll
+            for (int ni = 0; ni < WN; ++ni) {
+                float yv[16], dv[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int64_t rc = min(m0 + wr * 32 * WM + mi * 32 + acc_row(r, h), M - 1);
+                    yv[r] = a.ep_y[yb[ni] + rc * IHWe];
+                    dv[r] = a.ep_drop ? a.ep_drop[db[ni] + rc] : 1.f;
+                }
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int rl = wr * 32 * WM + mi * 32 + acc_row(r, h);
+                    const float4 k = cfl[rl];
+                    const bool rok = m0 + rl < M;
+                    const float y = yv[r];
+                    const float g = (valid[ni] && rok && fmaf(y, k.x, k.y) > 0.f) ? acc[mi][ni][r] * dv[r] : 0.f;
+                    sg[r] += g;
+                    sx[r] = fmaf(g, (y - k.z) * k.w, sx[r]);
+                }
+            }
+            const float tg = xsum16(sg, l32), tx = xsum16(sx, l32);
+            if (!(l32 & 1)) {
+                float* d = red + (wc * BM + wr * 32 * WM + mi * 32 + acc_row(l32 >> 1, h)) * 2;
+                d[0] = tg;
+                d[1] = tx;
+            }
+        }
+        __syncthreads();
+        if (tid < BM && m0 + tid < M) {
+            a.ep_pg[(m0 + tid) * ntile + tn] = red[tid * 2] + red[(BM + tid) * 2];
+            a.ep_px[(m0 + tid) * ntile + tn] = red[tid * 2 + 1] + red[(BM + tid) * 2 + 1];
+        }
+    }
+    if (MODE == 0 && a.st_part0 != nullptr) {
+        // BN forward partials of the tile (replaces the statistics pass over out): per (wave, channel)
+        // Chan statistics of its valid pixels about the channel's first pixel in the wave (K, v_readlane),
+        // reduced over the lanes with the transposed butterfly, then the two pixel halves merged
+        __syncthreads();  // every wave is done with the operand stages: the LDS holds the exchange
+        float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+        for (int mi = 0; mi < WM; ++mi) {
+            float kv[16], s1[16], s2[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float k0 = readlane_f(acc[mi][0][r], 0), k1 = readlane_f(acc[mi][0][r], 32);
+                kv[r] = h ? k1 : k0;
+                s1[r] = 0.f;
+                s2[r] = 0.f;
+#pragma unroll
+                for (int ni = 0; ni < WN; ++ni)
+                    if (valid[ni]) {
+                        const float d = acc[mi][ni][r] - kv[r];
+                        s1[r] += d;
+                        s2[r] = fmaf(d, d, s2[r]);
+                    }
+            }
+            const float t1 = xsum16(s1, l32), t2 = xsum16(s2, l32), K = xsel16(kv, l32);
+            if (!(l32 & 1)) {
+                const float n = (float)cnt_w;
+                float* d = red + (wc * BM + wr * 32 * WM + mi * 32 + acc_row(l32 >> 1, h)) * 3;
+                d[0] = n;
+                d[1] = cnt_w ? K + t1 / n : 0.f;
+                d[2] = cnt_w ? fmaxf(t2 - t1 * t1 / n, 0.f) : 0.f;
+            }
+        }
+        __syncthreads();
+        if (tid < BM && m0 + tid < M) {
+            float n = 0.f, mean = 0.f, m2 = 0.f;
+#pragma unroll
+            for (int w = 0; w < 2; ++w) {
+                const float* d = red + (w * BM + tid) * 3;
+                if (d[0] > 0.f) {
+                    const float nt = n + d[0], delta = d[1] - mean;
+                    mean += delta * d[0] / nt;
+                    m2 += d[2] + delta * delta * n * d[0] / nt;
+                    n = nt;
+                }
+            }
+            a.st_part0[(m0 + tid) * ntile + tn] = n * mean;
+            a.st_part1[(m0 + tid) * ntile + tn] = m2;
+            if (tid == 0 && tm == 0) a.st_partn[tn] = n;
+        }
+    }
+}
+
 // EP (mode 1 only): the producer BN's backward sums in the epilogue (a separate instantiation: its
 // registers held every data-gradient launch at 1-2 waves per SIMD)
 template <int MODE, int WM, int KC, bool EP = false>
@@ -334,162 +496,176 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
         }
     }
 
-    // ---- epilogue: planar NCHW float32 (columns = pixels: 128-byte rows per MFMA output row)
+    // ---- epilogue (shared with the halo-staged kernel)
+    int64_t col[WN];
+    bool valid[WN];
 #pragma unroll
     for (int ni = 0; ni < WN; ++ni) {
-        const int64_t col = n0 + wc * 32 * WN + ni * 32 + l32;
-        if (col >= N) continue;
-        int64_t obase, ostride;
-        float* dst = a.out;
-        if (MODE == 0) {
-            const int64_t b = col / OHW;
-            obase = b * a.cout * OHW + (col - b * OHW);
-            ostride = OHW;
-        } else if (MODE == 1) {
-            const int64_t b = col / IHW;
-            obase = b * a.cin * IHW + (col - b * IHW);
-            ostride = IHW;
-        } else {
-            const int64_t b = col / CHW, p = col - b * CHW;
-            if (a.par_out) {  // dense class planes (contiguous 128-byte rows)
-                dst = a.par_out;
-                obase = b * a.cin * CHW + p;
-                ostride = CHW;
-            } else {
-                const int ihc = (int)(p / IWc), iwc = (int)(p - (int64_t)(p / IWc) * IWc);
-                obase = b * a.cin * IHW + (int64_t)(2 * ihc + ph) * a.IW + 2 * iwc + pw;
-                ostride = IHW;
-            }
-        }
-#pragma unroll
-        for (int mi = 0; mi < WM; ++mi)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int64_t row = m0 + wr * 32 * WM + mi * 32 + acc_row(r, h);
-                if (row < M) {
-                    float* o = dst + obase + row * ostride;
-                    if (MODE != 0 && a.accumulate) *o += acc[mi][ni][r];
-                    else *o = acc[mi][ni][r];
-                }
-            }
+        const int64_t c = n0 + wc * 32 * WN + ni * 32 + l32;
+        valid[ni] = c < N;
+        col[ni] = valid[ni] ? c : N - 1;
     }
-    if constexpr (MODE == 1 && EP) {
-        // backward partials of the BN + ReLU (+ Dropout2d) that produced this conv's input (replaces
-        // the bwd_prep pass over dx): producer values loaded for all of a row block first, per-row
-        // sums over the lanes by the transposed butterfly, the two pixel halves added
-        __syncthreads();  // operand stages consumed
-        float* red = reinterpret_cast<float*>(smem);                   // [2 (wc)][BM][2]
-        float4* cfl = reinterpret_cast<float4*>(red + 4 * BM);        // [BM]
-        if (tid < BM) cfl[tid] = a.ep_cf[min(m0 + tid, M - 1)];
-        __syncthreads();
-        const int64_t IHWe = (int64_t)a.IH * a.IW;
-        int64_t yb[WN], db[WN];
-        bool valid[WN];
+    const int64_t nw0 = n0 + wc * 32 * WN;
+    const int cnt_w = (int)max((int64_t)0, min((int64_t)(32 * WN), N - nw0));
+    convn_epilogue<MODE, WM, WN, EP>(a, acc, smem, m0, M, col, valid, cnt_w, (N + BN - 1) / BN, tn, tm);
+}
+
+// ------------------------------------------------------------------ halo-staged forward / data gradient
+// (round 5) Stride 1, 3x3, pad 1, modes 0 and 1.  The per-tap kernel above copies every pixel's 64-byte
+// operand run once per tap (nine times per channel chunk) and is bound by that L2 -> LDS stream on the
+// 64-channel layers.  Here a tile is TR x TW output pixels of one sample (N columns n = r TW + c, up to
+// 128), and per 32-channel chunk the (TR + 2) x (TW + 2) pixels of the padded image it touches are copied
+// once (the halo); the nine taps read their B operand at shifted halo positions.  The weights come per
+// tap row (three BM x 32 tiles); the next row's weights and, spread over the rows, the next chunk's halo
+// are copied under the current row's MFMAs (both double-buffered, one barrier per tap row).
+struct HaloGeo {
+    int TR, TW;     // tile rows / columns
+    int nsr, nsc;   // tiles per sample along rows / columns
+    int hp;         // halo pixels (TR + 2) (TW + 2) rounded up to 16 (one DMA instruction = 16 pixels)
+};
+
+template <int MODE, int WM, bool EP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void convn_halo_kernel(ConvGArgs a, HaloGeo g) {
+    constexpr int WN = 2, KC = 32, RB = 64;
+    constexpr int BM = 64 * WM;
+    constexpr int ABYTES = BM * RB;
+    extern __shared__ __attribute__((aligned(1024))) char smem[];  // [2][3 A tiles] [2][halo]
+    const unsigned lds0 = (unsigned)(uintptr_t)(lds_void*)smem;
+    const int HB = g.hp * RB;  // halo stage bytes
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), wr = wave >> 1, wc = wave & 1;
+    // image of the B operand: mode 0 the input x, mode 1 dy (both padded, channel count CK)
+    int CK, H, W, Hp, Wp;
+    int64_t M;
+    if (MODE == 0) { CK = a.cin; H = a.OH; W = a.OW; M = a.cout; }
+    else { CK = a.cout; H = a.IH; W = a.IW; M = a.cin; }
+    Hp = H + 2; Wp = W + 2;
+    const int64_t HW = (int64_t)H * W;
+    const int tps = g.nsr * g.nsc;
+    const int64_t mt = (M + BM - 1) / BM, ntile = (int64_t)a.B * tps;
+    const int64_t lid = xcd_logical(mt * ntile);
+    if (lid >= mt * ntile) return;  // (grid padded to a multiple of 8)
+    const int64_t tm = lid % mt, tn = lid / mt;
+    const int64_t m0 = tm * BM;
+    const int b = (int)(tn / tps), tl = (int)(tn - (int64_t)b * tps);
+    const int sr = tl / g.nsc, sc = tl - sr * g.nsc;
+    const int oh0 = sr * g.TR, ow0 = sc * g.TW;
+    const int HW2 = g.TW + 2;
+
+    // A rows (weights, as the per-tap kernel: logical run q of row r in slot q ^ ((r >> 2) & 3))
+    constexpr int RPI = 1024 / RB, NA = BM / RPI / 4;
+    const int lr = lane >> 2, ls = lane & 3;
+    const __bf16* asrc[NA];
 #pragma unroll
-        for (int ni = 0; ni < WN; ++ni) {
-            const int64_t col = n0 + wc * 32 * WN + ni * 32 + l32;
-            valid[ni] = col < N;
-            const int64_t cc = valid[ni] ? col : N - 1, b = cc / IHWe;
-            yb[ni] = b * a.cin * IHWe + (cc - b * IHWe);
-            db[ni] = b * a.cin;
-        }
-#pragma unroll
-        for (int mi = 0; mi < WM; ++mi) {
-            // one pixel column block at a time (16 y and 16 dropout values live, not 2 x 32), summed in
-            // the same order as before (ni ascending)
-            float sg[16], sx[16];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) sg[r] = sx[r] = 0.f;
-#pragma unroll
-            for (int ni = 0; ni < WN; ++ni) {
-                float yv[16], dv[16];
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int64_t rc = min(m0 + wr * 32 * WM + mi * 32 + acc_row(r, h), M - 1);
-                    yv[r] = a.ep_y[yb[ni] + rc * IHWe];
-                    dv[r] = a.ep_drop ? a.ep_drop[db[ni] + rc] : 1.f;
-                }
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int rl = wr * 32 * WM + mi * 32 + acc_row(r, h);
-                    const float4 k = cfl[rl];
-                    const bool rok = m0 + rl < M;
-                    const float y = yv[r];
-                    const float g = (valid[ni] && rok && fmaf(y, k.x, k.y) > 0.f) ? acc[mi][ni][r] * dv[r] : 0.f;
-                    sg[r] += g;
-                    sx[r] = fmaf(g, (y - k.z) * k.w, sx[r]);
-                }
-            }
-            const float tg = xsum16(sg, l32), tx = xsum16(sx, l32);
-            if (!(l32 & 1)) {
-                float* d = red + (wc * BM + wr * 32 * WM + mi * 32 + acc_row(l32 >> 1, h)) * 2;
-                d[0] = tg;
-                d[1] = tx;
-            }
-        }
-        __syncthreads();
-        if (tid < BM && m0 + tid < M) {
-            const int64_t ntile = (N + BN - 1) / BN;
-            a.ep_pg[(m0 + tid) * ntile + tn] = red[tid * 2] + red[(BM + tid) * 2];
-            a.ep_px[(m0 + tid) * ntile + tn] = red[tid * 2 + 1] + red[(BM + tid) * 2 + 1];
-        }
+    for (int j = 0; j < NA; ++j) {
+        const int r = RPI * (wave + 4 * j) + lr;
+        const int64_t row = m0 + r;
+        asrc[j] = static_cast<const __bf16*>(a.wpack) + (row < M ? row : 0) * (int64_t)(9 * CK) + 8 * (ls ^ ((r >> 2) & 3));
     }
-    if (MODE == 0 && a.st_part0 != nullptr) {
-        // BN forward partials of the tile (replaces the statistics pass over out): per (wave, channel)
-        // Chan statistics of its 64 pixels about the channel's first pixel in the wave (K, v_readlane),
-        // reduced over the lanes with the transposed butterfly, then the two pixel halves merged
-        __syncthreads();  // every wave is done with the operand stages: the LDS holds the exchange
-        float* red = reinterpret_cast<float*>(smem);
-        const int64_t nw0 = n0 + wc * 32 * WN;
-        const int cnt_w = (int)max((int64_t)0, min((int64_t)(32 * WN), N - nw0));
-        bool valid[WN];
+    // halo copies: instruction j (of g.hp / 16) covers halo pixels 16 j .. 16 j + 15, lane -> pixel
+    // 16 j + (lane >> 2), slot (lane & 3) holding run (lane & 3) ^ swz(pixel); wave w issues j = w, w + 4, ..
+    const int nhi = g.hp / 16;
+    const int nhw = (nhi - wave + 3) / 4;  // this wave's halo instructions per chunk (<= 7)
+    const __bf16* img = static_cast<const __bf16*>(MODE == 0 ? a.xn : a.dyn) + (int64_t)b * Hp * Wp * CK;
+    unsigned hoff[7];
 #pragma unroll
-        for (int ni = 0; ni < WN; ++ni) valid[ni] = nw0 + ni * 32 + l32 < N;
-#pragma unroll
-        for (int mi = 0; mi < WM; ++mi) {
-            float kv[16], s1[16], s2[16];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float k0 = readlane_f(acc[mi][0][r], 0), k1 = readlane_f(acc[mi][0][r], 32);
-                kv[r] = h ? k1 : k0;
-                s1[r] = 0.f;
-                s2[r] = 0.f;
-#pragma unroll
-                for (int ni = 0; ni < WN; ++ni)
-                    if (valid[ni]) {
-                        const float d = acc[mi][ni][r] - kv[r];
-                        s1[r] += d;
-                        s2[r] = fmaf(d, d, s2[r]);
-                    }
-            }
-            const float t1 = xsum16(s1, l32), t2 = xsum16(s2, l32), K = xsel16(kv, l32);
-            if (!(l32 & 1)) {
-                const float n = (float)cnt_w;
-                float* d = red + (wc * BM + wr * 32 * WM + mi * 32 + acc_row(l32 >> 1, h)) * 3;
-                d[0] = n;
-                d[1] = cnt_w ? K + t1 / n : 0.f;
-                d[2] = cnt_w ? fmaxf(t2 - t1 * t1 / n, 0.f) : 0.f;
-            }
-        }
-        __syncthreads();
-        if (tid < BM && m0 + tid < M) {
-            float n = 0.f, mean = 0.f, m2 = 0.f;
-#pragma unroll
-            for (int w = 0; w < 2; ++w) {
-                const float* d = red + (w * BM + tid) * 3;
-                if (d[0] > 0.f) {
-                    const float nt = n + d[0], delta = d[1] - mean;
-                    mean += delta * d[0] / nt;
-                    m2 += d[2] + delta * delta * n * d[0] / nt;
-                    n = nt;
-                }
-            }
-            const int64_t ntile = (N + BN - 1) / BN;
-            a.st_part0[(m0 + tid) * ntile + tn] = n * mean;
-            a.st_part1[(m0 + tid) * ntile + tn] = m2;
-            if (tid == 0 && tm == 0) a.st_partn[tn] = n;
-        }
+    for (int k = 0; k < 7; ++k) {
+        const int j = wave + 4 * k;
+        int px = 16 * j + (lane >> 2);
+        if (px >= (g.TR + 2) * HW2) px = 0;  // the stage's round-up slack: any readable run
+        const int i = px / HW2, jj = px - i * HW2;
+        const int hr = min(oh0 + i, Hp - 1), hc = min(ow0 + jj, Wp - 1);  // (clamped: feeds masked outputs only)
+        const int q = (lane & 3) ^ ((px >> 2) & 3);
+        hoff[k] = 2u * (unsigned)((hr * Wp + hc) * CK + 8 * q);
     }
+    // A of one tap row (taps 3 th .. 3 th + 2 of chunk cc = iteration it = 3 cc + th): three BM x 32 tiles
+    auto issue_a = [&](int it, int stage) {
+#pragma unroll
+        for (int tw = 0; tw < 3; ++tw) {
+            const unsigned base = lds0 + (unsigned)((3 * stage + tw) * ABYTES);
+#pragma unroll
+            for (int j = 0; j < NA; ++j)
+                dma16(asrc[j] + (int64_t)(3 * it + tw) * KC, base + (unsigned)(RPI * (wave + 4 * j) * RB));
+        }
+    };
+    auto issue_h = [&](int cc, int k, int stage) {  // this wave's k-th halo instruction of chunk cc
+        const __bf16* sb = img + cc * KC;
+        const unsigned m0l = lds0 + (unsigned)(6 * ABYTES + stage * HB + (wave + 4 * k) * 1024);
+        const unsigned m0u = __builtin_amdgcn_readfirstlane(m0l);
+        const uint64_t v = (uint64_t)(uintptr_t)sb;
+        const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+        const __bf16* su = (const __bf16*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+        asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" :: "v"(hoff[k]), "s"(su), "{m0}"(m0u) : "memory");
+    };
+    // the lane's columns: tile pixel n = wc 64 + ni 32 + l32 -> (r, c); halo pixel of tap (th, tw):
+    // mode 0 (r + th) HW2 + c + tw, mode 1 (r + 2 - th) HW2 + c + 2 - tw
+    int hpb[WN];
+    bool valid[WN];
+    int64_t col[WN];
+    int cnt_w = 0;
+#pragma unroll
+    for (int ni = 0; ni < WN; ++ni) {
+        const int n = wc * 32 * WN + ni * 32 + l32;
+        const int r = n / g.TW, c = n - r * g.TW;
+        valid[ni] = n < g.TR * g.TW && oh0 + r < H && ow0 + c < W;
+        const int rr = valid[ni] ? r : 0, cq = valid[ni] ? c : 0;
+        hpb[ni] = MODE == 0 ? rr * HW2 + cq : (rr + 2) * HW2 + cq + 2;
+        col[ni] = (int64_t)b * HW + (int64_t)(oh0 + rr) * W + ow0 + cq;
+        cnt_w += __popcll(__ballot(valid[ni]) & 0xffffffffull);
+    }
+
+    f32x16 acc[WM][WN];
+#pragma unroll
+    for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < WN; ++ni) acc[mi][ni] = f32x16{0.f};
+
+    // one barrier per tap row (3 taps, 12 WM MFMAs per wave); the next chunk's halo instructions are
+    // spread over the rows (<= 3 of the wave's per row), issued after the next A
+    const int ncc = CK / KC, nit = 3 * ncc;
+    issue_a(0, 0);
+#pragma unroll
+    for (int k = 0; k < 7; ++k)
+        if (k < nhw) issue_h(0, k, 0);
+    int th = 0, cc = 0;
+    for (int it = 0; it < nit; ++it) {
+        // A(it) must have landed; the halo instructions issued after it in the previous row may fly
+        const int hprev = (th >= 1 && cc + 1 < ncc) ? min(3, max(0, nhw - 3 * (th - 1))) : 0;
+        if (hprev >= 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        else if (hprev == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else if (hprev == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // A(it) (and at th 0 the chunk's halo) in LDS for every wave; the other A stage free
+        if (it + 1 < nit) issue_a(it + 1, (it + 1) & 1);
+        if (cc + 1 < ncc)
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                if (3 * th + k < nhw) issue_h(cc + 1, 3 * th + k, (cc + 1) & 1);
+        const char* hs = smem + 6 * ABYTES + (cc & 1) * HB;
+#pragma unroll
+        for (int tw = 0; tw < 3; ++tw) {
+            const char* as = smem + (3 * (it & 1) + tw) * ABYTES;
+            const int toff = MODE == 0 ? th * HW2 + tw : -(th * HW2 + tw);
+#pragma unroll
+            for (int ks = 0; ks < KC / 16; ++ks) {
+                bf16x8 av8[WM], bv8[WN];
+#pragma unroll
+                for (int mi = 0; mi < WM; ++mi)
+                    av8[mi] = *reinterpret_cast<const bf16x8*>(as + swz<KC>(wr * 32 * WM + mi * 32 + l32, 2 * ks + h));
+#pragma unroll
+                for (int ni = 0; ni < WN; ++ni) {
+                    const int px = hpb[ni] + toff;
+                    bv8[ni] = *reinterpret_cast<const bf16x8*>(hs + px * RB + 16 * ((2 * ks + h) ^ ((px >> 2) & 3)));
+                }
+#pragma unroll
+                for (int mi = 0; mi < WM; ++mi)
+#pragma unroll
+                    for (int ni = 0; ni < WN; ++ni) acc[mi][ni] = mfma_bf16(av8[mi], bv8[ni], acc[mi][ni]);
+            }
+        }
+        if (++th == 3) { th = 0; ++cc; }
+    }
+    convn_epilogue<MODE, WM, WN, EP>(a, acc, smem, m0, M, col, valid, cnt_w, ntile, tn, tm);
 }
 
 // ------------------------------------------------------------------ weight gradient
@@ -706,8 +882,50 @@ int launch_to_nhwc(NhwcArgs a, hipStream_t s) {
 // 14 % faster than 32 on the 256-channel layers) where the channel count allows
 static int convn_kc(int ck) { return ck % 64 == 0 ? 64 : 32; }
 
+// halo-staged tiling of an H x W image (stride-1 3x3 pad-1 modes 0 / 1): the fewest TR x TW tiles of at
+// most 128 pixels (ties: the smaller halo); used only when the tiles keep >= 90 % of their MFMA columns
+// busy (T = 200: 20 x 100 -> 16 tiles of 5 x 25, 10 x 50 -> 4, 5 x 25 -> 1).  PCX_CONVN_HALO=0: per-tap
+// copies everywhere.
+static bool convn_halo_tiles(int H, int W, HaloGeo* out) {
+    static const bool off = getenv("PCX_CONVN_HALO") && atoi(getenv("PCX_CONVN_HALO")) == 0;
+    if (off || H < 1 || W < 1) return false;
+    HaloGeo best{};
+    int64_t bt = -1, bh = 0;
+    for (int nsc = 1; nsc <= W; ++nsc) {
+        const int TW = (W + nsc - 1) / nsc;
+        if (TW > 128) continue;
+        if (nsc > 1 && (W + nsc - 2) / (nsc - 1) == TW) continue;  // same width as nsc - 1
+        const int TR0 = std::min(H, 128 / TW);
+        const int nsr = (H + TR0 - 1) / TR0, TR = (H + nsr - 1) / nsr;
+        const int64_t tiles = (int64_t)nsr * nsc, halo = (int64_t)(TR + 2) * (TW + 2);
+        if (bt < 0 || tiles < bt || (tiles == bt && halo < bh)) {
+            bt = tiles; bh = halo;
+            best.TR = TR; best.TW = TW; best.nsr = nsr; best.nsc = nsc;
+            best.hp = (int)((halo + 15) / 16 * 16);
+        }
+        if (TW < 8) break;
+    }
+    if (bt < 0 || (double)H * W < 0.9 * (double)bt * 128 || best.hp > 448) return false;
+    if (out) *out = best;
+    return true;
+}
+
+static bool convn_halo_ok(const ConvGArgs& a, HaloGeo* g) {
+    if ((a.mode != 0 && a.mode != 1) || a.stride != 1 || a.KH != 3 || a.KW != 3 || a.pad != 1) return false;
+    if (a.mode == 0 ? (a.OH != a.IH || a.OW != a.IW) : (a.IH != a.OH || a.IW != a.OW)) return false;
+    return convn_halo_tiles(a.mode == 0 ? a.OH : a.IH, a.mode == 0 ? a.OW : a.IW, g);
+}
+
 int64_t convn_stat_tiles(const ConvGArgs& a) {
+    HaloGeo g;
+    if (convn_halo_ok(a, &g)) return (int64_t)a.B * g.nsr * g.nsc;
     return ceil_div((int64_t)a.B * (a.mode == 1 ? (int64_t)a.IH * a.IW : (int64_t)a.OH * a.OW), 128);
+}
+
+int64_t convn_tile_bound(int B, int H, int W) {
+    HaloGeo g;
+    const int64_t flat = ceil_div((int64_t)B * H * W, 128);
+    return convn_halo_tiles(H, W, &g) ? std::max(flat, (int64_t)B * g.nsr * g.nsc) : flat;
 }
 
 bool convn_fits(const ConvGArgs& a) {
@@ -753,7 +971,9 @@ int launch_convn(const ConvGArgs& a, hipStream_t s) {
         if ((nth == 0 || ntw == 0) && a.accumulate) return PCX_OK;
     }
     const int ck = a.mode == 0 ? a.cin : a.cout;
-    const int kc = convn_kc(ck);
+    HaloGeo hg;
+    const bool halo = a.mode != 3 && convn_halo_ok(a, &hg);
+    const int kc = halo ? 32 : convn_kc(ck);
     {
         const int64_t K = (int64_t)nth * ntw * ck;
         if (M * K > 0) {
@@ -764,6 +984,27 @@ int launch_convn(const ConvGArgs& a, hipStream_t s) {
         }
     }
     const int wm = M >= 128 ? 2 : 1;
+    const bool ep = a.ep_pg != nullptr;
+    if (halo) {
+        PCX_CHECK_ARG(!a.st_part0 || (a.mode == 0 && a.st_part1 && a.st_partn), "convn: forward statistics need mode 0");
+        PCX_CHECK_ARG(!a.ep_pg || (a.mode == 1 && a.ep_px && a.ep_y && a.ep_cf && !a.accumulate),
+                      "convn: data-gradient BN sums need mode 1, y, cf and both partial arrays");
+        const int64_t nblocks = ceil_div(M, 64 * wm) * (int64_t)a.B * hg.nsr * hg.nsc;
+        PCX_CHECK_ARG(nblocks < ((int64_t)1 << 31), "convn: grid too large");
+        const size_t smem = (size_t)6 * 64 * wm * 64 + (size_t)2 * hg.hp * 64;
+        dim3 grid((unsigned)(8 * xcd_per(nblocks)));
+#define PCX_CH(MODE_, WM_, EP_)                                                                             \
+        if (a.mode == MODE_ && wm == WM_ && ep == EP_) {                                                    \
+            (void)hipFuncSetAttribute((const void*)convn_halo_kernel<MODE_, WM_, EP_>,                      \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);               \
+            convn_halo_kernel<MODE_, WM_, EP_><<<grid, 256, smem, s>>>(a, hg);                              \
+            PCX_LAUNCH_CHECK("convn_halo_kernel");                                                          \
+            return PCX_OK;                                                                                  \
+        }
+        PCX_CH(0, 1, false) PCX_CH(0, 2, false) PCX_CH(1, 1, false) PCX_CH(1, 2, false) PCX_CH(1, 1, true)
+        PCX_CH(1, 2, true)
+#undef PCX_CH
+    }
     constexpr int wn = 2;  // (128 x 256 tiles measured slower: 2 blocks per CU instead of 4)
     PCX_CHECK_ARG(!a.st_part0 || (a.mode == 0 && a.st_part1 && a.st_partn && convn_stat_tiles(a) == ceil_div(N, 64 * wn)),
                   "convn: forward statistics need mode 0 and all three partial arrays");
@@ -773,7 +1014,6 @@ int launch_convn(const ConvGArgs& a, hipStream_t s) {
     const int64_t nblocks = ceil_div(M, 64 * wm) * ceil_div(N, 64 * wn);
     PCX_CHECK_ARG(nblocks < ((int64_t)1 << 31), "convn: grid too large");
     dim3 grid((unsigned)(8 * xcd_per(nblocks)));
-    const bool ep = a.ep_pg != nullptr;
 #define PCX_CN(MODE_, WM_, KC_, EP_)                                                           \
     if (a.mode == MODE_ && wm == WM_ && kc == KC_ && ep == EP_) {                              \
         convn_kernel<MODE_, WM_, KC_, EP_><<<grid, 256, 0, s>>>(a);                            \

@@ -184,7 +184,7 @@ int build_deep(Plan& p) {
         k.an = k.d1n = k.m8 = 0;
         if (k.cn) {
             // the channel-last forward writes BN partials per 128-pixel tile (conv1, conv2, shortcut)
-            const size_t nt = (size_t)ceil_div((int64_t)B * k.Ho * k.Wo, 128);
+            const size_t nt = (size_t)convn_tile_bound(B, k.Ho, k.Wo);
             stat = std::max(stat, (size_t)2 * k.cout * nt + nt);
             k.an = p.carve("nhwc_a", nhwc_bytes(B, k.cin, k.Hi, k.Wi));
             k.d1n = p.carve("nhwc_d1", nhwc_bytes(B, k.cout, k.Ho, k.Wo));
@@ -795,7 +795,9 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
         const bool ep_sums = k.cn && getenv("PCX_NO_EPSUMS") == nullptr;
         ConvGArgs ep{};
         if (ep_sums) {
-            ns = ceil_div((int64_t)B * P2, 128);
+            ConvGArgs q{};  // conv2's data gradient: its epilogue tiles
+            q.mode = 1; q.B = B; q.IH = q.OH = k.Ho; q.IW = q.OW = k.Wo; q.KH = q.KW = 3; q.stride = 1; q.pad = 1;
+            ns = (int)convn_stat_tiles(q);
             ep.ep_y = c.w<float>(k.y1);
             ep.ep_cf = c.w<float4>(k.cf1);
             ep.ep_drop = d.residual ? dmask[i] : nullptr;

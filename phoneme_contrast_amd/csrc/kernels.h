@@ -443,6 +443,7 @@ size_t nhwc_bytes(int B, int C, int H, int W);
 int launch_to_nhwc(NhwcArgs a, hipStream_t s);
 bool convn_fits(const ConvGArgs& a);
 int64_t convn_stat_tiles(const ConvGArgs& a);  // mode 0: the st_part* tile count; mode 1: ep_p*
+int64_t convn_tile_bound(int B, int H, int W);  // upper bound of convn_stat_tiles at an H x W resolution
 int launch_convn(const ConvGArgs& a, hipStream_t s);
 size_t convg_bf16_wpack_bytes(int mode, int cin, int cout, int k);
 size_t convg_wpack_bytes(int mode, int cin, int cout, int k);  // fp32 packed weights (wpack)
