@@ -26,6 +26,12 @@ SHAPES = [  # B, cin, cout, IH, IW, k, stride, pad
     (2, 128, 256, 10, 50, 3, 2, 1),
     (2, 256, 256, 5, 25, 3, 1, 1),
     (2, 256, 512, 5, 25, 1, 2, 0),
+    # halo-staged stride-1 path (round 5, convn_halo_tiles): 4 x 2 tiles of 5 x 25 at 19 x 49 (a partial last
+    # tile row and column), 11 x 11 tiles at 11 x 21 (7 idle MFMA columns), 10 x 12 tiles at 10 x 47, 128 rows
+    (2, 64, 32, 19, 49, 3, 1, 1),
+    (2, 32, 32, 11, 21, 3, 1, 1),
+    (2, 32, 64, 10, 47, 3, 1, 1),
+    (2, 128, 128, 10, 47, 3, 1, 1),
     # Winograd conv (fp32): cnn_small layer shapes, odd width (T = 201), ragged odd height / width
     (3, 32, 32, 40, 201, 3, 1, 1),
     (2, 64, 32, 20, 100, 3, 1, 1),
