@@ -700,24 +700,27 @@ __device__ __forceinline__ float sp_relu(float y, float kx, float ky) { return f
 // 3-column windows from the two neighbouring lanes (shuffles) with the maxpool3_fwd tie rule (first
 // maximum in row-major window order; 255 when the maximum is <= 0).  Writes a0, the tap, y0 at the tap
 // and (optional) the padded NHWC bf16 image of a0 (borders included).  No block barrier after staging.
-__global__ __launch_bounds__(64, 2) void stem_pool_kernel(StemArgs a) {
+// (round 5) Two waves per block, one per cout half, sharing the staged x: half the LDS and half the staging
+// per wave (the one-wave blocks held ~2 waves per SIMD at 16.5 KB of LDS each).
+__global__ __launch_bounds__(128, 2) void stem_pool_kernel(StemArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     __bf16* xs = reinterpret_cast<__bf16*>(smem);
-    const int lane = threadIdx.x, h = lane >> 5, l = lane & 31;
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l = lane & 31;
+    const int mt = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int H = a.H, W = a.W, OH = a.OH, OW = a.OW, C = a.cout, ncb = sp_ncb(OW);
-    const int k = blockIdx.x % ncb, mt = (blockIdx.x / ncb) & 1, b = blockIdx.x / (2 * ncb);
+    const int k = blockIdx.x % ncb, b = blockIdx.x / ncb;
     const int c0 = 2 * SP_CB * k, CP = sp_copy(H);
     {  // stage x columns c0 - 4 .. c0 + 35 (zero outside the image) into the four shifted copies; the
        // loads of a batch are all issued before its LDS writes (one memory latency per batch)
         const auto rs_x = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.x + (int64_t)b * H * W), (short)0,
                                                             H * W * 4, 0x00020000);
-        constexpr int NB = 10;
+        constexpr int NB = 5;
         const int n = (H + 7) * 40;
-        for (int base = 0; base < n; base += NB * 64) {
+        for (int base = 0; base < n; base += NB * 128) {
             float v[NB];
 #pragma unroll
             for (int u = 0; u < NB; ++u) {
-                const int idx = base + u * 64 + lane;
+                const int idx = base + u * 128 + tid;
                 const int sr = idx / 40, lc = idx - sr * 40;
                 const int xr = sr - 3, xc = c0 - 4 + lc;
                 const bool ok = idx < n && xr >= 0 && xr < H && xc >= 0 && xc < W;  // else 0 (out-of-range offset)
@@ -725,7 +728,7 @@ __global__ __launch_bounds__(64, 2) void stem_pool_kernel(StemArgs a) {
             }
 #pragma unroll
             for (int u = 0; u < NB; ++u) {
-                const int idx = base + u * 64 + lane;
+                const int idx = base + u * 128 + tid;
                 if (idx < n) {
                     const int sr = idx / 40, lc = idx - sr * 40;
                     const __bf16 bv = (__bf16)v[u];
@@ -1653,7 +1656,7 @@ int launch_stem_pool(StemArgs a, hipStream_t s) {
     PCX_CHECK_ARG((int64_t)2 * a.B * sp_ncb(a.OW) < ((int64_t)1 << 31), "stem_pool: batch %d too large", a.B);
     const size_t sm = stem_pool_smem(a.H, a.W);
     (void)hipFuncSetAttribute((const void*)stem_pool_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-    stem_pool_kernel<<<(unsigned)(2 * a.B * sp_ncb(a.OW)), 64, sm, s>>>(a);
+    stem_pool_kernel<<<(unsigned)(a.B * sp_ncb(a.OW)), 128, sm, s>>>(a);
     PCX_LAUNCH_CHECK("stem_pool_kernel");
     return PCX_OK;
 }
