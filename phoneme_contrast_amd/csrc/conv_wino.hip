@@ -805,12 +805,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
 #pragma unroll
                     for (int q = 0; q < 4; ++q)
                         av[mi][q] = *reinterpret_cast<const f32x4*>(bw + (((cl * 4 + q) * 32) + 16 * mi + n) * 4);
+                const f2 st = PRO != PRO_RAW ? *reinterpret_cast<const f2*>(cft + 2 * (c0 + cl)) : f2{1.f, 0.f};
+                // every LDS read of the K-step is issued before its arithmetic (one exposed latency per K-step,
+                // covered by the SIMD's other wave, instead of the scheduler's waits between MFMAs: -1 to -3 %,
+                // profiles/r5_wino_sched.txt)
+                __builtin_amdgcn_sched_barrier(0);
 #if defined(WINO_KO) && (WINO_KO & 8)  // analysis builds only: no BN + ReLU prologue arithmetic
                 if (false) {
 #else
                 if (PRO != PRO_RAW) {
 #endif
-                    const f2 st = *reinterpret_cast<const f2*>(cft + 2 * (c0 + cl));
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
 #pragma unroll
