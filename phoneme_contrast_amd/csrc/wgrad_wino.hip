@@ -54,16 +54,22 @@ template <int V>
 __device__ __forceinline__ vecf<V> bload(__amdgpu_buffer_rsrc_t r, int voff) {
     if constexpr (V == 4)
         return __builtin_bit_cast(vecf<4>, __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0));
-    else
+    else if constexpr (V == 2)
         return __builtin_bit_cast(vecf<2>, __builtin_amdgcn_raw_buffer_load_b64(r, voff, 0, 0));
+    else
+        return vecf<1>{__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, 0, 0))};
 }
 
 template <int V>
 __device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int voff, vecf<V> v) {
     if constexpr (V == 4)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, voff, 0, 0);
-    else
+    else if constexpr (V == 2)
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, voff, 0, 0);
+    else {
+        const float f = v.x;  // (a named copy: no bit_cast of a vector-lane lvalue)
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, f), r, voff, 0, 0);
+    }
 }
 
 // single v_fma_f32 (no SLP packing next to the stores of the same registers: see wgrad_s.hip)
@@ -276,9 +282,11 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
                     d[0] = v[0];
                     *reinterpret_cast<f2*>(d + 1) = f2{v[1], v[2]};
                     d[3] = v[3];
-                } else {
+                } else if constexpr (V == 2) {
                     d[0] = v[0];
                     d[1] = v[1];
+                } else {
+                    d[0] = v[0];
                 }
             }
         };
@@ -293,8 +301,12 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
                 const bool ok = (dm >> m) & 1;
                 const vecf<V> v = dzv[m];
                 float* d = dyl + dlb + (m / NIR) * 32 * DCS + 8 * V * (m % NIR);
-                *reinterpret_cast<f2*>(d) = f2{v[0], v[1]};
-                if constexpr (V == 4) *reinterpret_cast<f2*>(d + 2) = f2{v[2], v[3]};
+                if constexpr (V == 1) {
+                    d[0] = v[0];
+                } else {
+                    *reinterpret_cast<f2*>(d) = f2{v[0], v[1]};
+                    if constexpr (V == 4) *reinterpret_cast<f2*>(d + 2) = f2{v[2], v[3]};
+                }
                 if (write_dy) bstore<V>(rdo, ok ? 4 * (dgo(m) + db) : OOB, v);
             }
             store_x(st, xv);
@@ -454,9 +466,13 @@ int smallest_2odd(int n) {  // smallest m >= n with m = 2 * odd
 
 bool wgrad_wino_geometry(int B, int H, int W, int cin, int cout, WinoWgradArgs* a) {
     if (cin % 32 || cout % 32 || H < 1 || W < 4) return false;
-    const int V = W % 4 == 0 ? 4 : W % 2 == 0 ? 2 : 0;
-    if (!V) return false;
+    // staging vector: 16 / 8 bytes where the width allows, single floats at odd widths (round 5: the narrow
+    // 5 x 25 / 3 x 13 blocks of cnn_deep; the last tile column is half outside and stages zeros)
+    const int V = W % 4 == 0 ? 4 : W % 2 == 0 ? 2 : 1;
     const int TC = (W + 1) / 2;
+    // odd widths only where the 2 x 2 tiles cover the image well: 5 x 25 (0.80 of the tiles' outputs real)
+    // 5.77 vs 6.05 ms on the row-window kernel; 3 x 13 (0.70) 10.8 vs 8.7 ms (profiles/r5_wgrad_wino_odd.txt)
+    if (V == 1 && (double)H * W < 0.75 * 4.0 * ((H + 1) / 2) * TC) return false;
     int nseg = ceil_div(TC, 50);
     int S = ceil_div(TC, nseg);
     if (nseg > 1) S = (S + 1) & ~1;  // strip starts 2 t0 on a 16-byte boundary (V = 4)
@@ -518,6 +534,8 @@ int launch_wgrad_wino(int pro, WinoWgradArgs a, hipStream_t s) {
     PCX_WW(PRO_BNRELU, 4, false)
     PCX_WW(PRO_BNRELU, 2, false)
     PCX_WW(PRO_BNRELU, 4, true)  // cnn_small layer 4 (behind layer 5's pool)
+    PCX_WW(PRO_RAW, 1, false)
+    PCX_WW(PRO_BNRELU, 1, false)
 #undef PCX_WW
     set_error("wgrad_wino: unsupported combination (pro %d, vec %d)", pro, a.V);
     return PCX_EINVAL;

@@ -79,13 +79,19 @@ WW = os.path.join(ROOT, "tools", "ww_bench")
 WW_CASES = [  # H, W, cin, cout, B, reps, prologue, pooled dz
     (20, 100, 64, 64, 48, 1, 1, 1),  # cnn_small layer 4 behind layer 5's pool: dz rebuilt from the selection
     (20, 100, 64, 64, 48, 1, 1, 0),
+    # odd widths (single-float staging, round 5) against the 32x32 row-window kernel: cnn_deep block 3 at
+    # T = 200, an odd batch with the BN + ReLU prologue, a 7-row image (4 tile rows)
+    (5, 25, 256, 256, 24, 1, 0, 0),
+    (5, 25, 64, 96, 23, 1, 1, 0),
+    (7, 27, 32, 32, 5, 1, 1, 0),
 ]
 
 
 @pytest.mark.parametrize("case", WW_CASES)
 def test_winograd_wgrad_pooled_dz_matches_pixel_stream(case):
-    """wgrad_wino reading dz as a pooled gradient + window selection (EPI_BWD_POOLSELP's output) against
-    the pixel-stream weight gradient on the expanded full-resolution dz (dW within 1e-4, dy exact)."""
+    """wgrad_wino reading dz as a pooled gradient + window selection (EPI_BWD_POOLSELP's output), or at odd
+    widths, against the pixel-stream (narrow rows: row-window) weight gradient on the same dz (dW within 1e-4,
+    dy exact)."""
     assert os.path.exists(WW), "tools/ww_bench missing: run make"
     r = subprocess.run([WW] + [str(v) for v in case], capture_output=True, text=True, timeout=120)
     print(r.stdout)

@@ -80,7 +80,9 @@ int main(int argc, char** argv) {
     (void)hipMemset(dy1, 0, ny * 4); (void)hipMemset(dy2, 0, ny * 4);
     pcx::WgradArgs s{};
     pcx::WinoWgradArgs w{};
-    if (!pcx::wgrad_s_geometry(B, H, W, cin, cout, &s)) { printf("no wgrad_s geometry\n"); return 1; }
+    // reference: the pixel-stream kernel, or at narrow widths the 32 x 32 row-window kernel
+    const bool w32 = !pcx::wgrad_s_geometry(B, H, W, cin, cout, &s);
+    if (w32 && !pcx::wgrad_w32_geometry(B, H, W, cin, cout, &s)) { printf("no reference geometry\n"); return 1; }
     if (!pcx::wgrad_wino_geometry(B, H, W, cin, cout, &w)) { printf("no wgrad_wino geometry\n"); return 1; }
     size_t np = std::max((size_t)s.nslice * nw, (size_t)w.nslice * cout * cin * 16);
     (void)hipMalloc(&part, np * 4);
@@ -90,8 +92,8 @@ int main(int argc, char** argv) {
     w.B = B; w.H = H; w.W = W; w.cin = cin; w.cout = cout;
     w.dz = pd ? nullptr : dz; w.dzpool = dpool; w.parg = sel; w.y = y; w.cf_dy = (const float4*)cfd; w.src = x; w.cf_x = (const float4*)cfx;
     w.part = part; w.dy_out = dy2;
-    float ms_s = timeit<pcx::WgradArgs>(pcx::launch_wgrad_s, pro, s, reps);
-    pcx::launch_wgrad_s(pro, s, 0); pcx::launch_sum_slices(part, s.nslice, nw, g1, 0);
+    float ms_s = timeit<pcx::WgradArgs>(w32 ? pcx::launch_wgrad_w32 : pcx::launch_wgrad_s, pro, s, reps);
+    (w32 ? pcx::launch_wgrad_w32 : pcx::launch_wgrad_s)(pro, s, 0); pcx::launch_sum_slices(part, s.nslice, nw, g1, 0);
     float ms_w = timeit<pcx::WinoWgradArgs>(pcx::launch_wgrad_wino, pro, w, reps);
     pcx::launch_wgrad_wino(pro, w, 0); pcx::launch_wgrad_wino_reduce(part, w.nslice, cout, cin, g2, 0);
     hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
@@ -113,7 +115,7 @@ int main(int argc, char** argv) {
     }
     for (size_t i = 0; i < ny; ++i) { dmax = std::max(dmax, (double)std::fabs(d1[i] - d2[i])); dyabs = std::max(dyabs, (double)std::fabs(d1[i])); }
     const double fl = 2.0 * B * H * W * cin * cout * 9;
-    printf("%sH%d W%d %d->%d pro%d B%d | stream: %.3f ms (%.3f of 157.3 TF) | wino S %d V %d slices %d: %.3f ms (%.3f alg, "
+    printf("%sH%d W%d %d->%d pro%d B%d | reference: %.3f ms (%.3f of 157.3 TF) | wino S %d V %d slices %d: %.3f ms (%.3f alg, "
            "%.3f exec) + reduce %.3f ms | dW rel %.2e (worst [%d] %g vs %g) dy diff %.2e of %.2e\n",
            pd ? "(pooled dz) " : "", H, W, cin, cout, pro, B, ms_s, fl / ms_s / 1e9 / 157.3, w.S, w.V, w.nslice, ms_w, fl / ms_w / 1e9 / 157.3,
            fl * 4 / 9 / ms_w / 1e9 / 157.3, ms_r, emax / gmax, worst, h2[worst], h1[worst], dmax, dyabs);
