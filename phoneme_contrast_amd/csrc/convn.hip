@@ -227,13 +227,14 @@ __device__ __forceinline__ int64_t xcd_logical(int64_t nblocks) {
 // 128-byte rows per MFMA output row), optionally the producer BN's backward sums (EP, mode 1) or the BN
 // forward partials (mode 0).  col[ni]: the flattened pixel of the lane's column (a valid pixel even where
 // valid[ni] is false), cnt_w: valid pixels among the wave's 32 WN columns, tn of ntile: the partials' tile.
-template <int MODE, int WM, int WN, bool EP>
+template <int MODE, int WM, int WN, bool EP, int NWC = 2>
 __device__ __forceinline__ void convn_epilogue(const ConvGArgs& a, const f32x16 (&acc)[WM][WN], char* smem, int64_t m0,
                                                int64_t M, const int64_t (&col)[WN], const bool (&valid)[WN], int cnt_w,
                                                int64_t ntile, int64_t tn, int64_t tm) {
+    // (NWC wave columns of 32 WN pixels, two wave rows of 32 WM output rows)
     constexpr int BM = 64 * WM;
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
-    const int wave = tid >> 6, wr = wave >> 1, wc = wave & 1;
+    const int wave = tid >> 6, wr = wave / NWC, wc = wave % NWC;
     const int ph = a.par >> 1, pw = a.par & 1;
     const int64_t OHW = (int64_t)a.OH * a.OW, IHW = (int64_t)a.IH * a.IW;
     const int IHc = (a.IH - ph + 1) / 2, IWc = (a.IW - pw + 1) / 2;
@@ -281,8 +282,8 @@ __device__ __forceinline__ void convn_epilogue(const ConvGArgs& a, const f32x16 
         // the bwd_prep pass over dx): producer values loaded for all of a row block first, per-row
         // sums over the lanes by the transposed butterfly, the two pixel halves added
         __syncthreads();  // operand stages consumed
-        float* red = reinterpret_cast<float*>(smem);                   // [2 (wc)][BM][2]
-        float4* cfl = reinterpret_cast<float4*>(red + 4 * BM);        // [BM]
+        float* red = reinterpret_cast<float*>(smem);                   // [NWC (wc)][BM][2]
+        float4* cfl = reinterpret_cast<float4*>(red + 2 * NWC * BM);  // [BM]
         if (tid < BM) cfl[tid] = a.ep_cf[min(m0 + tid, M - 1)];
         __syncthreads();
         const int64_t IHWe = (int64_t)a.IH * a.IW;
@@ -329,8 +330,14 @@ __device__ __forceinline__ void convn_epilogue(const ConvGArgs& a, const f32x16 
         }
         __syncthreads();
         if (tid < BM && m0 + tid < M) {
-            a.ep_pg[(m0 + tid) * ntile + tn] = red[tid * 2] + red[(BM + tid) * 2];
-            a.ep_px[(m0 + tid) * ntile + tn] = red[tid * 2 + 1] + red[(BM + tid) * 2 + 1];
+            float pg = 0.f, px = 0.f;
+#pragma unroll
+            for (int w = 0; w < NWC; ++w) {
+                pg += red[(w * BM + tid) * 2];
+                px += red[(w * BM + tid) * 2 + 1];
+            }
+            a.ep_pg[(m0 + tid) * ntile + tn] = pg;
+            a.ep_px[(m0 + tid) * ntile + tn] = px;
         }
     }
     if (MODE == 0 && a.st_part0 != nullptr) {
@@ -369,7 +376,7 @@ __device__ __forceinline__ void convn_epilogue(const ConvGArgs& a, const f32x16 
         if (tid < BM && m0 + tid < M) {
             float n = 0.f, mean = 0.f, m2 = 0.f;
 #pragma unroll
-            for (int w = 0; w < 2; ++w) {
+            for (int w = 0; w < NWC; ++w) {
                 const float* d = red + (w * BM + tid) * 3;
                 if (d[0] > 0.f) {
                     const float nt = n + d[0], delta = d[1] - mean;
@@ -524,16 +531,17 @@ struct HaloGeo {
     int hp;         // halo pixels (TR + 2) (TW + 2) rounded up to 16 (one DMA instruction = 16 pixels)
 };
 
-template <int MODE, int WM, bool EP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void convn_halo_kernel(ConvGArgs a, HaloGeo g) {
-    constexpr int WN = 2, KC = 32, RB = 64;
+template <int MODE, int WM, bool EP, int NW = 4>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) void convn_halo_kernel(ConvGArgs a, HaloGeo g) {
+    // NW waves: two wave rows (32 WM output rows each) x NW / 2 wave columns (64 pixels each)
+    constexpr int WN = 2, KC = 32, RB = 64, NWC = NW / 2;
     constexpr int BM = 64 * WM;
     constexpr int ABYTES = BM * RB;
     extern __shared__ __attribute__((aligned(1024))) char smem[];  // [2][3 A tiles] [2][halo]
     const unsigned lds0 = (unsigned)(uintptr_t)(lds_void*)smem;
     const int HB = g.hp * RB;  // halo stage bytes
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), wr = wave >> 1, wc = wave & 1;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), wr = wave / NWC, wc = wave % NWC;
     // image of the B operand: mode 0 the input x, mode 1 dy (both padded, channel count CK)
     int CK, H, W, Hp, Wp;
     int64_t M;
@@ -553,24 +561,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     const int HW2 = g.TW + 2;
 
     // A rows (weights, as the per-tap kernel: logical run q of row r in slot q ^ ((r >> 2) & 3))
-    constexpr int RPI = 1024 / RB, NA = BM / RPI / 4;
+    constexpr int RPI = 1024 / RB, NAI = BM / RPI, NA = (NAI + NW - 1) / NW;  // A copy instructions: tile, wave
     const int lr = lane >> 2, ls = lane & 3;
     const __bf16* asrc[NA];
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
-        const int r = RPI * (wave + 4 * j) + lr;
+        const int r = RPI * (wave + NW * j) + lr;
         const int64_t row = m0 + r;
-        asrc[j] = static_cast<const __bf16*>(a.wpack) + (row < M ? row : 0) * (int64_t)(9 * CK) + 8 * (ls ^ ((r >> 2) & 3));
+        asrc[j] = static_cast<const __bf16*>(a.wpack) + (row < M && r < BM ? row : 0) * (int64_t)(9 * CK) + 8 * (ls ^ ((r >> 2) & 3));
     }
     // halo copies: instruction j (of g.hp / 16) covers halo pixels 16 j .. 16 j + 15, lane -> pixel
     // 16 j + (lane >> 2), slot (lane & 3) holding run (lane & 3) ^ swz(pixel); wave w issues j = w, w + 4, ..
     const int nhi = g.hp / 16;
-    const int nhw = (nhi - wave + 3) / 4;  // this wave's halo instructions per chunk (<= 7)
+    const int nhw = (nhi - wave + NW - 1) / NW;  // this wave's halo instructions per chunk (<= 7)
     const __bf16* img = static_cast<const __bf16*>(MODE == 0 ? a.xn : a.dyn) + (int64_t)b * Hp * Wp * CK;
     unsigned hoff[7];
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
-        const int j = wave + 4 * k;
+        const int j = wave + NW * k;
         int px = 16 * j + (lane >> 2);
         if (px >= (g.TR + 2) * HW2) px = 0;  // the stage's round-up slack: any readable run
         const int i = px / HW2, jj = px - i * HW2;
@@ -585,12 +593,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
             const unsigned base = lds0 + (unsigned)((3 * stage + tw) * ABYTES);
 #pragma unroll
             for (int j = 0; j < NA; ++j)
-                dma16(asrc[j] + (int64_t)(3 * it + tw) * KC, base + (unsigned)(RPI * (wave + 4 * j) * RB));
+                if (NAI % NW == 0 || wave + NW * j < NAI)
+                    dma16(asrc[j] + (int64_t)(3 * it + tw) * KC, base + (unsigned)(RPI * (wave + NW * j) * RB));
         }
     };
     auto issue_h = [&](int cc, int k, int stage) {  // this wave's k-th halo instruction of chunk cc
         const __bf16* sb = img + cc * KC;
-        const unsigned m0l = lds0 + (unsigned)(6 * ABYTES + stage * HB + (wave + 4 * k) * 1024);
+        const unsigned m0l = lds0 + (unsigned)(6 * ABYTES + stage * HB + (wave + NW * k) * 1024);
         const unsigned m0u = __builtin_amdgcn_readfirstlane(m0l);
         const uint64_t v = (uint64_t)(uintptr_t)sb;
         const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
@@ -665,7 +674,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
         }
         if (++th == 3) { th = 0; ++cc; }
     }
-    convn_epilogue<MODE, WM, WN, EP>(a, acc, smem, m0, M, col, valid, cnt_w, ntile, tn, tm);
+    convn_epilogue<MODE, WM, WN, EP, NWC>(a, acc, smem, m0, M, col, valid, cnt_w, ntile, tn, tm);
 }
 
 // ------------------------------------------------------------------ weight gradient
@@ -883,19 +892,19 @@ int launch_to_nhwc(NhwcArgs a, hipStream_t s) {
 static int convn_kc(int ck) { return ck % 64 == 0 ? 64 : 32; }
 
 // halo-staged tiling of an H x W image (stride-1 3x3 pad-1 modes 0 / 1): the fewest TR x TW tiles of at
-// most 128 pixels (ties: the smaller halo); used only when the tiles keep >= 90 % of their MFMA columns
-// busy (T = 200: 20 x 100 -> 16 tiles of 5 x 25, 10 x 50 -> 4, 5 x 25 -> 1).  PCX_CONVN_HALO=0: per-tap
-// copies everywhere.
-static bool convn_halo_tiles(int H, int W, HaloGeo* out) {
+// most maxpx pixels (ties: the smaller halo); used only when the tiles keep >= 90 % of their MFMA columns
+// busy (T = 200, 128 pixels: 20 x 100 -> 16 tiles of 5 x 25, 10 x 50 -> 4, 5 x 25 -> 1; 256 pixels:
+// 20 x 100 -> 8 of 10 x 25).  PCX_CONVN_HALO=0: per-tap copies everywhere.
+static bool convn_halo_tiles(int H, int W, int maxpx, HaloGeo* out) {
     static const bool off = getenv("PCX_CONVN_HALO") && atoi(getenv("PCX_CONVN_HALO")) == 0;
     if (off || H < 1 || W < 1) return false;
     HaloGeo best{};
     int64_t bt = -1, bh = 0;
     for (int nsc = 1; nsc <= W; ++nsc) {
         const int TW = (W + nsc - 1) / nsc;
-        if (TW > 128) continue;
+        if (TW > maxpx) continue;
         if (nsc > 1 && (W + nsc - 2) / (nsc - 1) == TW) continue;  // same width as nsc - 1
-        const int TR0 = std::min(H, 128 / TW);
+        const int TR0 = std::min(H, maxpx / TW);
         const int nsr = (H + TR0 - 1) / TR0, TR = (H + nsr - 1) / nsr;
         const int64_t tiles = (int64_t)nsr * nsc, halo = (int64_t)(TR + 2) * (TW + 2);
         if (bt < 0 || tiles < bt || (tiles == bt && halo < bh)) {
@@ -905,27 +914,41 @@ static bool convn_halo_tiles(int H, int W, HaloGeo* out) {
         }
         if (TW < 8) break;
     }
-    if (bt < 0 || (double)H * W < 0.9 * (double)bt * 128 || best.hp > 448) return false;
+    if (bt < 0 || (double)H * W < 0.9 * (double)bt * maxpx || best.hp > 7 * 16 * (maxpx / 32)) return false;
     if (out) *out = best;
     return true;
 }
 
-static bool convn_halo_ok(const ConvGArgs& a, HaloGeo* g) {
+// 8-wave blocks (256-pixel tiles: two blocks of 8 waves per CU instead of three of 4) for the 64-row
+// forward and the plain data gradient; 4 waves elsewhere (the BN-sum epilogue's registers, 128 rows' LDS)
+static int convn_halo_waves(const ConvGArgs& a) {
+    static const int env = getenv("PCX_CONVN_NW") ? atoi(getenv("PCX_CONVN_NW")) : 0;
+    const int64_t M = a.mode == 0 ? a.cout : a.cin;
+    const bool eight = M <= 64 && (a.mode == 0 || !a.ep_pg);
+    if (env == 4 || env == 8) return eight ? env : 4;
+    return eight ? 8 : 4;
+}
+
+// mode 1 here is always the BN-sum context (convn_stat_tiles): 4 waves
+static bool convn_halo_ok(const ConvGArgs& a, HaloGeo* g, int nw = 4) {
     if ((a.mode != 0 && a.mode != 1) || a.stride != 1 || a.KH != 3 || a.KW != 3 || a.pad != 1) return false;
     if (a.mode == 0 ? (a.OH != a.IH || a.OW != a.IW) : (a.IH != a.OH || a.IW != a.OW)) return false;
-    return convn_halo_tiles(a.mode == 0 ? a.OH : a.IH, a.mode == 0 ? a.OW : a.IW, g);
+    return convn_halo_tiles(a.mode == 0 ? a.OH : a.IH, a.mode == 0 ? a.OW : a.IW, 32 * nw, g);
 }
 
 int64_t convn_stat_tiles(const ConvGArgs& a) {
     HaloGeo g;
-    if (convn_halo_ok(a, &g)) return (int64_t)a.B * g.nsr * g.nsc;
+    const int nw = a.mode == 0 ? convn_halo_waves(a) : 4;
+    if (convn_halo_ok(a, &g, nw)) return (int64_t)a.B * g.nsr * g.nsc;
     return ceil_div((int64_t)a.B * (a.mode == 1 ? (int64_t)a.IH * a.IW : (int64_t)a.OH * a.OW), 128);
 }
 
 int64_t convn_tile_bound(int B, int H, int W) {
     HaloGeo g;
-    const int64_t flat = ceil_div((int64_t)B * H * W, 128);
-    return convn_halo_tiles(H, W, &g) ? std::max(flat, (int64_t)B * g.nsr * g.nsc) : flat;
+    int64_t t = ceil_div((int64_t)B * H * W, 128);
+    for (int px : {128, 256})
+        if (convn_halo_tiles(H, W, px, &g)) t = std::max(t, (int64_t)B * g.nsr * g.nsc);
+    return t;
 }
 
 bool convn_fits(const ConvGArgs& a) {
@@ -972,7 +995,8 @@ int launch_convn(const ConvGArgs& a, hipStream_t s) {
     }
     const int ck = a.mode == 0 ? a.cin : a.cout;
     HaloGeo hg;
-    const bool halo = a.mode != 3 && convn_halo_ok(a, &hg);
+    const int hnw = a.mode == 3 ? 4 : convn_halo_waves(a);
+    const bool halo = a.mode != 3 && convn_halo_ok(a, &hg, hnw);
     const int kc = halo ? 32 : convn_kc(ck);
     {
         const int64_t K = (int64_t)nth * ntw * ck;
@@ -993,16 +1017,16 @@ int launch_convn(const ConvGArgs& a, hipStream_t s) {
         PCX_CHECK_ARG(nblocks < ((int64_t)1 << 31), "convn: grid too large");
         const size_t smem = (size_t)6 * 64 * wm * 64 + (size_t)2 * hg.hp * 64;
         dim3 grid((unsigned)(8 * xcd_per(nblocks)));
-#define PCX_CH(MODE_, WM_, EP_)                                                                             \
-        if (a.mode == MODE_ && wm == WM_ && ep == EP_) {                                                    \
-            (void)hipFuncSetAttribute((const void*)convn_halo_kernel<MODE_, WM_, EP_>,                      \
+#define PCX_CH(MODE_, WM_, EP_, NW_)                                                                        \
+        if (a.mode == MODE_ && wm == WM_ && ep == EP_ && hnw == NW_) {                                      \
+            (void)hipFuncSetAttribute((const void*)convn_halo_kernel<MODE_, WM_, EP_, NW_>,                 \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);               \
-            convn_halo_kernel<MODE_, WM_, EP_><<<grid, 256, smem, s>>>(a, hg);                              \
+            convn_halo_kernel<MODE_, WM_, EP_, NW_><<<grid, 64 * NW_, smem, s>>>(a, hg);                    \
             PCX_LAUNCH_CHECK("convn_halo_kernel");                                                          \
             return PCX_OK;                                                                                  \
         }
-        PCX_CH(0, 1, false) PCX_CH(0, 2, false) PCX_CH(1, 1, false) PCX_CH(1, 2, false) PCX_CH(1, 1, true)
-        PCX_CH(1, 2, true)
+        PCX_CH(0, 1, false, 4) PCX_CH(0, 2, false, 4) PCX_CH(1, 1, false, 4) PCX_CH(1, 2, false, 4)
+        PCX_CH(1, 1, true, 4) PCX_CH(1, 2, true, 4) PCX_CH(0, 1, false, 8) PCX_CH(1, 1, false, 8)
 #undef PCX_CH
     }
     constexpr int wn = 2;  // (128 x 256 tiles measured slower: 2 blocks per CU instead of 4)
