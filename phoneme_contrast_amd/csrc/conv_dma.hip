@@ -339,7 +339,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dma_occ(WM)
 // One block per group of PPB channel planes; thread = 4 pooled outputs of one row (8 input columns
 // of two rows).  VEC4: source rows 16-byte aligned (Ws % 4 == 0) -> four 16-byte loads per thread;
 // otherwise paired / scalar loads.  32-bit index math only.
-template <int VEC>
+template <int VEC, int NI>
 __global__ __launch_bounds__(256) void bn_relu_pool_kernel(const float* __restrict__ y, const float4* __restrict__ cf,
                                                            const float* __restrict__ drop, float* __restrict__ x,
                                                            int nplanes, int C, int Hs, int Ws, int Hp, int Wp, int ppb,
@@ -347,75 +347,90 @@ __global__ __launch_bounds__(256) void bn_relu_pool_kernel(const float* __restri
     const int Wq = (Wp + 3) / 4, nqp = Hp * Wq;
     const int pbase = blockIdx.x * ppb;
     const int tot = min(ppb, nplanes - pbase) * nqp;
-    for (int t = threadIdx.x; t < tot; t += blockDim.x) {
-        const int pl = t / nqp, rem = t - pl * nqp;
-        const int hp = rem / Wq, q = rem - hp * Wq;
-        const int bc = pbase + pl;
-        const float4 k = cf[bc % C];
-        const float d = drop ? drop[bc] : 1.f;
-        const float* s0 = y + ((int64_t)bc * Hs + 2 * hp) * Ws + 8 * q;
-        const float* s1 = s0 + Ws;
-        float u[8], v[8];
-        if (VEC == 4 && 8 * q + 8 <= Ws) {
-            const float4 a0 = ld4(s0), a1 = ld4(s0 + 4), b0 = ld4(s1), b1 = ld4(s1 + 4);
-            u[0] = a0.x; u[1] = a0.y; u[2] = a0.z; u[3] = a0.w; u[4] = a1.x; u[5] = a1.y; u[6] = a1.z; u[7] = a1.w;
-            v[0] = b0.x; v[1] = b0.y; v[2] = b0.z; v[3] = b0.w; v[4] = b1.x; v[5] = b1.y; v[6] = b1.z; v[7] = b1.w;
-        } else if (VEC >= 2) {
+    // NI quads per thread per pass, all loads of a pass issued before any arithmetic (the pass keeps
+    // NI x 64 bytes per thread in flight instead of 64)
+    for (int t0 = threadIdx.x; t0 < tot; t0 += NI * blockDim.x) {
+        float u[NI][8], v[NI][8];
+        int bcs[NI], hps[NI], qs[NI];
+#pragma unroll
+        for (int n = 0; n < NI; ++n) {
+            const int t = min(t0 + n * (int)blockDim.x, tot - 1);  // (a tail item repeats the last quad: same values)
+            const int pl = t / nqp, rem = t - pl * nqp;
+            const int hp = rem / Wq, q = rem - hp * Wq;
+            const int bc = pbase + pl;
+            bcs[n] = bc; hps[n] = hp; qs[n] = q;
+            const float* s0 = y + ((int64_t)bc * Hs + 2 * hp) * Ws + 8 * q;
+            const float* s1 = s0 + Ws;
+            if (VEC == 4 && 8 * q + 8 <= Ws) {
+                const float4 a0 = ld4(s0), a1 = ld4(s0 + 4), b0 = ld4(s1), b1 = ld4(s1 + 4);
+                u[n][0] = a0.x; u[n][1] = a0.y; u[n][2] = a0.z; u[n][3] = a0.w;
+                u[n][4] = a1.x; u[n][5] = a1.y; u[n][6] = a1.z; u[n][7] = a1.w;
+                v[n][0] = b0.x; v[n][1] = b0.y; v[n][2] = b0.z; v[n][3] = b0.w;
+                v[n][4] = b1.x; v[n][5] = b1.y; v[n][6] = b1.z; v[n][7] = b1.w;
+            } else if (VEC >= 2) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const bool ok = 8 * q + 2 * j + 1 < Ws;
+                    const float2 a0 = ok ? *reinterpret_cast<const float2*>(s0 + 2 * j) : make_float2(0.f, 0.f);
+                    const float2 b0 = ok ? *reinterpret_cast<const float2*>(s1 + 2 * j) : make_float2(0.f, 0.f);
+                    u[n][2 * j] = a0.x; u[n][2 * j + 1] = a0.y; v[n][2 * j] = b0.x; v[n][2 * j + 1] = b0.y;
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const bool ok = 8 * q + e < 2 * Wp;
+                    u[n][e] = ok ? s0[e] : 0.f;
+                    v[n][e] = ok ? s1[e] : 0.f;
+                }
+            }
+        }
+#pragma unroll
+        for (int n = 0; n < NI; ++n) {
+            if (t0 + n * (int)blockDim.x >= tot) break;
+            const int bc = bcs[n], hp = hps[n], q = qs[n];
+            const float4 k = cf[bc % C];
+            const float d = drop ? drop[bc] : 1.f;
+            float out[4], ya[4];
+            unsigned ag = 0;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const bool ok = 8 * q + 2 * j + 1 < Ws;
-                const float2 a0 = ok ? *reinterpret_cast<const float2*>(s0 + 2 * j) : make_float2(0.f, 0.f);
-                const float2 b0 = ok ? *reinterpret_cast<const float2*>(s1 + 2 * j) : make_float2(0.f, 0.f);
-                u[2 * j] = a0.x; u[2 * j + 1] = a0.y; v[2 * j] = b0.x; v[2 * j + 1] = b0.y;
+                // first maximum of relu(BN) in window scan order (torch max_pool2d; the data gradient's rule)
+                const float q0 = fmaxf(fmaf(u[n][2 * j], k.x, k.y), 0.f), q1 = fmaxf(fmaf(u[n][2 * j + 1], k.x, k.y), 0.f);
+                const float q2 = fmaxf(fmaf(v[n][2 * j], k.x, k.y), 0.f), q3 = fmaxf(fmaf(v[n][2 * j + 1], k.x, k.y), 0.f);
+                float best = q0, yy = u[n][2 * j];
+                unsigned arg = 0;
+                if (q1 > best) { best = q1; arg = 1; yy = u[n][2 * j + 1]; }
+                if (q2 > best) { best = q2; arg = 2; yy = v[n][2 * j]; }
+                if (q3 > best) { best = q3; arg = 3; yy = v[n][2 * j + 1]; }
+                out[j] = d * best;
+                ya[j] = yy;
+                ag |= arg << (8 * j);
             }
-        } else {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const bool ok = 8 * q + e < 2 * Wp;
-                u[e] = ok ? s0[e] : 0.f;
-                v[e] = ok ? s1[e] : 0.f;
-            }
-        }
-        float out[4], ya[4];
-        unsigned ag = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            // first maximum of relu(BN) in window scan order (torch max_pool2d; the data gradient's rule)
-            const float q0 = fmaxf(fmaf(u[2 * j], k.x, k.y), 0.f), q1 = fmaxf(fmaf(u[2 * j + 1], k.x, k.y), 0.f);
-            const float q2 = fmaxf(fmaf(v[2 * j], k.x, k.y), 0.f), q3 = fmaxf(fmaf(v[2 * j + 1], k.x, k.y), 0.f);
-            float best = q0, yy = u[2 * j];
-            unsigned arg = 0;
-            if (q1 > best) { best = q1; arg = 1; yy = u[2 * j + 1]; }
-            if (q2 > best) { best = q2; arg = 2; yy = v[2 * j]; }
-            if (q3 > best) { best = q3; arg = 3; yy = v[2 * j + 1]; }
-            out[j] = d * best;
-            ya[j] = yy;
-            ag |= arg << (8 * j);
-        }
-        const int64_t po = ((int64_t)bc * Hp + hp) * Wp + 4 * q;
-        float* dst = x + po;
-        if ((Wp & 3) == 0) {
-            st4(dst, make_float4(out[0], out[1], out[2], out[3]));
-            if (ysel) {
-                st4(ysel + po, make_float4(ya[0], ya[1], ya[2], ya[3]));
-                *reinterpret_cast<unsigned*>(parg + po) = ag;
-            }
-        } else if ((Wp & 1) == 0) {  // 8-byte aligned pairs (the quad's second pair may lie past the row)
-#pragma unroll
-            for (int j = 0; j < 4; j += 2)
-                if (4 * q + j < Wp) {
-                    *reinterpret_cast<float2*>(dst + j) = make_float2(out[j], out[j + 1]);
-                    if (ysel) {
-                        *reinterpret_cast<float2*>(ysel + po + j) = make_float2(ya[j], ya[j + 1]);
-                        *reinterpret_cast<uint16_t*>(parg + po + j) = (uint16_t)(ag >> (8 * j));
-                    }
-                }
-        } else {
-            for (int j = 0; j < 4 && 4 * q + j < Wp; ++j) {
-                dst[j] = out[j];
+            const int64_t po = ((int64_t)bc * Hp + hp) * Wp + 4 * q;
+            float* dst = x + po;
+            if ((Wp & 3) == 0) {
+                st4(dst, make_float4(out[0], out[1], out[2], out[3]));
                 if (ysel) {
-                    ysel[po + j] = ya[j];
-                    parg[po + j] = (uint8_t)(ag >> (8 * j));
+                    st4(ysel + po, make_float4(ya[0], ya[1], ya[2], ya[3]));
+                    *reinterpret_cast<unsigned*>(parg + po) = ag;
+                }
+            } else if ((Wp & 1) == 0) {  // 8-byte aligned pairs (the quad's second pair may lie past the row)
+#pragma unroll
+                for (int j = 0; j < 4; j += 2)
+                    if (4 * q + j < Wp) {
+                        *reinterpret_cast<float2*>(dst + j) = make_float2(out[j], out[j + 1]);
+                        if (ysel) {
+                            *reinterpret_cast<float2*>(ysel + po + j) = make_float2(ya[j], ya[j + 1]);
+                            *reinterpret_cast<uint16_t*>(parg + po + j) = (uint16_t)(ag >> (8 * j));
+                        }
+                    }
+            } else {
+                for (int j = 0; j < 4 && 4 * q + j < Wp; ++j) {
+                    dst[j] = out[j];
+                    if (ysel) {
+                        ysel[po + j] = ya[j];
+                        parg[po + j] = (uint8_t)(ag >> (8 * j));
+                    }
                 }
             }
         }
@@ -515,15 +530,16 @@ int launch_bn_relu_pool(const float* y, const float4* cf, const float* drop, flo
     const int nplanes = B * C, nqp = Hp * ((Wp + 3) / 4);
     const int ppb = std::max(1, 1024 / std::max(1, nqp));  // ~1024 quads per block
     const int blocks = ceil_div(nplanes, ppb);
-    if (Ws % 4 == 0)
-        bn_relu_pool_kernel<4><<<blocks, 256, 0, s>>>(y, cf, drop, x, nplanes, C, Hs, Ws, Hp, Wp, ppb, ysel,
-                                                     parg);
-    else if (Ws % 2 == 0)
-        bn_relu_pool_kernel<2><<<blocks, 256, 0, s>>>(y, cf, drop, x, nplanes, C, Hs, Ws, Hp, Wp, ppb, ysel,
-                                                     parg);
-    else
-        bn_relu_pool_kernel<1><<<blocks, 256, 0, s>>>(y, cf, drop, x, nplanes, C, Hs, Ws, Hp, Wp, ppb, ysel,
-                                                     parg);
+    static const int ni = getenv("PCX_POOL_NI") ? atoi(getenv("PCX_POOL_NI")) : 2;
+#define PCX_BRP(V_, NI_)                                                                                       \
+    bn_relu_pool_kernel<V_, NI_><<<blocks, 256, 0, s>>>(y, cf, drop, x, nplanes, C, Hs, Ws, Hp, Wp, ppb, ysel, parg)
+    const int v = Ws % 4 == 0 ? 4 : Ws % 2 == 0 ? 2 : 1;
+    if (ni == 1) {
+        if (v == 4) PCX_BRP(4, 1); else if (v == 2) PCX_BRP(2, 1); else PCX_BRP(1, 1);
+    } else {
+        if (v == 4) PCX_BRP(4, 2); else if (v == 2) PCX_BRP(2, 2); else PCX_BRP(1, 2);
+    }
+#undef PCX_BRP
     PCX_LAUNCH_CHECK("bn_relu_pool_kernel");
     return PCX_OK;
 }
