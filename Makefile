@@ -1,24 +1,23 @@
 # libpcx.so: the MI355X (gfx950) kernels behind the C ABI in include/pcx.h.
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
+# AB: compile-time A/B alternates for analysis builds only (PCX_AB_* in csrc/pcx_common.h), e.g.
+#   make AB="-DPCX_AB_NO_WGBD=1" LIB=tools/ab/libpcx.so BUILD=tools/ab/obj
+AB ?=
 CXXFLAGS = -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Iinclude -Wall -Wno-unused-result \
-           -munsafe-fp-atomics
+           -munsafe-fp-atomics $(AB)
 SRC = $(wildcard phoneme_contrast_amd/csrc/*.hip)
-OBJ = $(patsubst phoneme_contrast_amd/csrc/%.hip,build/%.o,$(SRC))
+BUILD ?= build
+OBJ = $(patsubst phoneme_contrast_amd/csrc/%.hip,$(BUILD)/%.o,$(SRC))
 HDR = $(wildcard phoneme_contrast_amd/csrc/*.h) include/pcx.h
-LIB = phoneme_contrast_amd/libpcx.so
+LIB ?= phoneme_contrast_amd/libpcx.so
 
-TOOLS = tools/wino_bench tools/ww_bench tools/stem_bench tools/wb_bench tools/ws_bench tools/wino4_bench
+TOOLS = tools/wino_bench tools/ww_bench tools/stem_bench tools/wb_bench tools/ws_bench
 
 all: $(LIB) $(TOOLS)
 
 # engine cross-check / micro-benchmark (tests/test_wino_engine_gpu.py runs it)
 tools/wino_bench: tools/wino_bench.cpp $(LIB) $(HDR)
-	$(HIPCC) -O2 -std=c++17 --offload-arch=$(ARCH) -Iinclude $< -Lphoneme_contrast_amd -lpcx \
-	    -Wl,-rpath,'$$ORIGIN/../phoneme_contrast_amd' -o $@
-
-# F(4x3) Winograd conv vs the F(2x2) one (tests/test_wino_engine_gpu.py runs it)
-tools/wino4_bench: tools/wino4_bench.cpp $(LIB) $(HDR)
 	$(HIPCC) -O2 -std=c++17 --offload-arch=$(ARCH) -Iinclude $< -Lphoneme_contrast_amd -lpcx \
 	    -Wl,-rpath,'$$ORIGIN/../phoneme_contrast_amd' -o $@
 
@@ -42,15 +41,14 @@ tools/stem_bench: tools/stem_bench.cpp $(LIB) $(HDR)
 	$(HIPCC) -O2 -std=c++17 --offload-arch=$(ARCH) -Iinclude $< -Lphoneme_contrast_amd -lpcx \
 	    -Wl,-rpath,'$$ORIGIN/../phoneme_contrast_amd' -o $@
 
-build/%.o: phoneme_contrast_amd/csrc/%.hip $(HDR)
-	@mkdir -p build
+$(BUILD)/%.o: phoneme_contrast_amd/csrc/%.hip $(HDR)
+	@mkdir -p $(BUILD)
 	$(HIPCC) $(CXXFLAGS) -c $< -o $@
 
 # fp32 MFMA shares the vector pipe: packed f32 VALU (SLP) costs more issue than scalar beside it
-build/conv_wino.o: CXXFLAGS += -fno-slp-vectorize
-build/wgrad_wino.o: CXXFLAGS += -fno-slp-vectorize
-build/wgbd_wino.o: CXXFLAGS += -fno-slp-vectorize
-build/conv_wino4.o: CXXFLAGS += -fno-slp-vectorize
+$(BUILD)/conv_wino.o: CXXFLAGS += -fno-slp-vectorize
+$(BUILD)/wgrad_wino.o: CXXFLAGS += -fno-slp-vectorize
+$(BUILD)/wgbd_wino.o: CXXFLAGS += -fno-slp-vectorize
 
 $(LIB): $(OBJ)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJ)

@@ -112,20 +112,35 @@ def cpu_baseline(full=False, quick=False, T=200):
 
 
 def measure_peaks(dev):
-    """Achievable peaks on this box (report against vendor and measured): HBM by a
-    2 GiB device-to-device copy, fp32 matrix rate by an 8192^3 torch.mm (rocBLAS / hipBLASLt
-    fp32 GEMM on the MFMA).  Timed with HIP events after a warm-up; ~1 s in total."""
+    """Achievable peaks on this box (report against vendor and measured): HBM by a 2 GiB
+    float4 streaming copy (libpcx pcx_stream_copy: 16-byte nontemporal loads / stores, the copy the
+    MI355X guide measures at ~6.3 TB/s; torch's copy_ reached ~4.9 TB/s, which understated the roof of
+    an HBM-bound kernel), fp32 matrix rate by an 8192^3 torch.mm (rocBLAS / hipBLASLt fp32 GEMM on the
+    MFMA).  Timed with HIP events on the current stream after a warm-up; ~1 s in total."""
+    from phoneme_contrast_amd import _lib
     n = 1 << 29  # floats: 2 GiB per buffer
     a = torch.empty(n, device=dev)
     b = torch.empty(n, device=dev)
-    b.copy_(a)
+    so = _lib.lib()
+    st = _lib.stream_of(a)
+
+    def copy():
+        _lib.check(so.pcx_stream_copy(_lib.ptr(a), _lib.ptr(b), 4 * n, st), "pcx_stream_copy")
+
+    copy()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(5):
+        copy()
+    e1.record()
+    torch.cuda.synchronize()
+    hbm = 5 * 2 * 4 * n / (e0.elapsed_time(e1) / 1000.0) / 1e9
     e0.record()
     for _ in range(5):
         b.copy_(a)
     e1.record()
     torch.cuda.synchronize()
-    hbm = 5 * 2 * 4 * n / (e0.elapsed_time(e1) / 1000.0) / 1e9
+    hbm_torch = 5 * 2 * 4 * n / (e0.elapsed_time(e1) / 1000.0) / 1e9
     del a, b
     m = 8192
     x = torch.randn(m, m, device=dev)
@@ -137,8 +152,10 @@ def measure_peaks(dev):
     e1.record()
     torch.cuda.synchronize()
     gemm = 5 * 2 * m ** 3 / (e0.elapsed_time(e1) / 1000.0) / 1e12
-    return {"hbm_copy_GBps": round(hbm, 1), "fp32_gemm_TFLOPs": round(gemm, 1),
-            "note": "measured on this GPU: 2 GiB D2D copy (read + write bytes); torch.mm fp32 8192^3"}
+    return {"hbm_copy_GBps": round(hbm, 1), "hbm_torch_copy_GBps": round(hbm_torch, 1),
+            "fp32_gemm_TFLOPs": round(gemm, 1),
+            "note": "measured on this GPU: 2 GiB float4 streaming copy (pcx_stream_copy; read + write bytes), "
+                    "torch copy_ beside it; torch.mm fp32 8192^3"}
 
 
 def load_pmc(model, precision, label):
@@ -324,7 +341,7 @@ def main():
         for lab, (tot, cnt) in sorted(table.items(), key=lambda kv: -kv[1][0]):
             kernels[lab] = {"avg_ms": round(tot / cnt, 4), "launches": cnt,
                             "share": round(tot / tsteps / ms_step, 4)}
-    xfrac = (lambda lab: deep_executed_fraction(lab, F, T, bf16)) if deep else (lambda lab: executed_fraction(lab, T))
+    xfrac = (lambda lab: deep_executed_fraction(lab, F, T, bf16)) if deep else (lambda lab: executed_fraction(lab, T, F))
     if dom is not None and prof.get(dom):
         # the dominant kernel: the costed label with the largest total time in the table steps (every
         # kernel that matters has a cost model; the labels without one are tiny finalisers /
@@ -374,9 +391,12 @@ def main():
     xsf = executed_step_flops(B, F, T, D, deep=deep, bf16=bf16)
     step_roof = {"flops_per_step": sf, "executed_flops_per_step": xsf, "bytes_per_step": sb,
                  "byte_model": "SURVEY 8(d), e=2 (bf16 activations)" if bf16 else "SURVEY 8(d), e=4 (fp32)",
-                 "mfma_fraction": round(xsf / step_s / (peak * 1e12), 4),
-                 "mfma_fraction_counts": "executed FLOPs (Winograd kernels at 16 multiplies per 2x2 outputs)",
-                 "alg_equiv_mfma_fraction": round(sf / step_s / (peak * 1e12), 4),
+                 # (schema 2: mfma_fraction is the algorithmic (direct-conv) FLOP rate, as in rounds 1-4; the
+                 # round-5 lines wrote the executed rate under that key -- it is executed_mfma_fraction now)
+                 "schema": 2,
+                 "mfma_fraction": round(sf / step_s / (peak * 1e12), 4),
+                 "executed_mfma_fraction": round(xsf / step_s / (peak * 1e12), 4),
+                 "executed_counts": "Winograd kernels at 16 multiplies per 2x2 output tile (costs.wino_tile_fraction)",
                  "hbm_fraction": round(sb / step_s / (HBM_PEAK_GBS * 1e9), 4)}
     if table:
         mkey = (args.model, args.precision if deep else "fp32")

@@ -168,6 +168,10 @@ int pcx_net_grad_stages(const void* plan, int* first_param, int max_entries);
 int pcx_dropout_masks(float* out, int64_t n, float p, uint64_t seed, uint64_t offset,
                       hipStream_t stream);
 
+/* HBM streaming probe: dst = src (16-byte aligned, bytes % 16 == 0) with 16-byte nontemporal loads and
+ * stores; the achievable copy rate bench.py's measured_peaks reports (no reference counterpart). */
+int pcx_stream_copy(const void* src, void* dst, size_t bytes, hipStream_t stream);
+
 /* ------------------------------------------------------------------ feature path
  * Replaces torchaudio.transforms.MFCC / MelSpectrogram + AmplitudeToDB as called by
  * MFCCExtractor / MelSpectrogramExtractor (src/datasets/features.py:22-150), the random gain of

@@ -80,6 +80,7 @@ SIGNATURES = {
                                      c_int]),
     "pcx_dropout_masks": (c_int, [c_void_p, c_i64, c_float, ctypes.c_uint64, ctypes.c_uint64,
                                   c_void_p]),
+    "pcx_stream_copy": (c_int, [c_void_p, c_void_p, c_size, c_void_p]),
     "pcx_melspec": (c_int, [c_void_p, c_i64, c_i64, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                             c_int, c_void_p, c_void_p, c_void_p]),
     "pcx_mel_finish": (c_int, [c_void_p, c_void_p, c_i64, c_i64, c_int, c_int, c_float, c_void_p,

@@ -64,18 +64,60 @@ def kernel_costs(B, F, T, D=128):
     return out
 
 
-def executed_fraction(label, T):
+def wino_tile_fraction(H, W):
+    """Multiplies Winograd F(2x2,3x3) executes per direct-conv multiply on an H x W output: 16 per 2 x 2
+    tile, ceil(H / 2) x ceil(W / 2) tiles, against 9 per output (4/9 at even H and W; 5 x 25 -> 0.555)."""
+    return 16.0 * ((H + 1) // 2) * ((W + 1) // 2) / (9.0 * H * W)
+
+
+def wgrad_wino_routed(H, W, cin, cout):
+    """Whether the 3x3 weight gradient runs on the Winograd kernel: csrc/wgrad_wino.hip
+    wgrad_wino_geometry() restated (staging vector 4 / 2 / 1 floats; odd widths only where the 2 x 2 tiles'
+    outputs are >= 75 % real; strips of <= 50 tiles; 80 KB of LDS)."""
+    if cin % 32 or cout % 32 or H < 1 or W < 4:
+        return False
+    V = 4 if W % 4 == 0 else 2 if W % 2 == 0 else 1
+    TC = (W + 1) // 2
+    if V == 1 and H * W < 0.75 * 4.0 * ((H + 1) // 2) * TC:
+        return False
+    nseg = -(-TC // 50)
+    S = -(-TC // nseg)
+    if nseg > 1:
+        S = (S + 1) & ~1
+    nseg = -(-TC // S)
+    Ks = (S + 1) // 2
+    nd, kmax = 2 * S // V, (2 * S + 1 + V - 1) // V
+    nx = kmax + 1
+    if (2 * S) % V or 2 * nd > 64 or 2 * nx > 64:
+        return False
+
+    def odd2(n):  # smallest m >= n with m = 2 * odd
+        while n % 4 != 2:
+            n += 1
+        return n
+    XCS = odd2(max(V * kmax + 1, 4 * Ks + 2, 2 * S + 5))
+    DCS = odd2(4 * Ks)
+    return (4 + 128 * XCS + 64 * DCS) * 4 <= 80 * 1024
+
+
+def executed_fraction(label, T, F=40):
     """Multiplies executed per algorithmic (direct-conv) multiply for cnn_small's kernels: the 3x3
     forward / data-gradient convs run Winograd F(2x2,3x3) at W >= 31 (conv_wino.hip), the 3x3
-    weight gradients at even W (wgrad_wino.hip): 16 multiplies per 2x2 outputs instead of 36."""
-    widths = {2: T, 3: T // 2, 4: T // 2, 5: T // 4, 6: T // 4}
+    weight gradients where wgrad_wino_routed() (wgrad_wino.hip), the fused layer-2 backward (wgbd_wino.hip)
+    on both; a Winograd kernel executes wino_tile_fraction() of the direct multiplies (partial tiles at odd
+    sizes count whole).  Padding MFMAs a kernel runs beyond its tiles (wgbd's partial 16-tile groups) are not
+    counted: the MOPS counter includes them."""
+    shape = {2: (F, T, 32, 32), 3: (F // 2, T // 2, 32, 64), 4: (F // 2, T // 2, 64, 64),
+             5: (F // 4, T // 4, 64, 128), 6: (F // 4, T // 4, 128, 128)}
     for pre in ("conv_fwd_L", "conv_dgrad_L"):
         if label.startswith(pre):
-            return 4 / 9 if widths.get(int(label[len(pre):]), 0) >= 31 else 1.0
+            H, W, _, _ = shape.get(int(label[len(pre):]), (0, 0, 0, 0))
+            return wino_tile_fraction(H, W) if W >= 31 else 1.0
     if label.startswith("wgrad_L") and label[7:].isdigit() and int(label[7:]) >= 2:
-        return 4 / 9 if widths[int(label[7:])] % 2 == 0 else 1.0
+        H, W, ci, co = shape[int(label[7:])]
+        return wino_tile_fraction(H, W) if wgrad_wino_routed(H, W, ci, co) else 1.0
     if label == "wgbd_L2":  # fused layer-2 backward: both gradients on Winograd F(2x2,3x3)
-        return 4 / 9
+        return wino_tile_fraction(F, T)
     return 1.0
 
 
@@ -83,16 +125,17 @@ def deep_executed_fraction(label, F, T, bf16=False, h=DEEP_DIMS):
     """Multiplies executed per algorithmic multiply for cnn_deep's kernels (deep.hip routing): in fp32
     the stride-1 3x3 convs whose channel counts fit the cnn_small engines (block 0 conv1, every conv2)
     run forward / data gradient on Winograd F(2x2,3x3) (conv_wino.hip: rows >= 31 columns, and the
-    batch-spanning units below that) and the weight gradient on wgrad_wino.hip at even widths; the
-    stem, the stride-2 convs, the 1x1 shortcuts and every bf16 conv are direct."""
+    batch-spanning units below that) and the weight gradient on wgrad_wino.hip where wgrad_wino_routed();
+    a Winograd kernel executes wino_tile_fraction() of the direct multiplies (5 x 25: 0.555, 3 x 13: 0.635);
+    the stem, the stride-2 convs, the 1x1 shortcuts and every bf16 conv are direct."""
     if bf16:
         return 1.0
     routed = {}
     for fl, wl, dl, ci, co, k, s, IH, IW, OH, OW in deep_convs(F, T, h):
         fits = (co == 32 or co % 64 == 0) and (ci == 32 or ci % 64 == 0)
         if k == 3 and s == 1 and fits:
-            routed[fl] = routed[dl] = 4 / 9
-            routed[wl] = 4 / 9 if OW % 2 == 0 else 1.0
+            routed[fl] = routed[dl] = wino_tile_fraction(OH, OW)
+            routed[wl] = wino_tile_fraction(OH, OW) if wgrad_wino_routed(OH, OW, ci, co) else 1.0
     return routed.get(label, 1.0)
 
 
@@ -107,7 +150,7 @@ def executed_step_flops(B, F, T, D=128, deep=False, bf16=False):
     else:
         total, _ = step_cost(B, F, T, D)
         costs = kernel_costs(B, F, T, D)
-        frac = lambda lab: executed_fraction(lab, T)  # noqa: E731
+        frac = lambda lab: executed_fraction(lab, T, F)  # noqa: E731
         # (at even widths layer 2's data gradient and weight gradient run as one kernel, wgbd_L2, with the
         # same executed fraction as the two it replaces)
         labels = [f"{p}{l}" for l in range(2, 7) for p in ("conv_fwd_L", "conv_dgrad_L", "wgrad_L")]

@@ -530,7 +530,7 @@ int launch_bn_relu_pool(const float* y, const float4* cf, const float* drop, flo
     const int nplanes = B * C, nqp = Hp * ((Wp + 3) / 4);
     const int ppb = std::max(1, 1024 / std::max(1, nqp));  // ~1024 quads per block
     const int blocks = ceil_div(nplanes, ppb);
-    static const int ni = getenv("PCX_POOL_NI") ? atoi(getenv("PCX_POOL_NI")) : 2;
+    constexpr int ni = PCX_AB_POOL_NI;
 #define PCX_BRP(V_, NI_)                                                                                       \
     bn_relu_pool_kernel<V_, NI_><<<blocks, 256, 0, s>>>(y, cf, drop, x, nplanes, C, Hs, Ws, Hp, Wp, ppb, ysel, parg)
     const int v = Ws % 4 == 0 ? 4 : Ws % 2 == 0 ? 2 : 1;

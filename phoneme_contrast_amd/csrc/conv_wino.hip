@@ -1097,12 +1097,11 @@ int launch_conv3x3_wino(int pro, int epi, ConvArgs a, hipStream_t s) {
     int64_t nwg = std::min<int64_t>(units, 2 * (int64_t)num_cus());
     if (nwg >= 8) nwg &= ~(int64_t)7;
     dim3 grid((unsigned)nwg);
-    static const bool naive_env = getenv("PCX_WINO_SLOT") && atoi(getenv("PCX_WINO_SLOT")) == 1;
-    g.naive_slots = naive_env;
+    g.naive_slots = PCX_AB_WINO_SLOT;
     // pooled data gradient with 16-byte source rows
     const bool v4 = (epi == EPI_BWD_POOL || epi == EPI_BWD_POOLSEL) && (a.Ws & 3) == 0 && !(a.H & 1) && !(a.W & 1);
-    // 16-byte operand copies where the caller guarantees 4 readable bytes before src (PCX_WINO_X4=0: dword copies)
-    static const bool x4_env = getenv("PCX_WINO_X4") == nullptr || atoi(getenv("PCX_WINO_X4")) != 0;
+    // 16-byte operand copies where the caller guarantees 4 readable bytes before src (PCX_AB_NO_WINO_X4: dword copies)
+    constexpr bool x4_env = !PCX_AB_NO_WINO_X4;
     // (not the pooled data gradient: its window registers already spill at 8-14 VGPRs; the two more
     // copy offsets of X4 made that 31-34)
     // measured at B = 4096 (profiles/r4_x4_time.txt): BN + ReLU forward and the data gradients gain

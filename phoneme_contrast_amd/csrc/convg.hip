@@ -1052,8 +1052,8 @@ int launch_convg(ConvGArgs a, hipStream_t s) {
 int chan_slices(int B, int C, int* bps) {
     // ~16384 blocks per launch: each block's run of planes is short enough that the launch is not one
     // long tail of latency-bound blocks (same-box B = 4096: deep fp32 125.2 -> 123.2 ms, bf16 51.0 ->
-    // 50.2 against 2048, profiles/r4_chan_slices.txt; PCX_CHAN_TARGET overrides)
-    static const int target = getenv("PCX_CHAN_TARGET") ? std::max(256, atoi(getenv("PCX_CHAN_TARGET"))) : 16384;
+    // 50.2 against 2048, profiles/r4_chan_slices.txt; PCX_AB_CHAN_TARGET overrides)
+    constexpr int target = PCX_AB_CHAN_TARGET < 256 ? 256 : PCX_AB_CHAN_TARGET;
     int want = std::max(1, std::min(B, target / std::max(C, 1)));
     *bps = ceil_div(B, want);
     return ceil_div(B, *bps);
@@ -1083,9 +1083,9 @@ int launch_bwd_prep(BwdPrepArgs a, int* nslice, hipStream_t s) {
     return PCX_OK;
 }
 
-// short rows (flat form; PCX_BN_ROWTILE=1: the row tiles)
+// short rows (flat form; PCX_AB_BN_ROWTILE: the row tiles)
 static bool bn_flat(int64_t P, int64_t n, const void* a, const void* b, const void* c) {
-    static const bool off = getenv("PCX_BN_ROWTILE") && atoi(getenv("PCX_BN_ROWTILE"));
+    constexpr bool off = PCX_AB_BN_ROWTILE;
     auto al = [](const void* p) { return p == nullptr || ((uintptr_t)p & 15) == 0; };
     return !off && P < 1024 && n / P < ((int64_t)1 << 31) && al(a) && al(b) && al(c) && n > 0;
 }

@@ -870,7 +870,7 @@ int launch_to_nhwc(NhwcArgs a, hipStream_t s) {
     PCX_CHECK_ARG(!a.dst_b || (a.op == NHWC_BNBWD && a.y_b && a.cf_b), "to_nhwc: second image needs y_b and cf_b");
     // image rows per step: up to 128 floats of a channel (narrow images: fewer, fuller steps); one row
     // with the pooled residual (staged per row)
-    static const bool one_row = getenv("PCX_NHWC_ROWS1") && atoi(getenv("PCX_NHWC_ROWS1"));  // A/B: a row per step
+    constexpr bool one_row = PCX_AB_NHWC_ROWS1;  // A/B: a row per step
     a.rows = a.res_pool || one_row ? 1 : std::max(1, std::min(a.H, (a.dst_b ? 124 : 128) / a.W));
     const size_t sm = ((size_t)64 * ((a.rows * a.W + 3) & ~3) + 32) * 4 * (a.dst_b || a.res_pool ? 2 : 1);
     PCX_CHECK_ARG(!a.res_pool || a.C % 4 == 0, "to_nhwc: pooled residual needs C %% 4 == 0");
@@ -894,9 +894,9 @@ static int convn_kc(int ck) { return ck % 64 == 0 ? 64 : 32; }
 // halo-staged tiling of an H x W image (stride-1 3x3 pad-1 modes 0 / 1): the fewest TR x TW tiles of at
 // most maxpx pixels (ties: the smaller halo); used only when the tiles keep >= 90 % of their MFMA columns
 // busy (T = 200, 128 pixels: 20 x 100 -> 16 tiles of 5 x 25, 10 x 50 -> 4, 5 x 25 -> 1; 256 pixels:
-// 20 x 100 -> 8 of 10 x 25).  PCX_CONVN_HALO=0: per-tap copies everywhere.
+// 20 x 100 -> 8 of 10 x 25).  PCX_AB_NO_CONVN_HALO: per-tap copies everywhere.
 static bool convn_halo_tiles(int H, int W, int maxpx, HaloGeo* out) {
-    static const bool off = getenv("PCX_CONVN_HALO") && atoi(getenv("PCX_CONVN_HALO")) == 0;
+    constexpr bool off = PCX_AB_NO_CONVN_HALO;
     if (off || H < 1 || W < 1) return false;
     HaloGeo best{};
     int64_t bt = -1, bh = 0;
@@ -922,7 +922,7 @@ static bool convn_halo_tiles(int H, int W, int maxpx, HaloGeo* out) {
 // 8-wave blocks (256-pixel tiles: two blocks of 8 waves per CU instead of three of 4) for the 64-row
 // forward and the plain data gradient; 4 waves elsewhere (the BN-sum epilogue's registers, 128 rows' LDS)
 static int convn_halo_waves(const ConvGArgs& a) {
-    static const int env = getenv("PCX_CONVN_NW") ? atoi(getenv("PCX_CONVN_NW")) : 0;
+    constexpr int env = PCX_AB_CONVN_NW;
     const int64_t M = a.mode == 0 ? a.cout : a.cin;
     const bool eight = M <= 64 && (a.mode == 0 || !a.ep_pg);
     if (env == 4 || env == 8) return eight ? env : 4;

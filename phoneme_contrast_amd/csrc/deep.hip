@@ -41,9 +41,9 @@ struct DeepBlock {
 };
 
 // narrow stride-1 images (5 x 25, 3 x 13) on the Winograd conv with batch-spanning units
-// (PCX_NO_WINO_SPAN=1: the direct LDS-DMA conv)
+// (PCX_AB_NO_WINO_SPAN: the direct LDS-DMA conv)
 static bool wino_span_ok() {
-    static const bool off = getenv("PCX_NO_WINO_SPAN") && atoi(getenv("PCX_NO_WINO_SPAN"));
+    constexpr bool off = PCX_AB_NO_WINO_SPAN;
     return !off;
 }
 
@@ -221,9 +221,8 @@ int build_deep(Plan& p) {
     stat = std::max(stat, (size_t)2 * C4 * B);
     if (d.stem_fused) stat = std::max(stat, (size_t)2 * C0 * B);  // stem_pool_bwd partials [C0][B] x 2
     d.stat = p.carve("stat_part", stat * 4);
-    // stride-1 Winograd convs take their units from a per-XCD queue (PCX_NO_WINO_QUEUE=1: static order)
-    p.wq = getenv("PCX_NO_WINO_QUEUE") && atoi(getenv("PCX_NO_WINO_QUEUE")) ? 0
-                                                                           : p.carve("wino_queue", WINO_QUEUE_INTS * 4);
+    // stride-1 Winograd convs take their units from a per-XCD queue (PCX_AB_NO_WINO_QUEUE: static order)
+    p.wq = PCX_AB_NO_WINO_QUEUE ? 0 : p.carve("wino_queue", WINO_QUEUE_INTS * 4);
     d.wgp = p.carve("wg_part", wg * 4);
     d.ident = p.carve("ident", (size_t)C4 * 16);
     d.identw = p.carve("identw", (size_t)cmax * 16);
@@ -792,7 +791,7 @@ int deep_backward(const Plan& p, const float* const* P, const float* x, const fl
                       k.ww2 ? &k.wwa2 : nullptr));
         float* dd = c.w<float>(d.dd);
         // channel-last: conv2's data gradient also reduces BN1's backward sums (no bwd_prep pass over dd)
-        const bool ep_sums = k.cn && getenv("PCX_NO_EPSUMS") == nullptr;
+        const bool ep_sums = k.cn && !PCX_AB_NO_EPSUMS;
         ConvGArgs ep{};
         if (ep_sums) {
             ConvGArgs q{};  // conv2's data gradient: its epilogue tiles

@@ -282,8 +282,9 @@ extern "C" int pcx_draw_view_params(const int64_t* gain_seeds, const int64_t* au
     PCX_CHECK_ARG(!aug_seeds || (cfg && tband && fband && level), "draw_view_params: NULL output");
     // each view reseeds its own generators, so views split over threads with identical results
     // (every MT19937 reseed costs ~2k steps: 4 per view)
-    unsigned nt = std::thread::hardware_concurrency();
-    if (const char* e = getenv("OMP_NUM_THREADS")) nt = (unsigned)std::max(1, atoi(e));
+    // (at most 16 threads: a GPU box's share of its host; the draws do not depend on the split)
+    const unsigned nt0 = std::thread::hardware_concurrency();
+    unsigned nt = nt0 ? nt0 : 1;
     nt = (unsigned)std::max<int64_t>(1, std::min<int64_t>({(int64_t)nt, 16, n / 256}));
     if (nt <= 1) {
         draw_range(gain_seeds, aug_seeds, 0, n, F, T, cfg, gain, tband, fband, level);

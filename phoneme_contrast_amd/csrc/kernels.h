@@ -82,22 +82,6 @@ size_t wino_nblk(int B, int H, int W, int cin, int cout);
 // flip = 0: forward weights w[M][K][3][3]; flip = 1: data gradient of forward weights w[K][M][3][3]
 int launch_wino_pack(const float* w, float* u, int M, int K, int flip, hipStream_t s);
 int launch_conv3x3_wino(int pro, int epi, ConvArgs a, hipStream_t s);
-// Winograd F(4x3, 3x3) form (conv_wino4.hip): 4-row x 3-column output tiles, one wave per SIMD with 32 output
-// channels, weights packed by launch_wino4_pack into [cout / 32][cin][32][36]; rows of >= 46 columns (16 tile
-// columns), units of 64 tiles of the batch-wide tile order; PRO_RAW / PRO_BNRELU with EPI_FWD, PRO_RAW with
-// EPI_BWD_RELU / EPI_BWD_POOLSELP.  Partials per 64-tile block: nblk = wino4_nblk().
-struct Wino4Geo {
-    int TR, TC, NTS, NTOT;  // tile rows / columns per sample, tiles per sample, tiles of the batch
-    int ncg;                // output-channel groups of 32
-    float inv_ncg, inv_NTS, inv_TC;
-    int nblk;               // 64-tile blocks (BN partials) of the launch
-};
-bool wino4_geometry(int B, int H, int W, int cin, int cout, Wino4Geo* g);
-bool wino4_supports(int pro, int epi);
-size_t wino4_nblk(int B, int H, int W, int cin, int cout);
-size_t wino4_lds_bytes(int cin);
-int launch_wino4_pack(const float* w, float* u, int M, int K, int flip, hipStream_t s);
-int launch_conv3x3_wino4(int pro, int epi, ConvArgs a, hipStream_t s);
 // materialised block tail x = drop * maxpool2(relu(y*s + t)) (feeds PRO_RAW convs)
 // ysel / parg (optional, both or neither): y at each window's first maximum of relu(y s + t) (torch's
 // max_pool2d rule) and its index, for the EPI_BWD_POOLSEL data gradient

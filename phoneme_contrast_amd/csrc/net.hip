@@ -63,7 +63,7 @@ int build_small(Plan& p) {
             L.wu = p.carve("wu", (size_t)16 * L.cin * L.cout * 4);
             L.wud = p.carve("wud", (size_t)16 * L.cin * L.cout * 4);
             // the data gradient's tile blocks are the forward's (same H x W), so one nblk serves both
-            if (L.pooled_in && L.wino && getenv("PCX_NO_POOLSEL") == nullptr) {
+            if (L.pooled_in && L.wino && !PCX_AB_NO_POOLSEL) {
                 snprintf(nm, sizeof nm, "ysel%d", l);
                 L.ysel = p.carve(nm, (size_t)B * L.cin * L.H * L.W * 4);
                 snprintf(nm, sizeof nm, "parg%d", l);
@@ -73,7 +73,7 @@ int build_small(Plan& p) {
                             : (int)std::max(conv3x3_nblk(B, L.H, L.W, L.cout), conv3x3_nblk(B, L.H, L.W, L.cin));
             L.wgw = wgrad_wino_geometry(B, L.H, L.W, L.cin, L.cout, &L.ww);
             // layer 2 (32 -> 32 at full resolution, BN + ReLU input): both gradients in one pass
-            L.wgbd = l == 2 && !L.pooled_in && L.cin == 32 && L.cout == 32 && L.wino && getenv("PCX_NO_WGBD") == nullptr &&
+            L.wgbd = l == 2 && !L.pooled_in && L.cin == 32 && L.cout == 32 && L.wino && !PCX_AB_NO_WGBD &&
                      wgbd_wino_geometry(B, L.H, L.W, 32, &L.wb);
             if (L.wgbd) {
                 wg = std::max(wg, (size_t)L.wb.nslice * 32 * 32 * 16);
@@ -92,35 +92,16 @@ int build_small(Plan& p) {
         }
         stat = std::max(stat, (size_t)2 * L.cout * L.nblk + L.nblk);
     }
-    // Winograd F(4x3) (conv_wino4.hip): the forward of every layer whose rows hold >= 16 tiles of 3 columns, the
-    // data gradients whose epilogue it has (through ReLU; the pooled hand-over EPI_BWD_POOLSELP) -- chosen after the
-    // pooled hand-over flags below are known; PCX_WINO4=1 enables it (validation in progress)
-    const bool w4ok = getenv("PCX_WINO4") != nullptr && atoi(getenv("PCX_WINO4")) != 0;
     {  // layer 2's fused backward reads layer 3's pooled data gradient + selection (a quarter of dz2's bytes)
         Layer &L2 = p.L[2], &L3 = p.L[3];
         L2.pd = L2.wgbd && L3.pooled_in && L3.ysel && L3.wino && !(L2.H & 1) && L2.W % 4 == 0 &&
-                L3.H == L2.H / 2 && L3.W == L2.W / 2 && getenv("PCX_NO_POOLDZ") == nullptr;
+                L3.H == L2.H / 2 && L3.W == L2.W / 2 && !PCX_AB_NO_POOLDZ;
         for (int i = 0; L2.pd && i < L2.wb.nseg; ++i) L2.pd = !(L2.wb.seg_t0[i] & 1);
         // likewise layer 4's Winograd weight gradient behind layer 5's pool (its data gradient reads dy)
         Layer &L4 = p.L[4], &L5 = p.L[5];
         L4.pd = L4.wgw && !L4.wgbd && !L4.pooled_in && L5.pooled_in && L5.ysel && L5.wino && !(L4.H & 1) &&
                 L4.W % 4 == 0 && L4.ww.V == 4 && (L4.ww.nseg == 1 || !(L4.ww.S & 1)) && L5.H == L4.H / 2 &&
-                L5.W == L4.W / 2 && getenv("PCX_NO_POOLDZ") == nullptr;
-    }
-    for (int l = 2; l <= 6; ++l) {
-        Layer& L = p.L[l];
-        const Layer& Lp = p.L[l - 1];
-        L.w4f = w4ok && wino4_geometry(B, L.H, L.W, L.cin, L.cout, nullptr);
-        // data gradient epilogue: through ReLU (EPI_BWD_RELU), or behind a pool whose consumer rebuilds the windows
-        // (EPI_BWD_POOLSELP: the previous layer's pd); not layer 2's (inside wgbd) nor a full-resolution pooled one
-        const bool epi_ok = !L.pooled_in || (L.ysel && Lp.pd);
-        L.w4d = w4ok && L.wino && !L.wgbd && epi_ok && wino4_geometry(B, L.H, L.W, L.cout, L.cin, nullptr);
-        L.nblk4f = L.w4f ? (int)wino4_nblk(B, L.H, L.W, L.cin, L.cout) : 0;
-        L.nblk4d = L.w4d ? (int)wino4_nblk(B, L.H, L.W, L.cout, L.cin) : 0;
-        if (L.w4f) L.wu4 = p.carve("wu4", (size_t)36 * L.cin * L.cout * 4);
-        if (L.w4d) L.wud4 = p.carve("wud4", (size_t)36 * L.cin * L.cout * 4);
-        stat = std::max(stat, (size_t)2 * std::max(L.cin, L.cout) * std::max(L.nblk4f, L.nblk4d) +
-                                  std::max(L.nblk4f, L.nblk4d));
+                L5.W == L4.W / 2 && !PCX_AB_NO_POOLDZ;
     }
     // first-layer weight gradient slices
     {
@@ -133,9 +114,8 @@ int build_small(Plan& p) {
     p.P6 = H5 * W5;
     stat = std::max(stat, (size_t)2 * p.C6 * B);
     p.stat_part = p.carve("stat_part", stat * 4);
-    // the Winograd convs take their units from a per-XCD queue (PCX_NO_WINO_QUEUE=1: static order)
-    p.wq = getenv("PCX_NO_WINO_QUEUE") && atoi(getenv("PCX_NO_WINO_QUEUE")) ? 0
-                                                                           : p.carve("wino_queue", WINO_QUEUE_INTS * 4);
+    // the Winograd convs take their units from a per-XCD queue (PCX_AB_NO_WINO_QUEUE: static order)
+    p.wq = PCX_AB_NO_WINO_QUEUE ? 0 : p.carve("wino_queue", WINO_QUEUE_INTS * 4);
     {
         size_t dymax = 0;
         for (int l = 2; l <= 6; ++l) dymax = std::max(dymax, (size_t)B * p.L[l].cout * p.L[l].H * p.L[l].W);
@@ -222,8 +202,7 @@ int small_forward(const Plan& p, const float* const* P, float* const* bnstat, in
     for (int l = 2; l <= 6; ++l) {
         const Layer& L = p.L[l];
         const Layer& Lp = p.L[l - 1];
-        if (L.w4f) RC(launch_wino4_pack(P[p_conv_w(l)], at<float>(ws, L.wu4), L.cout, L.cin, 0, s));
-        else if (L.wino) RC(launch_wino_pack(P[p_conv_w(l)], at<float>(ws, L.wu), L.cout, L.cin, 0, s));
+        if (L.wino) RC(launch_wino_pack(P[p_conv_w(l)], at<float>(ws, L.wu), L.cout, L.cin, 0, s));
         else RC(launch_pack_fwd(P[p_conv_w(l)], at<float>(ws, L.wu), L.cout, L.cin, s));
         ConvArgs c{};
         c.B = B; c.H = L.H; c.W = L.W; c.cin = L.cin; c.cout = L.cout;
@@ -236,8 +215,7 @@ int small_forward(const Plan& p, const float* const* P, float* const* bnstat, in
         c.part0 = part;
         c.part1 = part + (size_t)L.cout * L.nblk;
         c.partn = part + (size_t)2 * L.cout * L.nblk;
-        c.nblk = L.w4f ? L.nblk4f : L.wino ? L.nblk : (int)conv3x3_nblk(B, L.H, L.W, L.cout);
-        if (L.w4f) c.wpack = at<float>(ws, L.wu4);
+        c.nblk = L.wino ? L.nblk : (int)conv3x3_nblk(B, L.H, L.W, L.cout);
         c.src_guard = 1;  // workspace tensors (and the input never reaches a 3x3 conv)
         c.queue = p.wq ? at<int>(ws, p.wq) : nullptr;
         int pro = PRO_BNRELU;
@@ -252,8 +230,7 @@ int small_forward(const Plan& p, const float* const* P, float* const* bnstat, in
         }
         {
             Scope sc(&p.prof, s, "conv_fwd", l);
-            RC(L.w4f ? launch_conv3x3_wino4(pro, EPI_FWD, c, s)
-                     : L.wino ? launch_conv3x3_wino(pro, EPI_FWD, c, s) : launch_conv3x3_dma(pro, EPI_FWD, c, s));
+            RC(L.wino ? launch_conv3x3_wino(pro, EPI_FWD, c, s) : launch_conv3x3_dma(pro, EPI_FWD, c, s));
         }
         RC(finalize(l, c.nblk));
     }
@@ -461,8 +438,7 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
         }
         // ---- data gradient -> dz of the previous BN (through ReLU / MaxPool / Dropout2d)
         {
-            if (L.w4d) RC(launch_wino4_pack(P[p_conv_w(l)], at<float>(ws, L.wud4), L.cin, L.cout, 1, s));
-            else if (L.wino) RC(launch_wino_pack(P[p_conv_w(l)], at<float>(ws, L.wud), L.cin, L.cout, 1, s));
+            if (L.wino) RC(launch_wino_pack(P[p_conv_w(l)], at<float>(ws, L.wud), L.cin, L.cout, 1, s));
             else RC(launch_pack_dgrad(P[p_conv_w(l)], at<float>(ws, L.wud), L.cout, L.cin, s));
             float* dzp = at<float>(ws, Lp.dz);
             if (L.pooled_in && ((L.srcH & 1) || (L.srcW & 1)))
@@ -477,13 +453,13 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
             c.src_guard = 1;
             c.queue = p.wq ? at<int>(ws, p.wq) : nullptr;
             c.srcH = L.H; c.srcW = L.W;
-            c.wpack = at<float>(ws, L.w4d ? L.wud4 : L.wud);
+            c.wpack = at<float>(ws, L.wud);
             c.out = dzp;
             c.yprev = at<float>(ws, Lp.y);
             c.cf_out = at<float4>(ws, Lp.cf);
             c.drop_out = L.pooled_in ? dmask[L.drop_idx] : nullptr;
             c.Hs = L.srcH; c.Ws = L.srcW;
-            const int nblk = L.w4d ? L.nblk4d : L.wino ? L.nblk : (int)conv3x3_nblk(B, L.H, L.W, L.cin);
+            const int nblk = L.wino ? L.nblk : (int)conv3x3_nblk(B, L.H, L.W, L.cin);
             c.part0 = part;
             c.part1 = part + (size_t)L.cin * nblk;
             c.nblk = nblk;
@@ -499,8 +475,7 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
                         c.dpool = dzp;
                     }
                 }
-                RC(L.w4d ? launch_conv3x3_wino4(PRO_RAW, epi, c, s)
-                         : L.wino ? launch_conv3x3_wino(PRO_RAW, epi, c, s) : launch_conv3x3_dma(PRO_RAW, epi, c, s));
+                RC(L.wino ? launch_conv3x3_wino(PRO_RAW, epi, c, s) : launch_conv3x3_dma(PRO_RAW, epi, c, s));
             }
             RC(bwd_finalize(l - 1, nblk, (double)B * Lp.H * Lp.W));
         }

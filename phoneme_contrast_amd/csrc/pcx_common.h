@@ -66,3 +66,54 @@ __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<floa
 inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
 }  // namespace pcx
+
+// ---------------------------------------------------------------- A/B alternates (analysis builds only)
+// The measured-and-superseded alternates of the product kernels (the round-4/5 A/B comparisons in DESIGN.md)
+// are compile-time switches: `make AB="-DPCX_AB_NO_WGBD=1"` builds a library that takes the old path.  The
+// shipped libpcx.so is built with every one at its default and reads no environment variable that selects a
+// kernel or changes numerics (PCX_ROCTX only names profiler ranges).
+#ifndef PCX_AB_WINO_SLOT          // 1: static blockIdx unit order in conv_wino (no XCD-contiguous slots)
+#define PCX_AB_WINO_SLOT 0
+#endif
+#ifndef PCX_AB_NO_WINO_X4         // 1: dword operand copies instead of 16-byte LDS-DMA in conv_wino
+#define PCX_AB_NO_WINO_X4 0
+#endif
+#ifndef PCX_AB_NO_WINO_QUEUE      // 1: static unit order instead of the per-XCD work queue
+#define PCX_AB_NO_WINO_QUEUE 0
+#endif
+#ifndef PCX_AB_NO_POOLSEL         // 1: pooled data gradients re-read the producer's full-resolution windows
+#define PCX_AB_NO_POOLSEL 0
+#endif
+#ifndef PCX_AB_NO_POOLDZ          // 1: no pooled gradient hand-over to layers 2 / 4 (dz written at full size)
+#define PCX_AB_NO_POOLDZ 0
+#endif
+#ifndef PCX_AB_NO_WGBD            // 1: layer 2's weight and data gradients as two kernels
+#define PCX_AB_NO_WGBD 0
+#endif
+#ifndef PCX_AB_WGBD_UNPAIRED      // 1: wgbd blocks walk their own task runs (no XCD-paired strips)
+#define PCX_AB_WGBD_UNPAIRED 0
+#endif
+#ifndef PCX_AB_POOL_NI            // pixel quads per thread and pass in bn_relu_pool
+#define PCX_AB_POOL_NI 2
+#endif
+#ifndef PCX_AB_NHWC_ROWS1         // 1: the channel-last writer steps one image row at a time
+#define PCX_AB_NHWC_ROWS1 0
+#endif
+#ifndef PCX_AB_NO_CONVN_HALO      // 1: per-tap channel-last bf16 conv instead of the halo-staged one
+#define PCX_AB_NO_CONVN_HALO 0
+#endif
+#ifndef PCX_AB_CONVN_NW           // 4 / 8: force the halo kernel's waves per block (0: by shape)
+#define PCX_AB_CONVN_NW 0
+#endif
+#ifndef PCX_AB_CHAN_TARGET        // blocks of the channel-reduction passes
+#define PCX_AB_CHAN_TARGET 16384
+#endif
+#ifndef PCX_AB_BN_ROWTILE         // 1: BN apply passes as row tiles instead of flat 16-byte streams
+#define PCX_AB_BN_ROWTILE 0
+#endif
+#ifndef PCX_AB_NO_WINO_SPAN       // 1: narrow cnn_deep blocks on the direct conv (no batch-spanning Winograd)
+#define PCX_AB_NO_WINO_SPAN 0
+#endif
+#ifndef PCX_AB_NO_EPSUMS          // 1: the BN-backward sums of the channel-last data gradient as a separate pass
+#define PCX_AB_NO_EPSUMS 0
+#endif

@@ -140,11 +140,6 @@ struct Layer {  // one 3x3 conv of the trunk (L = 1..6)
     bool wgbd;             // weight AND data gradient in one kernel (wgbd_wino.hip: layer 2, W % 4 == 0)
     WinoBwdArgs wb;
     bool pd;               // wgbd: dz read as layer 3's pooled gradient + window selection (EPI_BWD_POOLSELP)
-    // Winograd F(4x3) conv (conv_wino4.hip) for the forward / the data gradient where its geometry and the
-    // epilogue fit; weights packed [cout / 32][cin][32][36] into wu4 / wud4; BN partials per 64-tile block
-    bool w4f, w4d;
-    size_t wu4, wud4;
-    int nblk4f, nblk4d;
 };
 
 struct DeepPlan;  // deep.hip

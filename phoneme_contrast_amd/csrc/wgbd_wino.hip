@@ -556,8 +556,8 @@ bool wgbd_wino_geometry(int B, int H, int W, int C, WinoBwdArgs* a) {
         const int want = std::min(num_cus(), a->ntask);  // one block per CU
         a->per_slice = ceil_div(a->ntask, want);
         a->nslice = ceil_div(a->ntask, a->per_slice);
-        // XCD-paired strips (PCX_WGBD_UNPAIRED=1: each block walks its own run of tasks)
-        static const bool unpaired = getenv("PCX_WGBD_UNPAIRED") && atoi(getenv("PCX_WGBD_UNPAIRED"));
+        // XCD-paired strips (PCX_AB_WGBD_UNPAIRED: each block walks its own run of tasks)
+        constexpr bool unpaired = PCX_AB_WGBD_UNPAIRED;
         a->paired = !unpaired && nseg == 2 && a->nslice % 16 == 0 && a->nslice * a->per_slice == a->ntask;
     }
     return true;

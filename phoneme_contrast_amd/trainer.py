@@ -257,11 +257,12 @@ class ContrastiveTrainer:
             if cost is not None:
                 fl, by, peak, xfl = cost
                 per = seconds / steps
-                # mfma_fraction on the FLOPs the step executes (Winograd kernels: 16 multiplies per 2x2
-                # outputs); the direct-conv-equivalent rate beside it
-                rec.update({"step_tflops": round(xfl / per / 1e12, 2), "step_gbps": round(by / per / 1e9, 1),
-                            "mfma_fraction": round(xfl / per / (peak * 1e12), 4),
-                            "alg_equiv_mfma_fraction": round(fl / per / (peak * 1e12), 4),
+                # schema 2: mfma_fraction on the algorithmic (direct-conv) FLOPs, as bench.py; the FLOPs the
+                # step executes (Winograd kernels: 16 multiplies per 2x2 output tile) as executed_mfma_fraction
+                rec.update({"schema": 2, "step_tflops": round(xfl / per / 1e12, 2),
+                            "step_gbps": round(by / per / 1e9, 1),
+                            "mfma_fraction": round(fl / per / (peak * 1e12), 4),
+                            "executed_mfma_fraction": round(xfl / per / (peak * 1e12), 4),
                             "hbm_fraction": round(by / per / (HBM_PEAK_GBS * 1e9), 4),
                             "cost_model": "phoneme_contrast_amd/costs.py (SURVEY 8(d)); last batch shape "
                                           f"{list(shape)}"})

@@ -104,8 +104,9 @@ def test_perf_json_layout():
     assert e0["ms_per_step"] == 50.0 and e0["samples_per_s"] == 81920.0
     # executed FLOPs: the Winograd convs of layers 2-6 at 4/9 of their direct-conv count
     assert abs(e0["step_tflops"] - 3267966795776 / 0.05 / 1e12) < 0.01
-    assert abs(e0["mfma_fraction"] - 3267966795776 / 0.05 / 157.3e12) < 1e-4
-    assert abs(e0["alg_equiv_mfma_fraction"] - 7294498635776 / 0.05 / 157.3e12) < 1e-4
+    assert e0["schema"] == 2
+    assert abs(e0["executed_mfma_fraction"] - 3267966795776 / 0.05 / 157.3e12) < 1e-4
+    assert abs(e0["mfma_fraction"] - 7294498635776 / 0.05 / 157.3e12) < 1e-4
     assert 0 < e0["hbm_fraction"] < 1
 
 

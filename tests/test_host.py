@@ -135,3 +135,23 @@ def test_deep_precision_option():
     assert PhonemeNetDeep({"precision": "bf16"})._net_config().conv_bf16 == 1
     with pytest.raises(ValueError):
         PhonemeNetDeep({"precision": "fp8"})
+
+
+def test_executed_fraction_follows_the_routing():
+    """costs.py prices each Winograd kernel at the multiplies it executes (16 per 2 x 2 tile, partial tiles
+    whole) and routes the weight gradient as csrc/wgrad_wino.hip wgrad_wino_geometry() does: single-float
+    staging only where the image fits one <= 15-tile strip with >= 75 % of the tiles' outputs real (5 x 25,
+    7 x 27, 9 x 29), never at cnn_small T = 201 layer 2 (40 x 201) nor 3 x 13 (70 %)."""
+    from phoneme_contrast_amd import costs as c
+    assert c.wino_tile_fraction(40, 200) == 4 / 9
+    assert abs(c.wino_tile_fraction(5, 25) - 16 * 3 * 13 / (9 * 125)) < 1e-12
+    routed = {(40, 201, 32, 32): False, (5, 25, 256, 256): True, (3, 13, 512, 512): False, (10, 151, 32, 32): False,
+              (7, 27, 32, 32): True, (21, 101, 32, 64): False, (20, 100, 64, 64): True, (10, 50, 128, 128): True,
+              (40, 200, 32, 32): True, (11, 31, 32, 32): False, (9, 29, 32, 32): True}
+    for (H, W, ci, co), want in routed.items():
+        assert c.wgrad_wino_routed(H, W, ci, co) == want, (H, W, ci, co)
+    assert c.executed_fraction("wgrad_L2", 201) == 1.0 and c.executed_fraction("wgrad_L2", 200) == 4 / 9
+    assert c.executed_fraction("conv_fwd_L2", 201) == c.wino_tile_fraction(40, 201)
+    assert c.deep_executed_fraction("wgrad_L6", 40, 200) == c.wino_tile_fraction(5, 25)
+    assert c.deep_executed_fraction("wgrad_L8", 40, 200) == 1.0
+    assert c.deep_executed_fraction("conv_fwd_L8", 40, 200) == c.wino_tile_fraction(3, 13)

@@ -84,6 +84,7 @@ WW_CASES = [  # H, W, cin, cout, B, reps, prologue, pooled dz
     (5, 25, 256, 256, 24, 1, 0, 0),
     (5, 25, 64, 96, 23, 1, 1, 0),
     (7, 27, 32, 32, 5, 1, 1, 0),
+    (9, 29, 32, 32, 7, 1, 1, 0),  # the widest single-float image the staging capacity admits (15 tile columns)
 ]
 
 
@@ -115,27 +116,3 @@ def test_row_window_wgrad_matches_pixel_stream(case):
     r = subprocess.run([WS] + [str(v) for v in case], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, (case, r.stdout, r.stderr)
     assert " w32: " in r.stdout, r.stdout
-
-
-W4 = os.path.join(ROOT, "tools", "wino4_bench")
-W4_CASES = [  # H, W, cin, cout, B, reps, epilogue, prologue: F(4x3) (conv_wino4) vs F(2x2) (conv_wino)
-    (40, 200, 32, 32, 48, 1, 0, 1),    # cnn_small L2 forward (BN + ReLU prologue, statistics); batch ends inside a unit
-    (40, 201, 32, 32, 24, 1, 0, 1),    # T = 201: a partial last tile column
-    (20, 100, 32, 64, 40, 1, 0, 0),    # L3 forward on the pooled input; tile rows of the next sample in a wave
-    (20, 100, 64, 64, 24, 1, 1, 0),    # L4 data gradient through ReLU
-    (21, 100, 64, 64, 9, 1, 1, 0),     # odd H: a partial last tile row
-    (20, 100, 64, 32, 17, 1, 5, 0),    # L3 data gradient -> layer 2's pooled hand-over (EPI_BWD_POOLSELP)
-    (10, 50, 128, 128, 24, 1, 0, 1),   # L6 forward: 10 rows = 2.5 tile rows
-    (10, 50, 128, 64, 24, 1, 5, 0),    # L5 data gradient -> layer 4's pooled hand-over
-    (40, 201, 32, 32, 5, 1, 1, 0),     # T = 201 layer 2 data gradient (no fused backward at odd widths)
-]
-
-
-@pytest.mark.parametrize("case", W4_CASES)
-def test_winograd_f43_matches_f22(case):
-    """The F(4x3) conv's outputs and per-channel statistics sums agree with the F(2x2) engine on the same
-    operands (two exact-arithmetic algorithms in float32: <= 3e-5 of max|out|), and its work queue is left zero."""
-    assert os.path.exists(W4), "tools/wino4_bench missing: run make"
-    r = subprocess.run([W4] + [str(v) for v in case], capture_output=True, text=True, timeout=120)
-    print(r.stdout)
-    assert r.returncode == 0, (case, r.stdout, r.stderr)

@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC passes over the channel-last conv micro-benchmark (halo kernel at the block-0 shape, or the per-tap
-# kernel with PCX_CONVN_HALO=0); one counter group per run.  Analysis aid: gpurun_out/convn_halo_pmc/
+# kernel in a library built with make AB=-DPCX_AB_NO_CONVN_HALO=1); one counter group per run.  Analysis aid: gpurun_out/convn_halo_pmc/
 export TMPDIR=/tmp
 ROOT=$(pwd)
 OUT=gpurun_out/convn_halo_pmc${TAG:-}

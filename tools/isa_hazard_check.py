@@ -76,11 +76,17 @@ def scan(lines):
     return found
 
 
-BITCAST_SUB = re.compile(r"__builtin_bit_cast\s*\(\s*[^,()]+(?:\([^()]*\))?\s*,\s*([A-Za-z_][\w.]*\s*(?:\[[^\]]*\]\s*)+)\)")
+# operand = a subscripted lvalue (v[i], v[m][2]) or a vector-lane accessor (v.x / .y / .z / .w, .r-.a, .s0-.sF,
+# .hi / .lo / .even / .odd): both name an ext_vector_type element (tools/bitcast_lane_probe.cpp has each form)
+BITCAST_SUB = re.compile(r"__builtin_bit_cast\s*\(\s*[^,()]+(?:\([^()]*\))?\s*,\s*("
+                         r"[A-Za-z_][\w.]*\s*(?:\[[^\]]*\]\s*)+"
+                         r"|[A-Za-z_][\w]*(?:\s*\[[^\]]*\])*(?:\.\w+)*\.(?:[xyzwrgba]|s[0-9a-fA-F]+|hi|lo|even|odd)\s*"
+                         r")\)")
 
 
 def scan_bitcast_lanes(dirs):
-    """(file, line, text) of every __builtin_bit_cast whose operand is a subscripted lvalue."""
+    """(file, line, text) of every __builtin_bit_cast whose operand is a subscripted lvalue or a vector-lane
+    accessor."""
     found = []
     for d in dirs:
         for path in sorted(glob.glob(os.path.join(d, "*.hip")) + glob.glob(os.path.join(d, "*.h")) +
@@ -101,7 +107,7 @@ def main():
         dirs = sys.argv[2:] or [os.path.join(root, "phoneme_contrast_amd", "csrc"), os.path.join(root, "tools")]
         bad = scan_bitcast_lanes(dirs)
         for path, n, text in bad:
-            print(f"{os.path.relpath(path)}:{n}: bit_cast of a subscripted lvalue: {text}")
+            print(f"{os.path.relpath(path)}:{n}: bit_cast of a vector-element lvalue: {text}")
         print(f"{len(bad)} bit_cast lane finding(s)")
         return 1 if bad else 0
     bdir = sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(os.path.dirname(

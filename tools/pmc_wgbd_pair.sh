@@ -1,12 +1,12 @@
 #!/bin/bash
 # Analysis aid: L2-miss / write bytes of the fused layer-2 backward (wgbd_wino, pooled dz, B = 4096)
-# with the XCD-paired strips and without (PCX_WGBD_UNPAIRED=1), plus standalone timing; one counter per pass
+# with the XCD-paired strips and without (a library built with make AB=-DPCX_AB_WGBD_UNPAIRED=1), plus standalone timing; one counter per pass
 set -o pipefail
 cd "$(dirname "$0")"; mkdir -p ../gpurun_out
 export TMPDIR=/tmp
 OUT=$PWD/../gpurun_out/pmc_wgbd_pair; rm -rf $OUT; mkdir -p $OUT
 for mode in p u; do
-  envs=""; [ $mode = u ] && envs="PCX_WGBD_UNPAIRED=1"
+  envs=""  # (mode u: run against a library built with make AB=-DPCX_AB_WGBD_UNPAIRED=1)
   for c in FETCH_SIZE WRITE_SIZE; do
     env $envs timeout -s KILL 90 rocprofv3 --pmc $c -f csv -d $OUT/$mode$c -o run -- ./wb_bench 40 200 4096 2 1 > $OUT/$mode$c.log 2>&1 || { echo "pass $mode $c failed"; tail -5 $OUT/$mode$c.log; exit 1; }
   done

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Analysis aid: L2-miss (FETCH_SIZE) / write bytes and L2 hit rate of the Winograd forward of layer 2
 # (40 x 200, 32 -> 32, BN + ReLU prologue) at B = 4096 under three unit orders: s = static XCD-contiguous,
-# n = static blockIdx order (PCX_WINO_SLOT=1), q = per-XCD work queue (WINO_QUEUE=1); one counter group
+# n = static blockIdx order (a library built with make AB=-DPCX_AB_WINO_SLOT=1), q = per-XCD work queue (WINO_QUEUE=1); one counter group
 # per rocprofv3 pass.  SHAPE / MODES override.
 set -o pipefail
 cd "$(dirname "$0")"; mkdir -p ../gpurun_out
@@ -10,7 +10,7 @@ OUT=$PWD/../gpurun_out/pmc_wino_l2; rm -rf $OUT; mkdir -p $OUT
 SHAPE=${SHAPE:-"40 200 32 32 4096"}
 for mode in ${MODES:-s n q}; do
   envs=""
-  [ $mode = n ] && envs="PCX_WINO_SLOT=1"
+  # (mode n: run against a library built with make AB=-DPCX_AB_WINO_SLOT=1)
   [ $mode = q ] && envs="WINO_QUEUE=1"
   i=0
   for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
