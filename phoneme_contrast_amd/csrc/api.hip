@@ -74,24 +74,24 @@ extern "C" int pcx_dropout_masks(float* out, int64_t n, float p, uint64_t seed, 
     return PCX_OK;
 }
 
-// HBM probe (bench.py measured_peaks): dst = src, 16 bytes per lane, each lane moving 4 x 16 B of consecutive
-// 4 KB blocks per pass (all four loads issued before the stores), nontemporal; grid = 8 workgroups of 256 per
-// CU.  The achievable streaming rate an HBM-bound kernel is judged against (MI355X_MICROARCH.md: ~6.3 TB/s for
+// HBM probe (bench.py measured_peaks): dst = src, 16 bytes per lane, each lane moving 8 x 16 B of consecutive
+// 4 KB blocks per pass (all eight loads issued before the stores), nontemporal; grid = 16 workgroups of 256
+// per CU (the best of the variants tools/copy_probe.hip times: 5.68-5.75 TB/s on MI355X).  The achievable streaming rate an HBM-bound kernel is judged against (MI355X_MICROARCH.md: ~6.3 TB/s for
 // a float4 copy), in place of torch's copy_.
 namespace {
 typedef float sc_f4 __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void stream_copy_kernel(const sc_f4* __restrict__ src, sc_f4* __restrict__ dst,
                                                          int64_t n4) {
-    const int64_t stride = (int64_t)gridDim.x * 1024;
-    for (int64_t base = (int64_t)blockIdx.x * 1024 + threadIdx.x; base < n4; base += stride) {
-        sc_f4 v[4];
+    const int64_t stride = (int64_t)gridDim.x * 2048;
+    for (int64_t base = (int64_t)blockIdx.x * 2048 + threadIdx.x; base < n4; base += stride) {
+        sc_f4 v[8];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < 8; ++k) {
             const int64_t i = base + 256 * k;
             if (i < n4) v[k] = __builtin_nontemporal_load(src + i);
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < 8; ++k) {
             const int64_t i = base + 256 * k;
             if (i < n4) __builtin_nontemporal_store(v[k], dst + i);
         }
@@ -106,7 +106,7 @@ extern "C" int pcx_stream_copy(const void* src, void* dst, size_t bytes, hipStre
                   "stream_copy: 16-byte aligned buffers and sizes required");
     const int64_t n4 = (int64_t)(bytes / 16);
     if (n4 == 0) return PCX_OK;
-    const int64_t blocks = std::min<int64_t>(ceil_div(n4, 1024), (int64_t)8 * num_cus());
+    const int64_t blocks = std::min<int64_t>(ceil_div(n4, 2048), (int64_t)16 * num_cus());
     stream_copy_kernel<<<(unsigned)blocks, 256, 0, stream>>>(static_cast<const sc_f4*>(src),
                                                             static_cast<sc_f4*>(dst), n4);
     PCX_LAUNCH_CHECK("stream_copy_kernel");

@@ -20,7 +20,11 @@ void tile_shape(int cout, int* wm, int* wn) {
 typedef const __attribute__((address_space(4))) float* cfloat4p;  // constant space: scalar loads
 
 // ------------------------------------------------------------------ Cin = 1 first conv
-constexpr int C1_CPW = 8;  // output channels per wave
+constexpr int C1W_CPW = 8;  // output channels per wave (register weight gradient)
+constexpr int C1F_CPW = 8;  // output channels per wave (forward)
+#ifndef PCX_AB_C1_NT
+#define PCX_AB_C1_NT 1      // nontemporal y1 stores (same-box A/B: 0.917 -> 0.879 ms; 0: plain stores)
+#endif
 
 // 3 x 6 input window of a pixel quad (columns w0 - 1 .. w0 + 4, rows hh - 1 .. hh + 1), zero outside
 // the sample.  FULL: W % 4 == 0 (16-byte row quads; no partial quad)
@@ -83,29 +87,29 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Args a) {
     const int r1 = min(nrows, r0 + a.rows_per_blk);
     const int nq = (a.W + 3) >> 2;
     const int ntask = (r1 - r0) * nq;
-    for (int cg = wave * C1_CPW; cg < a.cout; cg += 4 * C1_CPW) {
-        float wt[C1_CPW][9];
+    for (int cg = wave * C1F_CPW; cg < a.cout; cg += 4 * C1F_CPW) {
+        float wt[C1F_CPW][9];
 #pragma unroll
-        for (int j = 0; j < C1_CPW; ++j)
+        for (int j = 0; j < C1F_CPW; ++j)
 #pragma unroll
             for (int t = 0; t < 9; ++t) wt[j][t] = a.w[(cg + j) * 9 + t];
         // shift for the one-pass variance: the output at the block's first pixel
-        float K[C1_CPW];
+        float K[C1F_CPW];
         {
             const int b = r0 / a.H, hh = r0 - b * a.H;
             float xr[3][6];
             c1_window<false>(a.x + (int64_t)b * HW, a.H, a.W, hh, 0, xr);
 #pragma unroll
-            for (int j = 0; j < C1_CPW; ++j) {
+            for (int j = 0; j < C1F_CPW; ++j) {
                 float v = 0.f;
 #pragma unroll
                 for (int t = 0; t < 9; ++t) v = fmaf(wt[j][t], xr[t / 3][1 + t % 3 - 1], v);
                 K[j] = v;
             }
         }
-        float s1[C1_CPW], s2[C1_CPW];
+        float s1[C1F_CPW], s2[C1F_CPW];
 #pragma unroll
-        for (int j = 0; j < C1_CPW; ++j) s1[j] = s2[j] = 0.f;
+        for (int j = 0; j < C1F_CPW; ++j) s1[j] = s2[j] = 0.f;
         // FULL: the next quad's window is loaded before this quad's stores are issued, so waiting for
         // it never waits for the stores (vmcnt counts both, in issue order)
         float xn[3][6];
@@ -138,7 +142,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Args a) {
             }
             float* ob = a.out + ((int64_t)b * a.cout + cg) * HW + (int64_t)hh * a.W + w0;
 #pragma unroll
-            for (int j = 0; j < C1_CPW; ++j) {
+            for (int j = 0; j < C1F_CPW; ++j) {
                 float v[4];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
@@ -148,7 +152,12 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Args a) {
                     v[e] = acc;
                 }
                 if (FULL) {
-                    st4(ob + (int64_t)j * HW, make_float4(v[0], v[1], v[2], v[3]));
+                    if constexpr (PCX_AB_C1_NT) {
+                        typedef float nf4 __attribute__((ext_vector_type(4)));
+                        __builtin_nontemporal_store(nf4{v[0], v[1], v[2], v[3]}, reinterpret_cast<nf4*>(ob + (int64_t)j * HW));
+                    } else {
+                        st4(ob + (int64_t)j * HW, make_float4(v[0], v[1], v[2], v[3]));
+                    }
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         const float d = v[e] - K[j];
@@ -169,7 +178,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Args a) {
         }
         const float n = (float)((r1 - r0) * a.W);
 #pragma unroll
-        for (int j = 0; j < C1_CPW; ++j) {
+        for (int j = 0; j < C1F_CPW; ++j) {
             float t1 = wave_sum(s1[j]), t2 = wave_sum(s2[j]);
             if (lane == 0) {
                 a.part0[(int64_t)(cg + j) * a.nblk + blockIdx.x] = n * K[j] + t1;
@@ -197,19 +206,19 @@ __global__ __launch_bounds__(256) void wgrad1_kernel(Wgrad1Args a) {
     const int r1 = min(nrows, r0 + a.rows_per_slice);
     const int nq = (a.W + 3) >> 2;
     const int ntask = (r1 - r0) * nq;
-    for (int cg = wave * C1_CPW; cg < a.cout; cg += 4 * C1_CPW) {
-        float acc[C1_CPW][9];
-        float A1[C1_CPW], A2[C1_CPW], A3[C1_CPW];
-        float wt[RC ? C1_CPW : 1][9];  // wave-uniform: constant-space loads into scalar registers
+    for (int cg = wave * C1W_CPW; cg < a.cout; cg += 4 * C1W_CPW) {
+        float acc[C1W_CPW][9];
+        float A1[C1W_CPW], A2[C1W_CPW], A3[C1W_CPW];
+        float wt[RC ? C1W_CPW : 1][9];  // wave-uniform: constant-space loads into scalar registers
         if constexpr (RC) {
             const cfloat4p wp = (cfloat4p)a.w;
 #pragma unroll
-            for (int j = 0; j < C1_CPW; ++j)
+            for (int j = 0; j < C1W_CPW; ++j)
 #pragma unroll
                 for (int t = 0; t < 9; ++t) wt[j][t] = wp[(cg + j) * 9 + t];
         }
 #pragma unroll
-        for (int j = 0; j < C1_CPW; ++j) {
+        for (int j = 0; j < C1W_CPW; ++j) {
             const float4 k = a.cf_dy[cg + j];  // dy = a (dz - mb - (y - mean) mgi)
             A1[j] = k.x;
             A2[j] = -k.x * k.z;
@@ -225,7 +234,7 @@ __global__ __launch_bounds__(256) void wgrad1_kernel(Wgrad1Args a) {
             c1_window<FULL>(a.x + (int64_t)b * HW, a.H, a.W, hh, w0, xr);
             const int64_t o = ((int64_t)b * a.cout + cg) * HW + (int64_t)hh * a.W + w0;
 #pragma unroll
-            for (int j = 0; j < C1_CPW; ++j) {
+            for (int j = 0; j < C1W_CPW; ++j) {
                 float dz[4], yy[4];
                 if (FULL) {
                     const float4 u = ld4(a.dz + o + (int64_t)j * HW);
@@ -259,12 +268,116 @@ __global__ __launch_bounds__(256) void wgrad1_kernel(Wgrad1Args a) {
             }
         }
 #pragma unroll
-        for (int j = 0; j < C1_CPW; ++j)
+        for (int j = 0; j < C1W_CPW; ++j)
 #pragma unroll
             for (int t = 0; t < 9; ++t) {
                 float v = wave_sum(acc[j][t]);
                 if (lane == 0) a.part[((int64_t)blockIdx.x * a.cout + cg + j) * 9 + t] = v;
             }
+    }
+}
+
+// Round 6: the same weight gradient with dz streamed HBM -> LDS by LDS-DMA (W % 4 == 0, W <= 252).  The
+// register kernel above alternated a wait for each quad's 16-byte loads with its ~650 VALU (1.13 ms at
+// B = 4096: 3.8 TB/s); here a block walks its slice's (sample, row) rows with the next row's 32 dz channel
+// rows and 3 input rows in flight (double-buffered, no VGPRs held) while the current row is computed from
+// LDS.  Thread (channel c = tid >> 3, quad group g = tid & 7) owns one channel: its 9 weights, BN-backward
+// coefficients and 9 accumulators live in registers (no SGPR pressure), quads q = g, g + 8, ... of the row.
+// Arithmetic per output is conv1_fwd_kernel's recompute of y and wgrad1_kernel's dy / tap order, term for
+// term, so each slice's partial sums are the same float operations in the same order as before per pixel;
+// only the slice boundaries (rows per slice) differ.
+constexpr int W1D_CS = 288;             // LDS floats per dz channel row: 1 KB of DMA + 32 floats, so the 8
+                                        // lanes of the next channel read the other 32 banks
+constexpr int W1D_XS = 260;             // LDS floats per input row: [4 zero][W][zeros]
+constexpr int W1D_BUF = 32 * W1D_CS + 3 * W1D_XS;
+
+__device__ __forceinline__ void w1d_dma(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned lds_byte_addr) {
+    const unsigned m0 = __builtin_amdgcn_readfirstlane(lds_byte_addr);
+    asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" :: "v"(voff), "s"(r), "{m0}"(m0) : "memory");
+}
+
+__global__ __launch_bounds__(256) void wgrad1_dma_kernel(Wgrad1Args a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int c = tid >> 3, g = tid & 7;
+    const int H = a.H, W = a.W, HW = H * W, nq = W >> 2;
+    const int nrows = a.B * H;
+    const int r0 = blockIdx.x * a.rows_per_slice, r1 = min(nrows, r0 + a.rows_per_slice);
+    const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)smem;
+    // zero both buffers once: the input rows' left pad (never written by the DMA) reads 0
+    for (int i = tid; i < 2 * W1D_BUF; i += 256) smem[i] = 0.f;
+    float wt[9], acc[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+        wt[t] = a.w[c * 9 + t];
+        acc[t] = 0.f;
+    }
+    const float4 k = a.cf_dy[c];  // dy = a (dz - mb - (y - mean) mgi)
+    const float A1 = k.x, A2 = -k.x * k.z, A3 = k.x * (k.w * k.z - k.y);
+    // DMA of row task gr into buffer buf: 32 dz channel rows (wave w: channels w, w + 4, ...) and the input
+    // rows h - 1 .. h + 1 (waves 0..2); lanes >= W / 4 and rows outside the sample read 0 (out of range)
+    const unsigned lq = (unsigned)lane < (unsigned)nq ? 16u * (unsigned)lane : 0x80000000u;
+    auto issue = [&](int gr, int buf) {
+        const int b = gr / H, h = gr - b * H;
+        const unsigned base = lds0 + 4u * (unsigned)(buf * W1D_BUF);
+        const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(a.dz + ((int64_t)b * 32 * H + h) * W), (short)0, (int)(((int64_t)31 * HW + W) * 4),
+            0x00020000);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int ch = wave + 4 * j;
+            w1d_dma(rd, lq == 0x80000000u ? lq : lq + 4u * (unsigned)(ch * HW), base + 4u * (unsigned)(ch * W1D_CS));
+        }
+        if (wave < 3) {
+            const int y = h - 1 + wave;
+            const bool ok = (unsigned)y < (unsigned)H;
+            const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<float*>(a.x + ((int64_t)b * H + (ok ? y : 0)) * W), (short)0, ok ? W * 4 : 0, 0x00020000);
+            w1d_dma(rx, lq, base + 4u * (unsigned)(32 * W1D_CS + wave * W1D_XS + 4));
+        }
+    };
+    __syncthreads();  // the zeroing is done before any DMA lands
+    if (r0 < r1) issue(r0, 0);
+    for (int gr = r0; gr < r1; ++gr) {
+        const int buf = (gr - r0) & 1;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // row gr landed for every wave; row gr - 1's buffer fully read
+        if (gr + 1 < r1) issue(gr + 1, buf ^ 1);
+        const float* dz = smem + buf * W1D_BUF + c * W1D_CS;
+        const float* xs = smem + buf * W1D_BUF + 32 * W1D_CS + 4;  // input row 0 (= image row h - 1), column 0
+        for (int q = g; q < nq; q += 8) {
+            const int w0 = 4 * q;
+            const float4 u = *reinterpret_cast<const float4*>(dz + w0);
+            float xr[3][6];
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                const float* row = xs + r * W1D_XS + w0;
+                const float4 v = *reinterpret_cast<const float4*>(row);
+                xr[r][0] = row[-1];
+                xr[r][1] = v.x; xr[r][2] = v.y; xr[r][3] = v.z; xr[r][4] = v.w;
+                xr[r][5] = row[4];
+            }
+            const float dzv[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float yv = 0.f;  // conv1_fwd_kernel's arithmetic, term for term
+#pragma unroll
+                for (int tp = 0; tp < 9; ++tp) yv = fmaf(wt[tp], xr[tp / 3][e + tp % 3], yv);
+                const float dy = fmaf(A1, dzv[e], fmaf(A2, yv, A3));
+#pragma unroll
+                for (int tp = 0; tp < 9; ++tp) acc[tp] = fmaf(dy, xr[tp / 3][e + tp % 3], acc[tp]);
+            }
+        }
+    }
+    // the 8 quad groups of a channel are 8 consecutive lanes
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+        float v = acc[t];
+        v += __shfl_xor(v, 1, 64);
+        v += __shfl_xor(v, 2, 64);
+        v += __shfl_xor(v, 4, 64);
+        if (g == 0) a.part[((int64_t)blockIdx.x * 32 + c) * 9 + t] = v;
     }
 }
 
@@ -1727,7 +1840,7 @@ int conv1_nblk(int B, int H, int* rows_per_blk) {
 }
 
 int launch_conv1_fwd(Conv1Args a, hipStream_t s) {
-    PCX_CHECK_ARG(a.cout % (4 * C1_CPW) == 0, "conv1: cout %d must be a multiple of 32", a.cout);
+    PCX_CHECK_ARG(a.cout % (4 * C1F_CPW) == 0, "conv1: cout %d must be a multiple of 16", a.cout);
     PCX_CHECK_ARG((int64_t)a.B * a.H < ((int64_t)1 << 31), "conv1: too many rows");
     if (a.W % 4 == 0)
         conv1_fwd_kernel<true><<<a.nblk, 256, 0, s>>>(a);
@@ -1737,11 +1850,32 @@ int launch_conv1_fwd(Conv1Args a, hipStream_t s) {
     return PCX_OK;
 }
 
+// the LDS-DMA form: 32 output channels, y recomputed, rows of whole 16-byte quads that one wave's DMA covers
+static bool wgrad1_dma_ok(int W, int cout) { return cout == 32 && W % 4 == 0 && W >= 4 && W <= 252; }
+
+int wgrad1_nslice(int B, int H, int W, int cout, int* rows_per_slice) {
+    const int64_t nrows = (int64_t)B * H;
+    // LDS-DMA form: two resident blocks per CU (2 x 78 KB of LDS), each streaming its rows; else ~5 slices
+    // per CU (the register kernel holds 5 waves per SIMD: one round of resident blocks)
+    const int want = (wgrad1_dma_ok(W, cout) ? 2 : 5) * num_cus();
+    *rows_per_slice = (int)std::max<int64_t>(1, (nrows + want - 1) / want);
+    return ceil_div(nrows, *rows_per_slice);
+}
+
 int launch_wgrad1(Wgrad1Args a, hipStream_t s) {
-    PCX_CHECK_ARG(a.cout % (4 * C1_CPW) == 0, "wgrad1: cout must be a multiple of 32");
+    PCX_CHECK_ARG(a.cout % (4 * C1W_CPW) == 0, "wgrad1: cout must be a multiple of %d", 4 * C1W_CPW);
     PCX_CHECK_ARG((int64_t)a.B * a.H < ((int64_t)1 << 31), "wgrad1: too many rows");
     PCX_CHECK_ARG(a.y || a.w, "wgrad1: needs the conv output y or the weights to recompute it");
+    PCX_CHECK_ARG(a.nslice == ceil_div((int64_t)a.B * a.H, a.rows_per_slice), "wgrad1: %d slices of %d rows",
+                  a.nslice, a.rows_per_slice);
     const bool rc = a.y == nullptr;
+    if (rc && wgrad1_dma_ok(a.W, a.cout) && (int64_t)32 * a.H * a.W * 4 < ((int64_t)1 << 31)) {
+        const size_t lds = (size_t)2 * W1D_BUF * 4;
+        (void)hipFuncSetAttribute((const void*)wgrad1_dma_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        wgrad1_dma_kernel<<<a.nslice, 256, lds, s>>>(a);
+        PCX_LAUNCH_CHECK("wgrad1_dma_kernel");
+        return PCX_OK;
+    }
     if (a.W % 4 == 0) {
         if (rc) wgrad1_kernel<true, true><<<a.nslice, 256, 0, s>>>(a);
         else wgrad1_kernel<true, false><<<a.nslice, 256, 0, s>>>(a);

@@ -235,6 +235,8 @@ struct Wgrad1Args {
     int nslice, rows_per_slice;
 };
 int launch_wgrad1(Wgrad1Args a, hipStream_t s);
+// slices of the layer-1 weight gradient for its kernel (rows_per_slice out; nslice returned)
+int wgrad1_nslice(int B, int H, int W, int cout, int* rows_per_slice);
 
 // sum `nslice` partial copies of an n-element array into out (deterministic order)
 int launch_sum_slices(const float* part, int nslice, int64_t n, float* out, hipStream_t s);

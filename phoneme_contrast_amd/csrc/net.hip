@@ -105,9 +105,7 @@ int build_small(Plan& p) {
     }
     // first-layer weight gradient slices
     {
-        int64_t nrows = (int64_t)B * H1;
-        p.wg1_rows = (int)std::max<int64_t>(1, nrows / 1024);
-        p.wg1_nslice = ceil_div(nrows, p.wg1_rows);
+        p.wg1_nslice = wgrad1_nslice(B, H1, W1, 32, &p.wg1_rows);
         wg = std::max(wg, (size_t)p.wg1_nslice * 32 * 9);
     }
     p.C6 = 128;

@@ -56,6 +56,21 @@ def _round_conv_operands(model):
 # (True, 200, None) and (True, 100, [16, 32, ...]) store the odd-width outputs of blocks 2 / 1 as byte
 # ReLU masks under a channel-last next block (the round-3 failure cases); T = 201 is the real-data
 # width (32000-sample clips, reference src/datasets/dataset.py:50): 101 / 51 / 26 / 13-wide blocks
+# Per-case bounds (round 6): ~3x the errors measured on MI355X (gpurun_out/r6a; recorded in
+# profiles/r6_bf16_parity_margins.json), never looser than the round-5 flat bounds (1e-2, 5e-2, 5e-2, 0.98).
+# (emb vs the rounded-operand float64 model, emb vs float64, |loss - float64 loss|, |loss - rounded-operand
+# float64 loss|, min gradient cosine).  The float64 gaps are mostly bf16 rounding itself (it moves the
+# float64 model as much); the rounded-operand columns measure the kernels.
+BF16_STEP_TOL = {
+    (True, 200, None, 32): (7e-3, 3e-2, 1.2e-2, 1e-2, 0.997),
+    (False, 57, None, 32): (1e-2, 5e-2, 5e-2, 1e-2, 0.99),
+    (True, 100, (16, 32, 64, 128), 32): (1e-2, 5e-2, 3.4e-2, 1e-2, 0.994),
+    (True, 100, tuple(FULL), 16): (1e-2, 5e-2, 5e-2, 1e-2, 0.988),
+    (True, 201, tuple(FULL), 16): (6.5e-3, 2.7e-2, 5e-3, 1e-2, 0.987),
+    (True, 201, None, 32): (3.2e-3, 3.2e-2, 1e-3, 1e-2, 0.999),
+}
+
+
 @pytest.mark.parametrize("residual,T,dims,B", [(True, 200, None, 32), (False, 57, None, 32),
                                                (True, 100, [16, 32, 64, 128], 32), (True, 100, FULL, 16),
                                                (True, 201, FULL, 16), (True, 201, None, 32)])
@@ -85,7 +100,8 @@ def test_deep_bf16_step(residual, T, dims, B):
     ref.train()
     rnd.train()
     e_rnd = _torch_reference(rnd, x.double(), md)
-    tp.supcon(e_rnd, labels, 0.15, 0.07).backward()
+    l_rnd = tp.supcon(e_rnd, labels, 0.15, 0.07)
+    l_rnd.backward()
     e_ref = _torch_reference(ref, x.double(), md)
     l_ref = tp.supcon(e_ref, labels, 0.15, 0.07)
     l_ref.backward()
@@ -114,12 +130,16 @@ def test_deep_bf16_step(residual, T, dims, B):
         g, r = p.grad.cpu().double().flatten(), q.grad.flatten()
         cos[k] = (g @ r / (g.norm() * r.norm() + 1e-300)).item()
     worst = min(cos, key=cos.get)
+    dl_ref, dl_rnd = abs(loss.item() - l_ref.item()), abs(loss.item() - l_rnd.item())
     print(f"bf16 residual={residual} T={T} dims={dims} B={B}: emb vs rounded-operand f64 {exact:.2e}, "
-          f"vs f64 {vs_f64:.2e}, |d loss| {abs(loss.item() - l_ref.item()):.2e}, min grad cosine {worst} {cos[worst]:.4f}")
-    assert exact < 1e-2
-    assert vs_f64 < 5e-2
-    assert abs(loss.item() - l_ref.item()) < 5e-2
-    assert cos[worst] > 0.98, (worst, cos[worst])
+          f"vs f64 {vs_f64:.2e}, |d loss| {dl_ref:.2e} (vs rounded-operand {dl_rnd:.2e}), "
+          f"min grad cosine {worst} {cos[worst]:.4f}")
+    t_exact, t_f64, t_loss, t_loss_rnd, t_cos = BF16_STEP_TOL[(residual, T, tuple(dims) if dims else None, B)]
+    assert exact < t_exact
+    assert vs_f64 < t_f64
+    assert dl_ref < t_loss
+    assert dl_rnd < t_loss_rnd
+    assert cos[worst] > t_cos, (worst, cos[worst])
     for (k, v), (_, w) in zip(m.state_dict().items(), rnd.state_dict().items()):
         if "running" in k:
             assert torch.allclose(v.cpu().double(), w, rtol=1e-2, atol=1e-3), k
@@ -157,8 +177,8 @@ def test_deep_bf16_b512_full_width_matches_rounded_f64(T):
     """cnn_deep bf16 (config 5's model, full widths 64..512) at B = 512, against the rounded-operand
     float64 reference evaluated on the GPU (torch im2col + rocBLAS in float64, MIOpen off): the
     persistent channel-last engine, its epilogue BN partials (forward mode 0, data-gradient mode 1) and
-    the multi-block channel reductions at a batch where every grid runs many rounds.  Same tolerances as
-    the small-batch cases above; the measured margins go to the full-size JSON record (profiles/).
+    the multi-block channel reductions at a batch where every grid runs many rounds.  Bounds ~3x the
+    measured errors (round 6); the measured margins go to the full-size JSON record (profiles/).
     Reference: src/models/phoneme_cnn.py:146-216, 274-304; T = 201: src/datasets/dataset.py:50."""
     import gc
     import json
@@ -219,8 +239,8 @@ def test_deep_bf16_b512_full_width_matches_rounded_f64(T):
     rec = {"B": B, "T": T, "emb_vs_rounded_f64": exact, "emb_vs_f64": vs_f64, "loss_vs_f64": abs(lgot - l_ref),
            "loss_vs_rounded_f64": abs(lgot - l_rnd), "min_grad_cosine": cos[worst], "min_grad_cosine_tensor": worst,
            "grad_cosine": cos, "running_stats_maxrel": rstat,
-           "tolerances": {"emb_vs_rounded_f64": 1e-2, "emb_vs_f64": 5e-2, "loss_vs_f64": 5e-2, "grad_cosine": 0.98,
-                          "running_stats": "rtol 1e-2, atol 1e-3"}}
+           "tolerances": {"emb_vs_rounded_f64": 1e-2, "emb_vs_f64": 3e-2, "loss_vs_f64": 5e-3,
+                          "loss_vs_rounded_f64": 5e-3, "grad_cosine": 0.99, "running_stats": "rtol 1e-2, atol 1e-3"}}
     print(f"\nFULLSIZE cnn_deep_bf16_B512_T{T} " + json.dumps(rec, sort_keys=True))
     path = os.environ.get("PCX_FULLSIZE_JSON", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                               "gpurun_out", "fullsize_parity.json"))
@@ -233,9 +253,11 @@ def test_deep_bf16_b512_full_width_matches_rounded_f64(T):
     allrec[f"cnn_deep_bf16_B512_T{T}"] = rec
     with open(path, "w") as f:
         json.dump(allrec, f, indent=1, sort_keys=True)
+    # (round 6: ~3x the measured B = 512 errors -- emb 1.1e-2 vs f64, loss 1.1e-3, cosine >= 0.9957)
     assert exact < 1e-2
-    assert vs_f64 < 5e-2
-    assert abs(lgot - l_ref) < 5e-2
-    assert cos[worst] > 0.98, (worst, cos[worst])
+    assert vs_f64 < 3e-2
+    assert abs(lgot - l_ref) < 5e-3
+    assert abs(lgot - l_rnd) < 5e-3
+    assert cos[worst] > 0.99, (worst, cos[worst])
     for k in s_rnd:
         assert torch.allclose(run_stats[k], s_rnd[k], rtol=1e-2, atol=1e-3), k
