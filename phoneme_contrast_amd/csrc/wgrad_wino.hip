@@ -30,6 +30,8 @@
 //    cover the 64 banks once).  Strips of <= 50 tiles keep the block at <= 80 KB: two blocks per CU.
 //  * per-slice partials [slice][cout][cin][16], summed in a fixed order by wgrad_wino_reduce
 //    (float64): deterministic.
+#include <type_traits>
+
 #include "kernels.h"
 
 namespace pcx {
@@ -178,194 +180,227 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
     unsigned pav[NIT];  // PD: the items' two selection bytes (their two pooled gradients wait in dzv[m][0..1])
     const int Wp = W >> 1, HWp = (H >> 1) * Wp;
 
-    for (int task = t0s; task < t1s; ++task) {
+    // per-task state: the sample's buffer resources and the items' column validity (whole vectors: V
+    // divides W and 2 t0)
+    struct Task {
+        int c0;
+        __amdgpu_buffer_rsrc_t rdz, rpa, ry, rdo, rx;
+        unsigned dcol, xcol;
+    };
+    auto task_of = [&](int task) {
+        Task t;
         const int b = task / a.nseg;
         const int t0 = (task - b * a.nseg) * a.S;
-        const int c0 = 2 * t0;
-        const __amdgpu_buffer_rsrc_t rdz = PD ? rsrc(a.dzpool + ((int64_t)b * a.cout + co0) * HWp, (int64_t)32 * HWp * 4)
-                                              : rsrc(a.dz + ((int64_t)b * a.cout + co0) * HW, (int64_t)32 * HW * 4);
-        const __amdgpu_buffer_rsrc_t rpa =
-            rsrc(reinterpret_cast<const float*>(PD ? a.parg + ((int64_t)b * a.cout + co0) * HWp : nullptr),
-                 PD ? (int64_t)32 * HWp : 0);
-        const __amdgpu_buffer_rsrc_t ry = rsrc(a.y + ((int64_t)b * a.cout + co0) * HW, (int64_t)32 * HW * 4);
-        const __amdgpu_buffer_rsrc_t rdo =
-            rsrc(write_dy ? a.dy_out + ((int64_t)b * a.cout + co0) * HW : a.dz, write_dy ? (int64_t)32 * HW * 4 : 0);
-        const __amdgpu_buffer_rsrc_t rx = rsrc(a.src + ((int64_t)b * a.cin + ci0) * HW, (int64_t)32 * HW * 4);
-        // per-task column validity of the items (whole vectors: V divides W and 2 t0)
+        t.c0 = 2 * t0;
+        t.rdz = PD ? rsrc(a.dzpool + ((int64_t)b * a.cout + co0) * HWp, (int64_t)32 * HWp * 4)
+                   : rsrc(a.dz + ((int64_t)b * a.cout + co0) * HW, (int64_t)32 * HW * 4);
+        t.rpa = rsrc(reinterpret_cast<const float*>(PD ? a.parg + ((int64_t)b * a.cout + co0) * HWp : nullptr),
+                     PD ? (int64_t)32 * HWp : 0);
+        t.ry = rsrc(a.y + ((int64_t)b * a.cout + co0) * HW, (int64_t)32 * HW * 4);
+        t.rdo = rsrc(write_dy ? a.dy_out + ((int64_t)b * a.cout + co0) * HW : a.dz, write_dy ? (int64_t)32 * HW * 4 : 0);
+        t.rx = rsrc(a.src + ((int64_t)b * a.cin + ci0) * HW, (int64_t)32 * HW * 4);
         unsigned dcol = 0, xcol = 0;
 #pragma unroll
         for (int i = 0; i < NIT; ++i) {
             const int kc = V * (j0 + 8 * (i % NIR));
-            dcol |= (unsigned)(c0 + kc < W) << i;
-            xcol |= (unsigned)((unsigned)(c0 + kc - V) < (unsigned)W) << i;
+            dcol |= (unsigned)(t.c0 + kc < W) << i;
+            xcol |= (unsigned)((unsigned)(t.c0 + kc - V) < (unsigned)W) << i;
         }
-        dcol &= dex;
-        xcol &= xex;
+        t.dcol = dcol & dex;
+        t.xcol = xcol & xex;
+        return t;
+    };
 
-        // stage st (= -1 .. TR - 1): dy rows 2 st, 2 st + 1 and x rows 2 st + 1, 2 st + 2
-        constexpr unsigned R1 = ((1u << NIR) - 1) << NIR;  // items of the stage's second row
-        auto masks = [&](int st, unsigned& dm, unsigned& xm) {
-            const bool d0 = 2 * st >= 0, d1 = 2 * st + 1 >= 0 && 2 * st + 1 < H;
-            const bool x0 = 2 * st + 1 >= 0 && 2 * st + 1 < H, x1 = 2 * st + 2 < H;
-            dm = dcol & ((d0 ? ~R1 : 0u) | (d1 ? R1 : 0u));
-            xm = xcol & ((x0 ? ~R1 : 0u) | (x1 ? R1 : 0u));
-        };
-        auto dgo = [&](int i) { return dgb + (i / NIR) * W + 8 * V * (i % NIR); };
-        auto xgo = [&](int i) { return xgb + (i / NIR) * W + 8 * V * (i % NIR); };
-        // part: only the items m with m NPT / NIT == part (-1: all items)
-        auto load_dy = [&](int st, int part) {
-            unsigned dm, xm;
-            masks(st, dm, xm);
-            int db = 2 * st * W + c0 + dgb;
-            asm volatile("" : "+v"(db));  // opaque: per-item offsets formed at the load, not kept live
-            int pb = ch * HWp + st * Wp + ((c0 + V * j0) >> 1);  // PD: pooled row st (dy rows 2 st, 2 st + 1)
-            if constexpr (PD) asm volatile("" : "+v"(pb));
+    // stage st (= -1 .. TR - 1): dy rows 2 st, 2 st + 1 and x rows 2 st + 1, 2 st + 2
+    constexpr unsigned R1 = ((1u << NIR) - 1) << NIR;  // items of the stage's second row
+    auto masks = [&](const Task& t, int st, unsigned& dm, unsigned& xm) {
+        const bool d0 = 2 * st >= 0, d1 = 2 * st + 1 >= 0 && 2 * st + 1 < H;
+        const bool x0 = 2 * st + 1 >= 0 && 2 * st + 1 < H, x1 = 2 * st + 2 < H;
+        dm = t.dcol & ((d0 ? ~R1 : 0u) | (d1 ? R1 : 0u));
+        xm = t.xcol & ((x0 ? ~R1 : 0u) | (x1 ? R1 : 0u));
+    };
+    auto dgo = [&](int i) { return dgb + (i / NIR) * W + 8 * V * (i % NIR); };
+    auto xgo = [&](int i) { return xgb + (i / NIR) * W + 8 * V * (i % NIR); };
+    // part: only the items m with m NPT / NIT == part (-1: all items)
+    auto load_dy = [&](const Task& t, int st, int part) {
+        unsigned dm, xm;
+        masks(t, st, dm, xm);
+        int db = 2 * st * W + t.c0 + dgb;
+        asm volatile("" : "+v"(db));  // opaque: per-item offsets formed at the load, not kept live
+        int pb = ch * HWp + st * Wp + ((t.c0 + V * j0) >> 1);  // PD: pooled row st (dy rows 2 st, 2 st + 1)
+        if constexpr (PD) asm volatile("" : "+v"(pb));
 #pragma unroll
-            for (int m = 0; m < NIT; ++m) {
-                if (part >= 0 && m * NPT / NIT != part) continue;
-                const int o = (dm >> m) & 1 ? 4 * (dgo(m) - dgb + db) : OOB;
-                if constexpr (PD) {
-                    const int op = (dm >> m) & 1 ? pb + 4 * V * (m % NIR) : OOB / 4;
-                    const vecf<2> dp = bload<2>(rdz, 4 * op);
-                    dzv[m][0] = dp[0];
-                    dzv[m][1] = dp[1];
-                    pav[m] = (unsigned)__builtin_amdgcn_raw_buffer_load_b16(rpa, op, 0, 0);
-                } else {
-                    dzv[m] = bload<V>(rdz, o);
-                }
-                yv[m] = bload<V>(ry, o);
+        for (int m = 0; m < NIT; ++m) {
+            if (part >= 0 && m * NPT / NIT != part) continue;
+            const int o = (dm >> m) & 1 ? 4 * (dgo(m) - dgb + db) : OOB;
+            if constexpr (PD) {
+                const int op = (dm >> m) & 1 ? pb + 4 * V * (m % NIR) : OOB / 4;
+                const vecf<2> dp = bload<2>(t.rdz, 4 * op);
+                dzv[m][0] = dp[0];
+                dzv[m][1] = dp[1];
+                pav[m] = (unsigned)__builtin_amdgcn_raw_buffer_load_b16(t.rpa, op, 0, 0);
+            } else {
+                dzv[m] = bload<V>(t.rdz, o);
             }
-        };
-        // dy = A1 dz + A2 y + A3 (exact 0 outside the image) into dzv
-        auto form_dy = [&](int st) {
-            unsigned dm, xm;
-            masks(st, dm, xm);
-#pragma unroll
-            for (int m = 0; m < NIT; ++m) {
-                const float a3 = (dm >> m) & 1 ? A3 : 0.f;
-                if constexpr (PD) {  // dz: each pooled gradient at its window's selected element (row parity m / NIR)
-                    const float g0 = dzv[m][0], g1 = dzv[m][1];
-                    const unsigned pa = pav[m], i2 = 2u * (unsigned)(m / NIR);
-#pragma unroll
-                    for (int e = 0; e < V; ++e)
-                        dzv[m][e] = ((pa >> (8 * (e >> 1))) & 3u) == i2 + (unsigned)(e & 1) ? (e >> 1 ? g1 : g0) : 0.f;
-                }
-#pragma unroll
-                for (int e = 0; e < V; ++e) dzv[m][e] = fma1(A1, dzv[m][e], fma1(A2, yv[m][e], a3));
-            }
-        };
-        auto load_x = [&](int st, int part) {
-            unsigned dm, xm;
-            masks(st, dm, xm);
-            int xb = (2 * st + 1) * W + c0 + xgb;
-            asm volatile("" : "+v"(xb));
-#pragma unroll
-            for (int m = 0; m < NIT; ++m)
-                if (part < 0 || m * NPT / NIT == part) xv[m] = bload<V>(rx, (xm >> m) & 1 ? 4 * (xgo(m) - xgb + xb) : OOB);
-        };
-        auto store_x = [&](int st, const vecf<V> (&xr)[NIT]) {
-            unsigned dm, xm;
-            masks(st, dm, xm);
-            // x rows 2 st + 1, 2 st + 2 -> ring slots (2 st + 2) & 3, (2 st + 3) & 3
-            const int sl0 = ((2 * st + 2) & 3) * 32 * XCS, sl1 = ((2 * st + 3) & 3) * 32 * XCS;
-#pragma unroll
-            for (int m = 0; m < NIT; ++m) {
-                if (!((xex >> m) & 1)) continue;
-                vecf<V> v = xr[m];
-                if (PRO == PRO_BNRELU) {
-                    const float tt = (xm >> m) & 1 ? xt : 0.f;
-#pragma unroll
-                    for (int e = 0; e < V; ++e) v[e] = fmaxf(fmaf(v[e], xs, tt), 0.f);
-                }
-                float* d = xl + (m / NIR ? sl1 : sl0) + xlb + 8 * V * (m % NIR);
-                if constexpr (V == 4) {
-                    d[0] = v[0];
-                    *reinterpret_cast<f2*>(d + 1) = f2{v[1], v[2]};
-                    d[3] = v[3];
-                } else if constexpr (V == 2) {
-                    d[0] = v[0];
-                    d[1] = v[1];
-                } else {
-                    d[0] = v[0];
-                }
-            }
-        };
-
-        auto store = [&](int st) {
-            unsigned dm, xm;
-            masks(st, dm, xm);
-            const int db = 2 * st * W + c0;
-#pragma unroll
-            for (int m = 0; m < NIT; ++m) {
-                if (!((dex >> m) & 1)) continue;
-                const bool ok = (dm >> m) & 1;
-                const vecf<V> v = dzv[m];
-                float* d = dyl + dlb + (m / NIR) * 32 * DCS + 8 * V * (m % NIR);
-                if constexpr (V == 1) {
-                    d[0] = v[0];
-                } else {
-                    *reinterpret_cast<f2*>(d) = f2{v[0], v[1]};
-                    if constexpr (V == 4) *reinterpret_cast<f2*>(d + 2) = f2{v[2], v[3]};
-                }
-                if (write_dy) bstore<V>(rdo, ok ? 4 * (dgo(m) + db) : OOB, v);
-            }
-            store_x(st, xv);
-        };
-
-        // task prologue: stages -1 and 0 (x rows -1 .. 2, dy rows 0, 1) loaded together: one round trip
-        {
-            load_dy(0, -1);
-            load_x(0, -1);
-            vecf<V> xa[NIT];  // stage -1: x rows -1 (zeros: the ring slot holds the previous task's rows), 0
-            unsigned dm, xm;
-            masks(-1, dm, xm);
-            const int xb = -W + c0;
-#pragma unroll
-            for (int m = 0; m < NIT; ++m) xa[m] = bload<V>(rx, (xm >> m) & 1 ? 4 * (xgo(m) + xb) : OOB);
-            store_x(-1, xa);
-            form_dy(0);
-            store(0);
+            yv[m] = bload<V>(t.ry, o);
         }
-        __syncthreads();
-        // wave constants of row Q: e = w + sx u from x rows (w, u) of the tile row's four; the dy row
-        // combination pr = r0 + sy r1 (Q 0: r0, 1: r0 + r1, 2: r0 - r1, 3: r1 via r0 := row 1, sy = 0)
-        const int IW = Q == 0 ? 0 : Q == 2 ? 2 : 1, IU = Q == 0 ? 2 : Q == 2 ? 1 : Q == 1 ? 2 : 3;
-        const float sx = Q == 1 ? 1.f : -1.f;
-        const float sy = Q == 1 ? 1.f : Q == 2 ? -1.f : 0.f;
-        const float* const dr0 = dyl + (Q == 3 ? 32 * DCS : 0) + c32 * DCS + 2 * g;
-        const float* const dr1 = dyl + 32 * DCS + c32 * DCS + 2 * g;
-        auto ksteps = [&](const float* xw, const float* xu, int s0, int s1) {
-            const int n = s1 - s0;
-            const float* w = xw + 4 * s0;
-            const float* u = xu + 4 * s0;
-            const float* q0 = dr0 + 4 * s0;
-            const float* q1 = dr1 + 4 * s0;
-            kloop(w, u, q0, q1, sx, sy, acc, n);
-        };
-        const int Ks = a.Ksteps;
-        for (int tr = 0; tr < TR; ++tr) {
-            const bool pre = tr + 1 < TR;
-            // x rows 2 tr - 1 + i of this tile row live in ring slot (2 tr + i) & 3
-            const float* xw = xl + ((2 * tr + IW) & 3) * 32 * XCS + c32 * XCS + 2 * g;
-            const float* xu = xl + ((2 * tr + IU) & 3) * 32 * XCS + c32 * XCS + 2 * g;
-            // the next tile row's dz / y / x rows loaded over this row's K-steps in NPT parts (a
-            // burst of 3 NIT loads at the row start stalls the issuing waves on the texture unit, MFMA
-            // pipes idle); dy formed after the last part
+    };
+    // dy = A1 dz + A2 y + A3 (exact 0 outside the image) into dzv
+    auto form_dy = [&](const Task& t, int st) {
+        unsigned dm, xm;
+        masks(t, st, dm, xm);
 #pragma unroll
-            for (int pt = 0; pt < NPT; ++pt) {
-                __builtin_amdgcn_sched_barrier(0);  // (no hoisting of later parts' loads: registers)
-                if (pre) {
-                    load_dy(tr + 1, pt);
-                    load_x(tr + 1, pt);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                ksteps(xw, xu, Ks * pt / NPT, Ks * (pt + 1) / NPT);
+        for (int m = 0; m < NIT; ++m) {
+            const float a3 = (dm >> m) & 1 ? A3 : 0.f;
+            if constexpr (PD) {  // dz: each pooled gradient at its window's selected element (row parity m / NIR)
+                const float g0 = dzv[m][0], g1 = dzv[m][1];
+                const unsigned pa = pav[m], i2 = 2u * (unsigned)(m / NIR);
+#pragma unroll
+                for (int e = 0; e < V; ++e)
+                    dzv[m][e] = ((pa >> (8 * (e >> 1))) & 3u) == i2 + (unsigned)(e & 1) ? (e >> 1 ? g1 : g0) : 0.f;
             }
-            if (pre) form_dy(tr + 1);
-            __syncthreads();  // the dy rows and the two oldest x rows are free
-            if (pre) store(tr + 1);
+#pragma unroll
+            for (int e = 0; e < V; ++e) dzv[m][e] = fma1(A1, dzv[m][e], fma1(A2, yv[m][e], a3));
+        }
+    };
+    auto load_x = [&](const Task& t, int st, int part, vecf<V> (&xr)[NIT]) {
+        unsigned dm, xm;
+        masks(t, st, dm, xm);
+        int xb = (2 * st + 1) * W + t.c0 + xgb;
+        asm volatile("" : "+v"(xb));
+#pragma unroll
+        for (int m = 0; m < NIT; ++m)
+            if (part < 0 || m * NPT / NIT == part) xr[m] = bload<V>(t.rx, (xm >> m) & 1 ? 4 * (xgo(m) - xgb + xb) : OOB);
+    };
+    auto store_x = [&](const Task& t, int st, const vecf<V> (&xr)[NIT]) {
+        unsigned dm, xm;
+        masks(t, st, dm, xm);
+        // x rows 2 st + 1, 2 st + 2 -> ring slots (2 st + 2) & 3, (2 st + 3) & 3
+        const int sl0 = ((2 * st + 2) & 3) * 32 * XCS, sl1 = ((2 * st + 3) & 3) * 32 * XCS;
+#pragma unroll
+        for (int m = 0; m < NIT; ++m) {
+            if (!((xex >> m) & 1)) continue;
+            vecf<V> v = xr[m];
+            if (PRO == PRO_BNRELU) {
+                const float tt = (xm >> m) & 1 ? xt : 0.f;
+#pragma unroll
+                for (int e = 0; e < V; ++e) v[e] = fmaxf(fmaf(v[e], xs, tt), 0.f);
+            }
+            float* d = xl + (m / NIR ? sl1 : sl0) + xlb + 8 * V * (m % NIR);
+            if constexpr (V == 4) {
+                d[0] = v[0];
+                *reinterpret_cast<f2*>(d + 1) = f2{v[1], v[2]};
+                d[3] = v[3];
+            } else if constexpr (V == 2) {
+                d[0] = v[0];
+                d[1] = v[1];
+            } else {
+                d[0] = v[0];
+            }
+        }
+    };
+    auto store = [&](const Task& t, int st) {
+        unsigned dm, xm;
+        masks(t, st, dm, xm);
+        const int db = 2 * st * W + t.c0;
+#pragma unroll
+        for (int m = 0; m < NIT; ++m) {
+            if (!((dex >> m) & 1)) continue;
+            const bool ok = (dm >> m) & 1;
+            const vecf<V> v = dzv[m];
+            float* d = dyl + dlb + (m / NIR) * 32 * DCS + 8 * V * (m % NIR);
+            if constexpr (V == 1) {
+                d[0] = v[0];
+            } else {
+                *reinterpret_cast<f2*>(d) = f2{v[0], v[1]};
+                if constexpr (V == 4) *reinterpret_cast<f2*>(d + 2) = f2{v[2], v[3]};
+            }
+            if (write_dy) bstore<V>(t.rdo, ok ? 4 * (dgo(m) + db) : OOB, v);
+        }
+        store_x(t, st, xv);
+    };
+    // x rows -1, 0 of a task (stage -1): row -1 is outside (zeros; the ring slot holds the previous task's rows)
+    auto load_xa = [&](const Task& t, vecf<V> (&xa)[NIT]) {
+        unsigned dm, xm;
+        masks(t, -1, dm, xm);
+        const int xb = -W + t.c0;
+#pragma unroll
+        for (int m = 0; m < NIT; ++m) xa[m] = bload<V>(t.rx, (xm >> m) & 1 ? 4 * (xgo(m) + xb) : OOB);
+    };
+
+    // wave constants of row Q: e = w + sx u from x rows (w, u) of the tile row's four; the dy row
+    // combination pr = r0 + sy r1 (Q 0: r0, 1: r0 + r1, 2: r0 - r1, 3: r1 via r0 := row 1, sy = 0)
+    const int IW = Q == 0 ? 0 : Q == 2 ? 2 : 1, IU = Q == 0 ? 2 : Q == 2 ? 1 : Q == 1 ? 2 : 3;
+    const float sx = Q == 1 ? 1.f : -1.f;
+    const float sy = Q == 1 ? 1.f : Q == 2 ? -1.f : 0.f;
+    const float* const dr0 = dyl + (Q == 3 ? 32 * DCS : 0) + c32 * DCS + 2 * g;
+    const float* const dr1 = dyl + 32 * DCS + c32 * DCS + 2 * g;
+    auto ksteps = [&](const float* xw, const float* xu, int s0, int s1) {
+        const int n = s1 - s0;
+        const float* w = xw + 4 * s0;
+        const float* u = xu + 4 * s0;
+        const float* q0 = dr0 + 4 * s0;
+        const float* q1 = dr1 + 4 * s0;
+        kloop(w, u, q0, q1, sx, sy, acc, n);
+    };
+    const int Ks = a.Ksteps;
+    // Round 6 (PF: the V = 2 / 1 narrow images, 5-row tasks at cnn_small layers 5 / 6): the NEXT task's
+    // stages -1 / 0 are loaded during this task's last tile row, in parts under its K-steps like any next
+    // row, so its prologue round trip no longer stalls the block between tasks.  (V = 4: the extra staging
+    // registers spilled; its tasks are 10+ rows long.)
+    constexpr bool PF = V != 4;
+    vecf<V> xa[NIT];
+    // one tile row: KIND 0 = a row with a successor (loads row tr + 1 of t), 1 = the task's last row loading
+    // the next task's prologue (t = that task), 2 = the last row with nothing to load
+    auto row = [&](const Task& t, int tr, auto kind) {
+        constexpr int KIND = decltype(kind)::value;
+        // x rows 2 tr - 1 + i of this tile row live in ring slot (2 tr + i) & 3
+        const float* xw = xl + ((2 * tr + IW) & 3) * 32 * XCS + c32 * XCS + 2 * g;
+        const float* xu = xl + ((2 * tr + IU) & 3) * 32 * XCS + c32 * XCS + 2 * g;
+        // the next tile row's dz / y / x rows loaded over this row's K-steps in NPT parts (a burst of 3
+        // NIT loads at the row start stalls the issuing waves on the texture unit, MFMA pipes idle); dy
+        // formed after the last part
+#pragma unroll
+        for (int pt = 0; pt < NPT; ++pt) {
+            __builtin_amdgcn_sched_barrier(0);  // (no hoisting of later parts' loads: registers)
+            if constexpr (KIND == 0) {
+                load_dy(t, tr + 1, pt);
+                load_x(t, tr + 1, pt, xv);
+            } else if constexpr (KIND == 1) {
+                load_dy(t, 0, pt);
+                load_x(t, 0, pt, xv);
+                if (pt == 0) load_xa(t, xa);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            ksteps(xw, xu, Ks * pt / NPT, Ks * (pt + 1) / NPT);
+        }
+        if constexpr (KIND != 2) form_dy(t, KIND == 0 ? tr + 1 : 0);
+        __syncthreads();  // the dy rows and the two oldest x rows are free (last row: every ring slot)
+        if constexpr (KIND == 0) {
+            store(t, tr + 1);
             __syncthreads();
+        } else if constexpr (KIND == 1) {
+            store_x(t, -1, xa);
+            store(t, 0);
         }
+    };
+    auto prologue = [&](const Task& t) {  // stages -1 and 0 (x rows -1 .. 2, dy rows 0, 1): one round trip
+        load_dy(t, 0, -1);
+        load_x(t, 0, -1, xv);
+        load_xa(t, xa);
+        store_x(t, -1, xa);
+        form_dy(t, 0);
+        store(t, 0);
+    };
+    bool staged = false;  // (PF) the current task's prologue was stored by the previous task's last row
+    for (int task = t0s; task < t1s; ++task) {
+        const Task cur = task_of(task);
+        if (!staged) prologue(cur);
+        __syncthreads();
+        for (int tr = 0; tr + 1 < TR; ++tr) row(cur, tr, std::integral_constant<int, 0>{});
+        staged = PF && task + 1 < t1s;
+        if (staged) row(task_of(task + 1), TR - 1, std::integral_constant<int, 1>{});
+        else row(cur, TR - 1, std::integral_constant<int, 2>{});
     }
     // partials: C register r of lane l = (cout row (r & 3) + 8 (r >> 2) + 4 g, cin c32); xi = 4 Q + e
     float* out = a.part + (int64_t)slice * a.cout * a.cin * 16;

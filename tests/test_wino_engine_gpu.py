@@ -85,6 +85,11 @@ WW_CASES = [  # H, W, cin, cout, B, reps, prologue, pooled dz
     (5, 25, 64, 96, 23, 1, 1, 0),
     (7, 27, 32, 32, 5, 1, 1, 0),
     (9, 29, 32, 32, 7, 1, 1, 0),  # the widest single-float image the staging capacity admits (15 tile columns)
+    # cnn_small layers 6 / 5 (V = 2) with several tasks per slice: each task's prologue is loaded during the
+    # previous task's last tile row (round 6)
+    (10, 50, 128, 128, 100, 1, 1, 0),
+    (10, 50, 64, 128, 200, 1, 0, 0),
+    (11, 50, 64, 64, 300, 1, 1, 0),  # odd H: a half last tile row
 ]
 
 
