@@ -160,6 +160,19 @@ __device__ __forceinline__ float bld1(__amdgpu_buffer_rsrc_t r, unsigned vo, int
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
 }
 
+// True in the last of the block's 4 waves to call it for this unit (an LDS counter at red + 514, reset by that
+// wave): the wave's scratch writes are complete before it counts itself in.
+__device__ __forceinline__ bool last_wave(float* red, int lane) {
+    int* cnt = reinterpret_cast<int*>(red + 514);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    int v = 0;
+    if (lane == 0) v = atomicAdd(cnt, 1);
+    v = __builtin_amdgcn_readfirstlane(v);
+    if (v != 3) return false;
+    if (lane == 0) *cnt = 0;
+    return true;
+}
+
 // Epilogue of one unit.  Lane (n, kq) holds output channels n0 + 16 mi + 4 kq + i (j = 4 mi + i < 8)
 // of its tile (outputs y[j][e] at (2 tr + (e >> 1), 2 tc + (e & 1))).  The 16 lanes of a row hold
 // 16 consecutive tiles of one or two tile rows, so a store of one output row is a 128-byte run.
@@ -234,14 +247,17 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
             d[0] = T1; d[1] = T2; d[2] = K;
         }
         if (lane == 0) red[384 + wave] = cnt;  // valid outputs of the wave (all channels alike)
-        __syncthreads();
-        if (tid < 32) {
+        // the last of the block's 4 waves to get here merges the 4 waves' statistics (round 6: no block barrier;
+        // a __syncthreads here cost 3-6 % of the forward convs, profiles/r6_wino_epilogue_barrier.txt).  The
+        // scratch is safe to reuse: every wave passes the next unit's first chunk barrier only after this merge.
+        if (last_wave(red, lane)) {
+            const int c = lane;
             float nn = 0.f, mean = 0.f, m2 = 0.f;
 #pragma unroll
             for (int w = 0; w < 4; ++w) {
                 const float nw = red[384 + w];
                 if (nw > 0.f) {
-                    const float* d = red + (w * 32 + tid) * 3;
+                    const float* d = red + (w * 32 + c) * 3;
                     const float rw = __builtin_amdgcn_rcpf(nw);  // 1-ulp reciprocals (statistics)
                     const float mw = d[2] + d[0] * rw, m2w = fmaxf(d[1] - d[0] * d[0] * rw, 0.f);
                     const float nt = nn + nw, delta = mw - mean, f = nw * __builtin_amdgcn_rcpf(nt);
@@ -250,9 +266,11 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
                     nn = nt;
                 }
             }
-            a.part0[(int64_t)(n0 + tid) * a.nblk + tb] = nn * mean;
-            a.part1[(int64_t)(n0 + tid) * a.nblk + tb] = m2;
-            if (tid == 0 && n0 == 0) a.partn[tb] = nn;
+            if (c < 32) {
+                a.part0[(int64_t)(n0 + c) * a.nblk + tb] = nn * mean;
+                a.part1[(int64_t)(n0 + c) * a.nblk + tb] = m2;
+                if (c == 0 && n0 == 0) a.partn[tb] = nn;
+            }
         }
     } else if (EPI == EPI_BWD_STORE) {
         const __amdgpu_buffer_rsrc_t rs = wrs(a.out, HW, 4);
@@ -515,20 +533,23 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
             red[(wave * 32 + cosel) * 2] = tz;
             red[(wave * 32 + cosel) * 2 + 1] = tx;
         }
-        __syncthreads();
-        if (tid < 32) {
+        if (last_wave(red, lane)) {  // (as the forward: the last wave sums, no block barrier)
+            const int c = lane & 31;
             float s0 = 0.f, s1 = 0.f;
 #pragma unroll
             for (int w = 0; w < 4; ++w) {
-                s0 += red[(w * 32 + tid) * 2];
-                s1 += red[(w * 32 + tid) * 2 + 1];
+                s0 += red[(w * 32 + c) * 2];
+                s1 += red[(w * 32 + c) * 2 + 1];
             }
-            a.part0[(int64_t)(n0 + tid) * a.nblk + tb] = s0;
-            a.part1[(int64_t)(n0 + tid) * a.nblk + tb] = s1;
+            if (lane < 32) {
+                a.part0[(int64_t)(n0 + c) * a.nblk + tb] = s0;
+                a.part1[(int64_t)(n0 + c) * a.nblk + tb] = s1;
+            }
         }
     }
 }
 
+// (WINO_KO bits, analysis builds only: 1 no operand copies, 2 no epilogue, 4 no chunk sync, 8 no BN + ReLU)
 // Persistent: each workgroup walks units u = it * G + (XCD-contiguous slot); unit = (64-tile block tb
 // of one sample, 32-channel output group cg).  The first K-chunk of the next unit is copied while the
 // last chunk of the current one is multiplied and during its epilogue.
@@ -559,6 +580,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
             cft[2 * c] = f.x;
             cft[2 * c + 1] = f.y;
         }
+    if (tid == 0) reinterpret_cast<int*>(red + 514)[0] = 0;  // the epilogue's last-wave counter
     const int nunits = (SP ? g.nblk : a.B * g.BPS) * g.ncg;
     const int G = gridDim.x;
     // XCD-contiguous slot of this workgroup inside a round (dispatch is round-robin over the 8 XCDs)
