@@ -10,6 +10,9 @@ of the exact float64 loss, every gradient tensor at cosine > 0.98 to the rounded
 running statistics within 1e-2 relative.  bf16 is a throughput option, not fp32 parity.
 Reference: src/models/phoneme_cnn.py:146-304 (the reference trains in float32; bf16 is an MI355X
 addition)."""
+import json
+import os
+
 import pytest
 import torch
 import torch.nn as nn
@@ -69,6 +72,22 @@ BF16_STEP_TOL = {
     (True, 201, tuple(FULL), 16): (6.5e-3, 2.7e-2, 5e-3, 1e-2, 0.987),
     (True, 201, None, 32): (3.2e-3, 3.2e-2, 1e-3, 1e-2, 0.999),
 }
+
+
+def _record(key, rec):
+    """Measured errors and their bounds into the full-size JSON record (PCX_FULLSIZE_JSON; profiles/)."""
+    print(f"\nFULLSIZE {key} " + json.dumps(rec, sort_keys=True))
+    path = os.environ.get("PCX_FULLSIZE_JSON", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                              "gpurun_out", "fullsize_parity.json"))
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    try:
+        with open(path) as f:
+            allrec = json.load(f)
+    except (OSError, ValueError):
+        allrec = {}
+    allrec[key] = rec
+    with open(path, "w") as f:
+        json.dump(allrec, f, indent=1, sort_keys=True)
 
 
 @pytest.mark.parametrize("residual,T,dims,B", [(True, 200, None, 32), (False, 57, None, 32),
@@ -135,6 +154,11 @@ def test_deep_bf16_step(residual, T, dims, B):
           f"vs f64 {vs_f64:.2e}, |d loss| {dl_ref:.2e} (vs rounded-operand {dl_rnd:.2e}), "
           f"min grad cosine {worst} {cos[worst]:.4f}")
     t_exact, t_f64, t_loss, t_loss_rnd, t_cos = BF16_STEP_TOL[(residual, T, tuple(dims) if dims else None, B)]
+    _record(f"bf16_step_res{int(residual)}_T{T}_{'x'.join(map(str, dims)) if dims else 'default'}_B{B}",
+            {"emb_vs_rounded_f64": exact, "emb_vs_f64": vs_f64, "loss_vs_f64": dl_ref, "loss_vs_rounded_f64": dl_rnd,
+             "min_grad_cosine": cos[worst], "min_grad_cosine_tensor": worst,
+             "tolerances": {"emb_vs_rounded_f64": t_exact, "emb_vs_f64": t_f64, "loss_vs_f64": t_loss,
+                            "loss_vs_rounded_f64": t_loss_rnd, "grad_cosine": t_cos}})
     assert exact < t_exact
     assert vs_f64 < t_f64
     assert dl_ref < t_loss
@@ -181,8 +205,6 @@ def test_deep_bf16_b512_full_width_matches_rounded_f64(T):
     measured errors (round 6); the measured margins go to the full-size JSON record (profiles/).
     Reference: src/models/phoneme_cnn.py:146-216, 274-304; T = 201: src/datasets/dataset.py:50."""
     import gc
-    import json
-    import os
     from oracle import torch_port as tp
     from phoneme_contrast_amd.losses import SupervisedContrastiveLoss
     from phoneme_contrast_amd.models import PhonemeNetDeep
@@ -241,18 +263,7 @@ def test_deep_bf16_b512_full_width_matches_rounded_f64(T):
            "grad_cosine": cos, "running_stats_maxrel": rstat,
            "tolerances": {"emb_vs_rounded_f64": 1e-2, "emb_vs_f64": 3e-2, "loss_vs_f64": 5e-3,
                           "loss_vs_rounded_f64": 5e-3, "grad_cosine": 0.99, "running_stats": "rtol 1e-2, atol 1e-3"}}
-    print(f"\nFULLSIZE cnn_deep_bf16_B512_T{T} " + json.dumps(rec, sort_keys=True))
-    path = os.environ.get("PCX_FULLSIZE_JSON", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                                                              "gpurun_out", "fullsize_parity.json"))
-    os.makedirs(os.path.dirname(path), exist_ok=True)
-    try:
-        with open(path) as f:
-            allrec = json.load(f)
-    except (OSError, ValueError):
-        allrec = {}
-    allrec[f"cnn_deep_bf16_B512_T{T}"] = rec
-    with open(path, "w") as f:
-        json.dump(allrec, f, indent=1, sort_keys=True)
+    _record(f"cnn_deep_bf16_B512_T{T}", rec)
     # (round 6: ~3x the measured B = 512 errors -- emb 1.1e-2 vs f64, loss 1.1e-3, cosine >= 0.9957)
     assert exact < 1e-2
     assert vs_f64 < 3e-2
