@@ -37,6 +37,7 @@
 #include <type_traits>
 
 #include "conv_epilogue.h"
+#include "pk_f32.h"
 
 namespace pcx {
 namespace {
@@ -571,6 +572,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     const int tid = threadIdx.x, lane = tid & 63, n = lane & 15, kq = lane >> 4;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int HW = a.H * a.W;
+    const PkK pk = pk_consts();
     float* cft = smem + 2 * BUFF;             // [cin] float2 {s, t}
     float* red = cft + 2 * a.cin;             // epilogue scratch (512 floats)
     const unsigned lds0 = (unsigned)(uintptr_t)(lds_void*)smem;
@@ -813,13 +815,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
             auto kstep = [&](const float* bi, const float* bw, int s, int c0, auto ftag) {
                 constexpr bool FIRST = decltype(ftag)::value;
                     const int cl = 4 * s + kq;
-                float d[4][4];
+                f2 P[4][2];  // patch row r, columns 2 k, 2 k + 1
                 const float* pp = bi + pbase + 4 * s * WSP;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const f2 u0 = *reinterpret_cast<const f2*>(pp + r * WROW);
-                    const f2 u1 = *reinterpret_cast<const f2*>(pp + r * WROW + 2);
-                    d[r][0] = u0.x; d[r][1] = u0.y; d[r][2] = u1.x; d[r][3] = u1.y;
+                    P[r][0] = *reinterpret_cast<const f2*>(pp + r * WROW);
+                    P[r][1] = *reinterpret_cast<const f2*>(pp + r * WROW + 2);
                 }
                 f32x4 av[2][4];
 #pragma unroll
@@ -840,19 +841,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
 #pragma unroll
-                        for (int c = 0; c < 4; ++c) d[r][c] = fmaxf(fmaf(d[r][c], st.x, st.y), 0.f);
+                        for (int k = 0; k < 2; ++k) P[r][k] = pk_bnrelu(P[r][k], st);
                     if constexpr (BRD && !X4) {
 #pragma unroll
-                        for (int c = 0; c < 4; ++c) {
-                            d[0][c] *= fr0;
-                            d[2][c] *= fr2;
-                            d[3][c] *= fr3;
+                        for (int k = 0; k < 2; ++k) {
+                            P[0][k] *= fr0;
+                            P[2][k] *= fr2;
+                            P[3][k] *= fr3;
                         }
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
-                            d[r][0] *= fc0;
-                            d[r][2] *= fc2;
-                            d[r][3] *= fc3;
+                            P[r][0].x *= fc0;
+                            P[r][1].x *= fc2;
+                            P[r][1].y *= fc3;
                         }
                     }
                 }
@@ -862,35 +863,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
                     // value before a tensor's first plane is the workspace's unwritten slack)
                     if constexpr (PRO != PRO_RAW) {
 #pragma unroll
-                        for (int c = 0; c < 4; ++c) {
-                            d[0][c] = fr0 != 0.f ? d[0][c] : 0.f;
-                            d[2][c] = fr2 != 0.f ? d[2][c] : 0.f;
-                            d[3][c] = fr3 != 0.f ? d[3][c] : 0.f;
+                        for (int k = 0; k < 2; ++k) {
+                            P[0][k] = fr0 != 0.f ? P[0][k] : f2{0.f, 0.f};
+                            P[2][k] = fr2 != 0.f ? P[2][k] : f2{0.f, 0.f};
+                            P[3][k] = fr3 != 0.f ? P[3][k] : f2{0.f, 0.f};
                         }
                     }
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        d[r][0] = fc0 != 0.f ? d[r][0] : 0.f;
-                        d[r][2] = fc2 != 0.f ? d[r][2] : 0.f;
-                        d[r][3] = fc3 != 0.f ? d[r][3] : 0.f;
+                        P[r][0].x = fc0 != 0.f ? P[r][0].x : 0.f;
+                        P[r][1].x = fc2 != 0.f ? P[r][1].x : 0.f;
+                        P[r][1].y = fc3 != 0.f ? P[r][1].y : 0.f;
                     }
                 }
-                // V = B^T d B (rows first, then columns): 32 additions
-                float e_[4][4], v[16];
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    e_[0][c] = d[0][c] - d[2][c];
-                    e_[1][c] = d[1][c] + d[2][c];
-                    e_[2][c] = d[2][c] - d[1][c];
-                    e_[3][c] = d[1][c] - d[3][c];
-                }
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    v[4 * r + 0] = e_[r][0] - e_[r][2];
-                    v[4 * r + 1] = e_[r][1] + e_[r][2];
-                    v[4 * r + 2] = e_[r][2] - e_[r][1];
-                    v[4 * r + 3] = e_[r][1] - e_[r][3];
-                }
+                // V = B^T d B (rows first, then columns): 32 additions as 16 packed
+                float v[16];
+                pk_input_transform(pk, P, v);
 #pragma unroll
                 for (int x = 0; x < 16; ++x)
 #pragma unroll
@@ -947,21 +935,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
 
         // ---- output transform Y = A^T M A: y[j][e] = output (2 tr + (e >> 1), 2 tc + (e & 1)) of
         // channel j = 4 mi + i
+        // (packed over channel pairs i, i + 1: 24 additions per channel as 12 packed, same order: pk_f32.h)
         float y[8][4];
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                float s0[4], s1[4];
+            for (int ih = 0; ih < 2; ++ih) {
+                auto A = [&](int x) -> f2 {
+                    return ih ? __builtin_shufflevector(acc[x][mi], acc[x][mi], 2, 3)
+                              : __builtin_shufflevector(acc[x][mi], acc[x][mi], 0, 1);
+                };
+                f2 s0[4], s1[4];
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
-                    s0[c] = acc[c][mi][i] + acc[4 + c][mi][i] + acc[8 + c][mi][i];
-                    s1[c] = acc[4 + c][mi][i] - acc[8 + c][mi][i] - acc[12 + c][mi][i];
+                    s0[c] = A(c) + A(4 + c) + A(8 + c);
+                    s1[c] = pk_sub(pk, pk_sub(pk, A(4 + c), A(8 + c)), A(12 + c));
                 }
-                y[4 * mi + i][0] = s0[0] + s0[1] + s0[2];
-                y[4 * mi + i][1] = s0[1] - s0[2] - s0[3];
-                y[4 * mi + i][2] = s1[0] + s1[1] + s1[2];
-                y[4 * mi + i][3] = s1[1] - s1[2] - s1[3];
+                const f2 y0 = s0[0] + s0[1] + s0[2];
+                const f2 y1 = pk_sub(pk, pk_sub(pk, s0[1], s0[2]), s0[3]);
+                const f2 y2 = s1[0] + s1[1] + s1[2];
+                const f2 y3 = pk_sub(pk, pk_sub(pk, s1[1], s1[2]), s1[3]);
+                const int j = 4 * mi + 2 * ih;
+                y[j][0] = y0.x; y[j][1] = y1.x; y[j][2] = y2.x; y[j][3] = y3.x;
+                y[j + 1][0] = y0.y; y[j + 1][1] = y1.y; y[j + 1][2] = y2.y; y[j + 1][3] = y3.y;
             }
 #if defined(WINO_KO) && (WINO_KO & 2)  // analysis builds only: no epilogue (one guarded store keeps y live)
         {

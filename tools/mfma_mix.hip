@@ -3,7 +3,8 @@
 // N filler instructions of one kind:
 //   kind 0 none, 1 v_fma_f32 (independent), 2 ds_read_b128 (results kept live, consumed at the end),
 //   3 buffer_load_dwordx4 ... lds (1 KiB LDS-DMA per wave-instruction, L2-resident source; vmcnt bounded),
-//   4 buffer_load_dword ... lds (256 B), 5 ds_read_b64
+//   4 buffer_load_dword ... lds (256 B), 5 ds_read_b64, 6 v_add_f32 (inline asm, independent), 7 v_pk_add_f32
+//   (two f32 adds per lane), 8 v_pk_fma_f32, 9 v_max_f32 (inline asm, independent)
 // at 1 wave per SIMD (256-thread blocks) and 2 waves per SIMD (512), one block per CU.  Prints cycles per
 // MFMA at the measured clock-free rate (ms) and the extra time per filler instruction.
 //   hipcc -O3 --offload-arch=gfx950 tools/mfma_mix.hip -o tools/mfma_mix && tools/mfma_mix
@@ -25,6 +26,11 @@ __global__ __launch_bounds__(512) void mix(const float* __restrict__ src, float*
     float v[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] = tid * 1e-3f + i;
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    f2v p2[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) p2[i] = f2v{tid * 1e-3f + i, tid * 2e-3f - i};
+    const f2v ka = f2v{a, b}, kb = f2v{b, a};
     f32x4 r4[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) r4[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -42,6 +48,14 @@ __global__ __launch_bounds__(512) void mix(const float* __restrict__ src, float*
                     const unsigned ad = ldsb + 16u * lane + 1024u * (unsigned)((j * N + q) & 7);
                     asm volatile("ds_read_b128 %0, %1" : "=v"(r4[(j * N + q) & 7]) : "v"(ad) : "memory");
                 }
+                if constexpr (KIND == 6)
+                    asm volatile("v_add_f32 %0, %0, %1" : "+v"(v[(j * N + q) & 7]) : "v"(aa));
+                if constexpr (KIND == 7)
+                    asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(p2[(j * N + q) & 7]) : "v"(ka));
+                if constexpr (KIND == 8)
+                    asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(p2[(j * N + q) & 7]) : "v"(ka), "v"(kb));
+                if constexpr (KIND == 9)
+                    asm volatile("v_max_f32 %0, %0, %1" : "+v"(v[(j * N + q) & 7]) : "v"(aa));
                 if constexpr (KIND == 5) {
                     const unsigned ad = ldsb + 8u * lane + 1024u * (unsigned)((j * N + q) & 7);
                     float2 t;
@@ -64,7 +78,7 @@ __global__ __launch_bounds__(512) void mix(const float* __restrict__ src, float*
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     float s = 0.f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) s += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3] + v[i] + r4[i][0] + r4[i][3];
+    for (int i = 0; i < 8; ++i) s += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3] + v[i] + r4[i][0] + r4[i][3] + p2[i][0] + p2[i][1];
     if (s == 1234.5f) out[tid] = s + sh[tid];
 }
 
@@ -105,6 +119,14 @@ int main() {
         rep("v_fma_f32", 1, run<1, 1>(src, threads, iters));
         rep("v_fma_f32", 2, run<1, 2>(src, threads, iters));
         rep("v_fma_f32", 4, run<1, 4>(src, threads, iters));
+        rep("v_add_f32 (asm)", 2, run<6, 2>(src, threads, iters));
+        rep("v_add_f32 (asm)", 4, run<6, 4>(src, threads, iters));
+        rep("v_pk_add_f32", 1, run<7, 1>(src, threads, iters));
+        rep("v_pk_add_f32", 2, run<7, 2>(src, threads, iters));
+        rep("v_pk_add_f32", 4, run<7, 4>(src, threads, iters));
+        rep("v_pk_fma_f32", 2, run<8, 2>(src, threads, iters));
+        rep("v_pk_fma_f32", 4, run<8, 4>(src, threads, iters));
+        rep("v_max_f32 (asm)", 4, run<9, 4>(src, threads, iters));
         rep("ds_read_b128", 1, run<2, 1>(src, threads, iters));
         rep("ds_read_b128", 2, run<2, 2>(src, threads, iters));
         rep("ds_read_b64", 1, run<5, 1>(src, threads, iters));
