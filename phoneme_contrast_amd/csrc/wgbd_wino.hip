@@ -33,6 +33,7 @@
 #include <type_traits>
 
 #include "kernels.h"
+#include "pk_f32.h"
 
 #if defined(WB_KO) && (WB_KO & 4)
 #define WB_KO_EPI 1
@@ -83,7 +84,10 @@ struct WOps {
     f2 w0, w1, u0, u1, a0, a1, b0, b1;
 };
 
-__device__ __forceinline__ WOps wload(const float* w, const float* u, const float* d0, const float* d1, int s) {
+typedef __attribute__((address_space(3))) const float lds_f;
+__device__ __forceinline__ f2 ld2(lds_f* p) { return *reinterpret_cast<const __attribute__((address_space(3))) f2*>(p); }
+
+__device__ __forceinline__ WOps wload(lds_f* w, lds_f* u, lds_f* d0, lds_f* d1, int s) {
     const int p = 4 * s;
     WOps o;
     o.w0 = ld2(w + p);
@@ -97,15 +101,18 @@ __device__ __forceinline__ WOps wload(const float* w, const float* u, const floa
     return o;
 }
 
-// V row Q from e = w + sx u; Yh' row Q from pr = r0 + sy r1 (as wgrad_wino.hip kmul)
-__device__ __forceinline__ void wmul(const WOps& o, float sx, float sy, f32x16 (&acc)[4]) {
-    const float e0 = fmaf(sx, o.u0.x, o.w0.x), e1 = fmaf(sx, o.u0.y, o.w0.y);
-    const float e2 = fmaf(sx, o.u1.x, o.w1.x), e3 = fmaf(sx, o.u1.y, o.w1.y);
-    const float px = fmaf(sy, o.b0.y, o.a0.y), py = fmaf(sy, o.b1.x, o.a1.x);
-    acc[0] = mfma32(px, e0 - e2, acc[0]);
-    acc[1] = mfma32(px + py, e1 + e2, acc[1]);
-    acc[2] = mfma32(px - py, e2 - e1, acc[2]);
-    acc[3] = mfma32(py, e1 - e3, acc[3]);
+// V row Q from e = w + sx u; Yh' row Q from pr = r0 + sy r1 (as wgrad_wino.hip kmul, packed: pk_f32.h; px / py
+// are the middle pair of the 4-column dy reads, not a register pair, so they stay two scalar fma)
+__device__ __forceinline__ void wmul(const WOps& o, const PkK& k, f2 sxx, float sy, f32x16 (&acc)[4]) {
+    const f2 e01 = __builtin_elementwise_fma(o.u0, sxx, o.w0), e23 = __builtin_elementwise_fma(o.u1, sxx, o.w1);
+    const f2 pp = {fmaf(sy, o.b0.y, o.a0.y), fmaf(sy, o.b1.x, o.a1.x)};
+    const f2 b03 = pk_sub(k, e01, e23);
+    const f2 b12 = __builtin_elementwise_fma(e01.yy, k.pm, e23.xx);
+    const f2 a12 = __builtin_elementwise_fma(pp.yy, k.pm, pp.xx);
+    acc[0] = mfma32(pp.x, b03.x, acc[0]);
+    acc[1] = mfma32(a12.x, b12.x, acc[1]);
+    acc[2] = mfma32(a12.y, b12.y, acc[2]);
+    acc[3] = mfma32(pp.y, b03.y, acc[3]);
 }
 
 // XCT: the ring's channel stride as a compile-time constant (LDS offsets become instruction immediates:
@@ -140,6 +147,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
     // ---- Winograd row constants (both GEMMs combine the same patch rows: B^T row Q)
     const int IW = Q == 0 ? 0 : Q == 2 ? 2 : 1, IU = Q == 0 ? 2 : Q == 2 ? 1 : Q == 1 ? 2 : 3;
     const float sx = Q == 1 ? 1.f : -1.f;
+    const f2 sxx = {sx, sx};
+    const PkK pk = pk_consts();
     // weight gradient: lane channel c32, tile parity g2; dy output rows 2 tr (patch row 1) / 2 tr + 1 (row 2)
     const int c32 = lane & 31, g2 = lane >> 5;
     const int ID0 = Q == 3 ? 2 : 1;
@@ -342,24 +351,31 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
                 if constexpr (!DG) {
 #if !(defined(WB_KO) && (WB_KO & 1))
                     // ---- weight gradient: K-steps 8 g .. 8 g + 7 (tiles 16 g .. 16 g + 15)
-                    const float* w = xr + sw + c32 * XCS + 2 * g2;
-                    const float* u = xr + su + c32 * XCS + 2 * g2;
-                    const float* d0 = dr + ((2 * tr + ID0) & 3) * CH * XCS + c32 * XCS + 2 * g2;
-                    const float* d1 = dr + ((2 * tr + 2) & 3) * CH * XCS + c32 * XCS + 2 * g2;
+                    // (LDS pointers advanced once per two K-steps: every read is a base register plus an
+                    // immediate; the look-ahead read past an even group end stays inside the LDS row, unused)
                     const int s0 = 8 * g, s1 = min(8 * g + 8, Ks);
-                    WOps A = wload(w, u, d0, d1, s0);
+                    lds_f* w = (lds_f*)(xr + sw + c32 * XCS + 2 * g2 + 4 * s0);
+                    lds_f* u = (lds_f*)(xr + su + c32 * XCS + 2 * g2 + 4 * s0);
+                    lds_f* d0 = (lds_f*)(dr + ((2 * tr + ID0) & 3) * CH * XCS + c32 * XCS + 2 * g2 + 4 * s0);
+                    lds_f* d1 = (lds_f*)(dr + ((2 * tr + 2) & 3) * CH * XCS + c32 * XCS + 2 * g2 + 4 * s0);
+                    asm volatile("" : "+v"(w), "+v"(u), "+v"(d0), "+v"(d1));
+                    WOps A = wload(w, u, d0, d1, 0);
                     int s = s0;
                     for (; s + 2 <= s1; s += 2) {
-                        const WOps Bn = wload(w, u, d0, d1, s + 1);
+                        const WOps Bn = wload(w, u, d0, d1, 1);
                         __builtin_amdgcn_sched_barrier(0);
-                        wmul(A, sx, sy, R);
+                        wmul(A, pk, sxx, sy, R);
                         __builtin_amdgcn_sched_barrier(0);
-                        A = wload(w, u, d0, d1, s + 2 < s1 ? s + 2 : s + 1);
+                        A = wload(w, u, d0, d1, 2);
                         __builtin_amdgcn_sched_barrier(0);
-                        wmul(Bn, sx, sy, R);
+                        wmul(Bn, pk, sxx, sy, R);
                         __builtin_amdgcn_sched_barrier(0);
+                        w += 8;
+                        u += 8;
+                        d0 += 8;
+                        d1 += 8;
                     }
-                    if (s < s1) wmul(A, sx, sy, R);
+                    if (s < s1) wmul(A, pk, sxx, sy, R);
 #endif
                 } else {
 #if !(defined(WB_KO) && (WB_KO & 2))
@@ -384,9 +400,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
                         if (ks + 1 < 8) dload(op[(ks + 1) & 1], ks + 1);
                         __builtin_amdgcn_sched_barrier(0);
                         const f2* o = op[ks & 1];
-                        const float q0 = fmaf(sx, o[2].x, o[0].x), q1 = fmaf(sx, o[2].y, o[0].y);
-                        const float q2 = fmaf(sx, o[3].x, o[1].x), q3 = fmaf(sx, o[3].y, o[1].y);
-                        const float v[4] = {q0 - q2, q1 + q2, q2 - q1, q1 - q3};
+                        // (packed: {q0, q1}, {q2, q3}, {q0 - q2, q1 - q3}, {q1 + q2, q2 - q1}; pk_f32.h)
+                        const f2 q01 = __builtin_elementwise_fma(o[2], sxx, o[0]);
+                        const f2 q23 = __builtin_elementwise_fma(o[3], sxx, o[1]);
+                        const f2 b03 = pk_sub(pk, q01, q23);
+                        const f2 b12 = __builtin_elementwise_fma(q01.yy, pk.pm, q23.xx);
+                        const float v[4] = {b03.x, b12.x, b12.y, b03.y};
 #pragma unroll
                         for (int e = 0; e < 4; ++e)
 #pragma unroll

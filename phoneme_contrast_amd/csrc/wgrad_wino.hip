@@ -33,6 +33,7 @@
 #include <type_traits>
 
 #include "kernels.h"
+#include "pk_f32.h"
 
 namespace pcx {
 namespace {
@@ -81,7 +82,6 @@ __device__ __forceinline__ float fma1(float a, float b, float c) {
     return r;
 }
 
-__device__ __forceinline__ f2 ld2(const float* p) { return *reinterpret_cast<const f2*>(p); }
 
 // Operands of one K-step (2 tiles, lane tile 2 s + g): the wave's two x rows (w, u: 4 values
 // each) and the two dy rows (r0, r1: 2 values each) of the lane's channel.
@@ -89,7 +89,10 @@ struct KOps {
     f2 w0, w1, u0, u1, r0, r1;
 };
 
-__device__ __forceinline__ KOps kload(const float* w, const float* u, const float* q0, const float* q1, int s) {
+typedef __attribute__((address_space(3))) const float lds_f;
+__device__ __forceinline__ f2 ld2(lds_f* p) { return *reinterpret_cast<const __attribute__((address_space(3))) f2*>(p); }
+
+__device__ __forceinline__ KOps kload(lds_f* w, lds_f* u, lds_f* q0, lds_f* q1, int s) {
     const int p = 4 * s;  // 2 * (2 s + g), the lane's 2 g folded into the row bases
     KOps o;
     o.w0 = ld2(w + p);
@@ -102,35 +105,53 @@ __device__ __forceinline__ KOps kload(const float* w, const float* u, const floa
 }
 
 // V row Q = (B^T d B) row Q from e = w + sx u; Yh' row Q = (A dY A^T) row Q (row / column 3 sign-
-// folded) from pr = r0 + sy r1; four 32x32x2 MFMAs
-__device__ __forceinline__ void kmul(const KOps& o, float sx, float sy, f32x16 (&acc)[4]) {
-    const float e0 = fmaf(sx, o.u0.x, o.w0.x), e1 = fmaf(sx, o.u0.y, o.w0.y);
-    const float e2 = fmaf(sx, o.u1.x, o.w1.x), e3 = fmaf(sx, o.u1.y, o.w1.y);
-    const float px = fmaf(sy, o.r1.x, o.r0.x), py = fmaf(sy, o.r1.y, o.r0.y);
-    acc[0] = mfma32(px, e0 - e2, acc[0]);
-    acc[1] = mfma32(px + py, e1 + e2, acc[1]);
-    acc[2] = mfma32(px - py, e2 - e1, acc[2]);
-    acc[3] = mfma32(py, e1 - e3, acc[3]);
+// folded) from pr = r0 + sy r1; four 32x32x2 MFMAs.  Packed (pk_f32.h, round 6): 6 v_pk_fma_f32 instead of
+// 12 scalar operations, each lane bit-identical to the scalar form:
+//   {e0, e1} = fma(u0, sx, w0), {e2, e3} = fma(u1, sx, w1), {px, py} = fma(r1, sy, r0),
+//   {e0 - e2, e1 - e3},  {e1 + e2, e2 - e1} = fma({e1, e1}, {1, -1}, {e2, e2}),  {px + py, px - py} likewise
+__device__ __forceinline__ void kmul(const KOps& o, const PkK& k, f2 sxx, f2 syy, f32x16 (&acc)[4]) {
+    const f2 e01 = __builtin_elementwise_fma(o.u0, sxx, o.w0), e23 = __builtin_elementwise_fma(o.u1, sxx, o.w1);
+    const f2 pp = __builtin_elementwise_fma(o.r1, syy, o.r0);
+    const f2 b03 = pk_sub(k, e01, e23);
+    const f2 b12 = __builtin_elementwise_fma(e01.yy, k.pm, e23.xx);
+    const f2 a12 = __builtin_elementwise_fma(pp.yy, k.pm, pp.xx);
+    acc[0] = mfma32(pp.x, b03.x, acc[0]);
+    acc[1] = mfma32(a12.x, b12.x, acc[1]);
+    acc[2] = mfma32(a12.y, b12.y, acc[2]);
+    acc[3] = mfma32(pp.y, b03.y, acc[3]);
 }
 
-// K-steps s0 .. s0 + n - 1, software-pipelined: the reads of step s + 1 are in flight while step s
-// multiplies (two operand sets, alternating: no register moves)
-__device__ __forceinline__ void kloop(const float* w, const float* u, const float* q0, const float* q1, float sx,
-                                      float sy, f32x16 (&acc)[4], int n) {
+// K-steps 0 .. n - 1 from the row pointers, software-pipelined: the reads of step s + 1 are in flight while
+// step s multiplies (two operand sets, alternating: no register moves).  The pointers advance once per two
+// steps, so each read is a base register plus an immediate offset (no address arithmetic per step); the
+// last pair's look-ahead read of step n (n even) is a read past the strip inside the LDS row (unused).
+__device__ __forceinline__ void kloop(const float* w_, const float* u_, const float* q0_, const float* q1_, const PkK& k,
+                                      f2 sxx, f2 syy, f32x16 (&acc)[4], int n) {
     if (n <= 0) return;
+    // LDS pointers, opaque: the compiler re-added a lane offset to each pointer per step instead of folding it
+    // in once
+    lds_f* w = (lds_f*)w_;
+    lds_f* u = (lds_f*)u_;
+    lds_f* q0 = (lds_f*)q0_;
+    lds_f* q1 = (lds_f*)q1_;
+    asm volatile("" : "+v"(w), "+v"(u), "+v"(q0), "+v"(q1));
     KOps A = kload(w, u, q0, q1, 0);
     int s = 0;
     for (; s + 2 <= n; s += 2) {
-        const KOps Bn = kload(w, u, q0, q1, s + 1);
+        const KOps Bn = kload(w, u, q0, q1, 1);
         __builtin_amdgcn_sched_barrier(0);  // reads issued ahead of the MFMAs they overlap
-        kmul(A, sx, sy, acc);
+        kmul(A, k, sxx, syy, acc);
         __builtin_amdgcn_sched_barrier(0);
-        A = kload(w, u, q0, q1, s + 2 < n ? s + 2 : s + 1);
+        A = kload(w, u, q0, q1, 2);
         __builtin_amdgcn_sched_barrier(0);
-        kmul(Bn, sx, sy, acc);
+        kmul(Bn, k, sxx, syy, acc);
         __builtin_amdgcn_sched_barrier(0);
+        w += 8;
+        u += 8;
+        q0 += 8;
+        q1 += 8;
     }
-    if (s < n) kmul(A, sx, sy, acc);
+    if (s < n) kmul(A, k, sxx, syy, acc);
 }
 
 // one wave's work: Winograd row Q = wave (elements 4 Q .. 4 Q + 3) of the 32 x 32 channel block
@@ -333,6 +354,7 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
     const int IW = Q == 0 ? 0 : Q == 2 ? 2 : 1, IU = Q == 0 ? 2 : Q == 2 ? 1 : Q == 1 ? 2 : 3;
     const float sx = Q == 1 ? 1.f : -1.f;
     const float sy = Q == 1 ? 1.f : Q == 2 ? -1.f : 0.f;
+    const PkK pk = pk_consts();
     const float* const dr0 = dyl + (Q == 3 ? 32 * DCS : 0) + c32 * DCS + 2 * g;
     const float* const dr1 = dyl + 32 * DCS + c32 * DCS + 2 * g;
     auto ksteps = [&](const float* xw, const float* xu, int s0, int s1) {
@@ -341,7 +363,7 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
         const float* u = xu + 4 * s0;
         const float* q0 = dr0 + 4 * s0;
         const float* q1 = dr1 + 4 * s0;
-        kloop(w, u, q0, q1, sx, sy, acc, n);
+        kloop(w, u, q0, q1, pk, f2{sx, sx}, f2{sy, sy}, acc, n);
     };
     const int Ks = a.Ksteps;
     // Round 6 (PF: the V = 2 / 1 narrow images, 5-row tasks at cnn_small layers 5 / 6): the NEXT task's
