@@ -4,7 +4,9 @@
 //   kind 0 none, 1 v_fma_f32 (independent), 2 ds_read_b128 (results kept live, consumed at the end),
 //   3 buffer_load_dwordx4 ... lds (1 KiB LDS-DMA per wave-instruction, L2-resident source; vmcnt bounded),
 //   4 buffer_load_dword ... lds (256 B), 5 ds_read_b64, 6 v_add_f32 (inline asm, independent), 7 v_pk_add_f32
-//   (two f32 adds per lane), 8 v_pk_fma_f32, 9 v_max_f32 (inline asm, independent)
+//   (two f32 adds per lane), 8 v_pk_fma_f32, 9 v_max_f32 (inline asm, independent), 10 global_load_lds_dwordx4
+//   (saddr + voffset LDS-DMA, 1 KiB), 11 global_load_dwordx4 to VGPRs, 12 buffer_load_dwordx4 to VGPRs,
+//   13 ds_write_b128
 // at 1 wave per SIMD (256-thread blocks) and 2 waves per SIMD (512), one block per CU.  Prints cycles per
 // MFMA at the measured clock-free rate (ms) and the extra time per filler instruction.
 //   hipcc -O3 --offload-arch=gfx950 tools/mfma_mix.hip -o tools/mfma_mix && tools/mfma_mix
@@ -56,6 +58,23 @@ __global__ __launch_bounds__(512) void mix(const float* __restrict__ src, float*
                     asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(p2[(j * N + q) & 7]) : "v"(ka), "v"(kb));
                 if constexpr (KIND == 9)
                     asm volatile("v_max_f32 %0, %0, %1" : "+v"(v[(j * N + q) & 7]) : "v"(aa));
+                if constexpr (KIND == 10) {
+                    const unsigned m0 = __builtin_amdgcn_readfirstlane(ldsb + 8192u * (unsigned)((j * N + q) & 1));
+                    const unsigned voff = (unsigned)((lane * 16 + 1024 * ((it * 8 + j) * N + q)) & ((1 << 22) - 1));
+                    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" :: "v"(voff), "s"(src), "{m0}"(m0) : "memory");
+                }
+                if constexpr (KIND == 11) {
+                    const unsigned voff = (unsigned)((lane * 16 + 1024 * ((it * 8 + j) * N + q)) & ((1 << 22) - 1));
+                    asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(r4[(j * N + q) & 7]) : "v"(voff), "s"(src) : "memory");
+                }
+                if constexpr (KIND == 12) {
+                    const unsigned voff = (unsigned)((lane * 16 + 1024 * ((it * 8 + j) * N + q)) & ((1 << 22) - 1));
+                    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(r4[(j * N + q) & 7]) : "v"(voff), "s"(rs) : "memory");
+                }
+                if constexpr (KIND == 13) {
+                    const unsigned ad = ldsb + 16u * lane + 1024u * (unsigned)((j * N + q) & 7);
+                    asm volatile("ds_write_b128 %0, %1" :: "v"(ad), "v"(r4[(j * N + q) & 7]) : "memory");
+                }
                 if constexpr (KIND == 5) {
                     const unsigned ad = ldsb + 8u * lane + 1024u * (unsigned)((j * N + q) & 7);
                     float2 t;
@@ -72,9 +91,9 @@ __global__ __launch_bounds__(512) void mix(const float* __restrict__ src, float*
                 }
             }
         }
-        if constexpr (KIND == 3 || KIND == 4) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        if constexpr (KIND == 3 || KIND == 4 || KIND >= 10) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     }
-    if constexpr (KIND == 3 || KIND == 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (KIND == 3 || KIND == 4 || KIND >= 10) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     float s = 0.f;
 #pragma unroll
@@ -133,6 +152,11 @@ int main() {
         rep("buffer_load_dwordx4 lds", 1, run<3, 1>(src, threads, iters));
         rep("buffer_load_dwordx4 lds", 2, run<3, 2>(src, threads, iters));
         rep("buffer_load_dword lds", 1, run<4, 1>(src, threads, iters));
+        rep("global_load_lds_dwordx4", 1, run<10, 1>(src, threads, iters));
+        rep("global_load_dwordx4 (VGPR)", 1, run<11, 1>(src, threads, iters));
+        rep("buffer_load_dwordx4 (VGPR)", 1, run<12, 1>(src, threads, iters));
+        rep("ds_write_b128", 1, run<13, 1>(src, threads, iters));
+        rep("ds_write_b128", 2, run<13, 2>(src, threads, iters));
     }
     return 0;
 }
