@@ -115,6 +115,13 @@ __device__ __forceinline__ void wmul(const WOps& o, const PkK& k, f2 sxx, float 
     acc[3] = mfma32(pp.y, b03.y, acc[3]);
 }
 
+// (M A) exchange offset of row Q's pair for (channel, tile) pair p = 16 c + t: Q-major, 2 floats per pair, the
+// 32-float halves of each 64-float block swapped for odd c >> 2.  A data-gradient wave's write (lanes: 4 channels
+// c = 4 n_l + r apart by 4, 16 tiles) then covers the 64 banks once per 32 lanes, and the epilogue's reads
+// (consecutive p per lane) are contiguous; round 5's [p][Q][2] layout put the 64 lanes of a write on 8 bank
+// pairs (8-way conflicts; SQ_LDS_BANK_CONFLICT 2.36 cycles per LDS instruction in the kernel)
+__device__ __forceinline__ int xoff(int q, int p) { return q * 1024 + ((2 * p) ^ (((p >> 6) & 1) << 5)); }
+
 // XCT: the ring's channel stride as a compile-time constant (LDS offsets become instruction immediates:
 // ~20 address VALU per 16-tile group less), or 0 for a runtime stride
 // PD: dz rebuilt from the pooled gradient and the window selection (WinoBwdArgs::dzpool / parg)
@@ -129,7 +136,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
     const int XCS = XCT ? XCT : a.XCS, H = a.H, W = a.W, HW = H * W;
     float* const xr = smem + 4;                // x ring [4][32][XCS]
     float* const dr = xr + 4 * CH * XCS;       // dy ring [4][32][XCS]
-    float* const xb = dr + 4 * CH * XCS;       // (M A) exchange [2][512 (c, tile) pairs][8]
+    float* const xb = dr + 4 * CH * XCS;       // (M A) exchange [2][4 Q][512 (c, tile) pairs p][2] (xoff)
     const int slice = blockIdx.x;
     const int TR = (H + 1) >> 1;
 
@@ -422,7 +429,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
                             const int c = 16 * cs + 4 * n_l + r;
                             const float m0 = acc[0][cs][r] + acc[1][cs][r] + acc[2][cs][r];
                             const float m1 = acc[1][cs][r] - acc[2][cs][r] - acc[3][cs][r];
-                            *reinterpret_cast<f2*>(xo + (c * 16 + t_l) * 8 + 2 * Q) = f2{m0, m1};
+                            *reinterpret_cast<f2*>(xo + xoff(Q, c * 16 + t_l)) = f2{m0, m1};
                         }
 #endif
                     if (pre && WB_LOADPOS == 1) load(tr + 1, g, ng);
@@ -450,8 +457,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
                     for (int k2 = 0; k2 < 2; ++k2) {
                         const int p = ld + 256 * k2, c = p >> 4, tile = 16 * g + (p & 15);
                         if (tile >= S) continue;
-                        const f32x4 m0 = *reinterpret_cast<const f32x4*>(xi + p * 8);
-                        const f32x4 m1 = *reinterpret_cast<const f32x4*>(xi + p * 8 + 4);
+                        const f2 v0 = *reinterpret_cast<const f2*>(xi + xoff(0, p));
+                        const f2 v1 = *reinterpret_cast<const f2*>(xi + xoff(1, p));
+                        const f2 v2 = *reinterpret_cast<const f2*>(xi + xoff(2, p));
+                        const f2 v3 = *reinterpret_cast<const f2*>(xi + xoff(3, p));
+                        const f32x4 m0 = {v0.x, v0.y, v1.x, v1.y};
+                        const f32x4 m1 = {v2.x, v2.y, v3.x, v3.y};
                         // m0 = {q0 j0, q0 j1, q1 j0, q1 j1}, m1 = {q2 j0, q2 j1, q3 j0, q3 j1}
                         const float y00 = m0[0] + m0[2] + m1[0], y01 = m0[1] + m0[3] + m1[1];
                         const float y10 = m0[2] - m1[0] - m1[2], y11 = m0[3] - m1[1] - m1[3];
