@@ -109,26 +109,34 @@ __device__ __forceinline__ float row16_sum(float v) {
 }
 // transposed butterfly: v[j] (j < 8) summed over the 16 lanes of a row in 8 shuffles; lane n
 // returns the total of j = (n >> 1) & 7
+// (every element passes an empty asm first: a select between two loads of a local array was otherwise turned
+// into one dynamically indexed load, which kept the array in scratch -- a store per element and a scratch load
+// per unit in the forward epilogue)
+__device__ __forceinline__ float opq(float x) {
+    asm("" : "+v"(x));
+    return x;
+}
 __device__ __forceinline__ float row16_xsum8(const float (&v)[8], int n) {
     const bool b3 = n & 8, b2 = n & 4, b1 = n & 2;
-    float w4[4], w2[2];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) w4[j] = (b3 ? v[j + 4] : v[j]) + __shfl_xor(b3 ? v[j] : v[j + 4], 8, 64);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) w2[j] = (b2 ? w4[j + 2] : w4[j]) + __shfl_xor(b2 ? w4[j] : w4[j + 2], 4, 64);
-    const float w1 = (b1 ? w2[1] : w2[0]) + __shfl_xor(b1 ? w2[0] : w2[1], 2, 64);
+    const float a0 = (b3 ? v[4] : v[0]) + __shfl_xor(b3 ? v[0] : v[4], 8, 64);
+    const float a1 = (b3 ? v[5] : v[1]) + __shfl_xor(b3 ? v[1] : v[5], 8, 64);
+    const float a2 = (b3 ? v[6] : v[2]) + __shfl_xor(b3 ? v[2] : v[6], 8, 64);
+    const float a3 = (b3 ? v[7] : v[3]) + __shfl_xor(b3 ? v[3] : v[7], 8, 64);
+    const float c0 = (b2 ? a2 : a0) + __shfl_xor(b2 ? a0 : a2, 4, 64);
+    const float c1 = (b2 ? a3 : a1) + __shfl_xor(b2 ? a1 : a3, 4, 64);
+    const float w1 = (b1 ? c1 : c0) + __shfl_xor(b1 ? c0 : c1, 2, 64);
     return w1 + __shfl_xor(w1, 1, 64);
 }
 
 // select v[(n >> 1) & 7] with the butterfly's lane bits (no shuffles)
 __device__ __forceinline__ float row16_xsel8(const float (&v)[8], int n) {
     const bool b3 = n & 8, b2 = n & 4, b1 = n & 2;
-    float w4[4], w2[2];
+    float w[8];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) w4[j] = b3 ? v[j + 4] : v[j];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) w2[j] = b2 ? w4[j + 2] : w4[j];
-    return b1 ? w2[1] : w2[0];
+    for (int j = 0; j < 8; ++j) w[j] = opq(v[j]);
+    const float a0 = b3 ? w[4] : w[0], a1 = b3 ? w[5] : w[1], a2 = b3 ? w[6] : w[2], a3 = b3 ? w[7] : w[3];
+    const float c0 = b2 ? a2 : a0, c1 = b2 ? a3 : a1;
+    return b1 ? c1 : c0;
 }
 
 
@@ -594,11 +602,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     // order from that XCD's counter (then help the other XCDs), so neighbours are in flight together.
     const int nq = (a.queue && !(G & 7)) ? 8 : 1;
     int* qsl = reinterpret_cast<int*>(red + 512);  // [2]: the next unit, by unit parity
+    // (queue q covers units [q nunits / nq, (q + 1) nunits / nq): nq is 1 or 8 and nunits < 2^22 (host-checked),
+    // so a shift, not the 64-bit division the compiler emitted for `/ nq` -- ~150 scalar instructions per grab)
+    const int lq = nq == 8 ? 3 : 0;
     auto grab = [&]() -> int {  // lane 0 of wave 0 only
         const int x0 = nq == 8 ? (int)(blockIdx.x & 7) : 0;
         for (int k = 0; k < nq; ++k) {
             const int q = (x0 + k) & (nq - 1);
-            const int lo = (int)((int64_t)q * nunits / nq), len = (int)((int64_t)(q + 1) * nunits / nq) - lo;
+            const int lo = (q * nunits) >> lq, len = (((q + 1) * nunits) >> lq) - lo;
             const int v = atomicAdd(a.queue + 32 * q, 1);
             if (v < len) return lo + v;
         }
@@ -679,14 +690,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
         if constexpr (X4) {
             // granule gi = 64 j + lane of the chunk: plane gi / 40, row (gi % 40) / 10, slot column 4 (gi % 10);
             // offsets relative to a.src + (b cin + c0) HW - 1 (the granule of image column -1 starts in range)
+            // (branch-free: with short-circuit && the compiler put the offset multiply under exec-mask branches,
+            // ~50 instructions per copy offset and unit; here every term is evaluated and one select picks)
             const int SB = (segw + 3) & ~3, segwB = 2 * (16 - len_a) + 2;
+            const bool twoseg = len_a < 16;
 #pragma unroll
             for (int j = 0; j < NCP; ++j) {
                 const int gi = 64 * j + lane, pl = gi / 40, gg = gi - pl * 40, r = gg / 10, sc = 4 * (gg - r * 10);
                 const bool sB = sc >= SB;
                 const int grow = r + (sB ? rb1 : rb0), gcol = sB ? sc - SB - 1 : cb0 + sc;
-                const bool ok = (unsigned)grow < (unsigned)a.H && (sB ? (len_a < 16 && sc - SB < segwB) : sc < segw);
-                voff[j] = ok ? 4u * (unsigned)(pl * HW + grow * a.W + gcol + 1) : 0x80000000u;
+                const bool colok = sB ? (twoseg & (sc - SB < segwB)) : (sc < segw);
+                const bool ok = ((unsigned)grow < (unsigned)a.H) & colok;
+                const unsigned off = 4u * (unsigned)(pl * HW + grow * a.W + gcol + 1);
+                voff[j] = ok ? off : 0x80000000u;
             }
             return;
         }
