@@ -187,7 +187,7 @@ __device__ __forceinline__ bool last_wave(float* red, int lane) {
 // 16 consecutive tiles of one or two tile rows, so a store of one output row is a 128-byte run.
 // red: 512 floats of LDS private to the epilogue.
 template <int EPI, bool V4>
-__device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y)[8][4], float* red, int b,
+__device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y)[8][4], float* red, const float4* cfl, int b,
                                               int tb, int n0, int tr, int tc, bool tvalid, int wave, int tid) {
     const int lane = tid & 63, n = lane & 15, kq = lane >> 4;
     const int HW = a.H * a.W;
@@ -225,6 +225,10 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
         float cnt = 0.f;
 #pragma unroll
         for (int e = 0; e < 4; ++e) cnt += ok[e] ? 1.f : 0.f;
+        // (round 6: the shifted sums packed over channel pairs j, j + 1 -- the register pairs the packed output
+        // transform produced -- with the validity as a 0 / 1 factor: 15 packed instructions per two channels
+        // instead of 32 scalar ones; the outputs of invalid tiles are finite)
+        const PkK pk = pk_consts();
         float s1[8], s2[8], kv[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -238,15 +242,20 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
                 for (int e = 0; e < 4; ++e) bst1(rs, oe[e], so, v[e]);
             }
             kv[j] = __shfl(v[0], lane & 48, 64);
-            float t1 = 0.f, t2 = 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+            const pk_f2 kk = {kv[j], kv[j + 1]};
+            pk_f2 t = {0.f, 0.f}, q = {0.f, 0.f};
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const float dd = ok[e] ? v[e] - kv[j] : 0.f;
-                t1 += dd;
-                t2 = fmaf(dd, dd, t2);
+                const float m = ok[e] ? 1.f : 0.f;
+                const pk_f2 d = pk_sub(pk, pk_f2{y[j][e], y[j + 1][e]}, kk) * pk_f2{m, m};
+                t = e ? t + d : d;
+                q = e ? __builtin_elementwise_fma(d, d, q) : d * d;
             }
-            s1[j] = t1;
-            s2[j] = t2;
+            s1[j] = t.x; s1[j + 1] = t.y;
+            s2[j] = q.x; s2[j + 1] = q.y;
         }
         const float T1 = row16_xsum8(s1, n), T2 = row16_xsum8(s2, n);
         const float K = row16_xsel8(kv, n);
@@ -317,7 +326,7 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
             for (int j = 0; j < 8; ++j) {
                 const int co = 16 * (j >> 2) + 4 * kq + (j & 3);
                 const int so = chs(j, 4 * HW);
-                cf[j] = a.cf_out[n0 + co];
+                cf[j] = cfl[n0 + co];
                 if (vec) {
                     const float2 p0 = bld2(ry, oe[0], so), p1 = bld2(ry, oe[2], so);
                     yy[j][0] = p0.x; yy[j][1] = p0.y; yy[j][2] = p1.x; yy[j][3] = p1.y;
@@ -372,7 +381,7 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
                     const int j = 4 * half + jj;
                     const int co = 16 * (j >> 2) + 4 * kq + (j & 3);
                     const int so = chs(j, 4 * HW), sb = chs(j, HW);
-                    cf[jj] = a.cf_out[n0 + co];
+                    cf[jj] = cfl[n0 + co];
                     dv[jj] = a.drop_out ? a.drop_out[(int64_t)b * a.cout + n0 + co] : 1.f;
                     if (vec) {
                         const float2 p0 = bld2(ry, oe[0], so), p1 = bld2(ry, oe[2], so);
@@ -465,7 +474,7 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
                 for (int jj = 0; jj < PB; ++jj) {
                     const int j = PB * half + jj;
                     const int co = 16 * (j >> 2) + 4 * kq + (j & 3);
-                    cf[jj] = a.cf_out[n0 + co];
+                    cf[jj] = cfl[n0 + co];
                     dv[jj] = a.drop_out ? a.drop_out[(int64_t)b * a.cout + n0 + co] : 1.f;
                     const float* yp = yb + (int64_t)co * HWs;
                     if (V4) {  // host-checked: H, W even, Ws % 4 == 0: a tile's window is four 16-byte rows
@@ -582,7 +591,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     const int HW = a.H * a.W;
     const PkK pk = pk_consts();
     float* cft = smem + 2 * BUFF;             // [cin] float2 {s, t}
-    float* red = cft + 2 * a.cin;             // epilogue scratch (512 floats)
+    float* red = cft + 2 * a.cin;             // epilogue scratch (512 floats + the queue slots and the counter)
+    // data-gradient epilogues: the producer BN's coefficients per output channel, read from LDS (round 6: eight
+    // 16-byte global loads per unit and lane, with their 64-bit address arithmetic, exposed at the unit's end)
+    constexpr bool CFL = EPI != EPI_FWD && EPI != EPI_BWD_STORE;
+    float4* cfl = reinterpret_cast<float4*>(red + 516);
+    if (CFL)
+        for (int c = tid; c < a.cout; c += 256) cfl[c] = a.cf_out[c];
     const unsigned lds0 = (unsigned)(uintptr_t)(lds_void*)smem;
     if (PRO != PRO_RAW)
         for (int c = tid; c < a.cin; c += 256) {
@@ -983,7 +998,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
             if (t == 1234.5f) a.out[tid] = t;
         }
 #else
-        wino_epilogue<EPI, V4>(a, y, red, lb, cur.tb, cur.cg * 32, tr, tc, tvalid, wave, tid);
+        wino_epilogue<EPI, V4>(a, y, red, cfl, lb, cur.tb, cur.cg * 32, tr, tc, tvalid, wave, tid);
 #endif
         u = un;
         cur = nxt;
@@ -1124,7 +1139,8 @@ int launch_conv3x3_wino(int pro, int epi, ConvArgs a, hipStream_t s) {
     PCX_CHECK_ARG(epi != EPI_BWD_POOLSELP || a.dpool, "conv3x3_wino: EPI_BWD_POOLSELP needs dpool");
     const int ck = wino_ck(a.cin);
     const size_t buff = (size_t)4 * (ck * WSP + 32) + (size_t)ck * 512;
-    const size_t smem = (2 * buff + 2 * (size_t)a.cin + 512 + 4) * 4;  // + the queue's 2 ints
+    const bool cfl = epi != EPI_FWD && epi != EPI_BWD_STORE;  // + the epilogue's BN coefficients (float4 per channel)
+    const size_t smem = (2 * buff + 2 * (size_t)a.cin + 512 + 4 + (cfl ? 4 * (size_t)a.cout : 0)) * 4;
     PCX_CHECK_ARG(smem <= 160 * 1024, "conv3x3_wino: %zu B of LDS", smem);
     // persistent workgroups: two per CU (a multiple of 8, one XCD-contiguous run of units each round)
     const int64_t units = (int64_t)g.nblk * g.ncg;
