@@ -522,6 +522,36 @@ int launch_conv3x3_dma(int pro, int epi, ConvArgs a, hipStream_t s) {
     return PCX_EINVAL;
 }
 
+// x = drop[b, c] relu(ysel s_c + t_c) at the pooled resolution: bn_relu_pool_kernel's output value at the window's
+// selected element (the same fmaf, the same product with the dropout factor), 16 bytes per thread and step
+__global__ __launch_bounds__(256) void pool_act_kernel(const float4* __restrict__ ysel, const float4* __restrict__ cf,
+                                                       const float* __restrict__ drop, float4* __restrict__ x, int C,
+                                                       int q4, int64_t n4) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+        const int bc = (int)(i / q4);
+        const float4 k = cf[bc % C];
+        const float d = drop ? drop[bc] : 1.f;
+        const float4 v = ysel[i];
+        float4 o;
+        o.x = d * fmaxf(fmaf(v.x, k.x, k.y), 0.f);
+        o.y = d * fmaxf(fmaf(v.y, k.x, k.y), 0.f);
+        o.z = d * fmaxf(fmaf(v.z, k.x, k.y), 0.f);
+        o.w = d * fmaxf(fmaf(v.w, k.x, k.y), 0.f);
+        x[i] = o;
+    }
+}
+
+int launch_pool_act(const float* ysel, const float4* cf, const float* drop, float* x, int B, int C, int HWp,
+                    hipStream_t s) {
+    PCX_CHECK_ARG(HWp % 4 == 0 && (int64_t)B * C < ((int64_t)1 << 31), "pool_act: %d pooled pixels per plane", HWp);
+    const int64_t n4 = (int64_t)B * C * (HWp / 4);
+    const int blocks = (int)std::min<int64_t>(ceil_div(n4, (int64_t)256), (int64_t)num_cus() * 16);
+    pool_act_kernel<<<blocks, 256, 0, s>>>(reinterpret_cast<const float4*>(ysel), cf, drop,
+                                           reinterpret_cast<float4*>(x), C, HWp / 4, n4);
+    PCX_LAUNCH_CHECK("pool_act_kernel");
+    return PCX_OK;
+}
+
 int launch_bn_relu_pool(const float* y, const float4* cf, const float* drop, float* x, int B, int C,
                         int Hs, int Ws, hipStream_t s, float* ysel, uint8_t* parg) {
     PCX_CHECK_ARG((ysel == nullptr) == (parg == nullptr), "bn_relu_pool: ysel and parg go together");

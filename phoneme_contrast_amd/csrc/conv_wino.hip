@@ -186,7 +186,7 @@ __device__ __forceinline__ bool last_wave(float* red, int lane) {
 // of its tile (outputs y[j][e] at (2 tr + (e >> 1), 2 tc + (e & 1))).  The 16 lanes of a row hold
 // 16 consecutive tiles of one or two tile rows, so a store of one output row is a 128-byte run.
 // red: 512 floats of LDS private to the epilogue.
-template <int EPI, bool V4>
+template <int EPI, bool V4, bool POOL>
 __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y)[8][4], float* red, const float4* cfl, int b,
                                               int tb, int n0, int tr, int tc, bool tvalid, int wave, int tid) {
     const int lane = tid & 63, n = lane & 15, kq = lane >> 4;
@@ -265,6 +265,38 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
             d[0] = T1; d[1] = T2; d[2] = K;
         }
         if (lane == 0) red[384 + wave] = cnt;  // valid outputs of the wave (all channels alike)
+        if constexpr (POOL) {
+            // (round 6) the consumer block's 2x2 max-pool selection, made here: a tile IS a pooling window (H, W
+            // even, host-checked).  relu(s y + t) with s = gamma invstd is monotone in y with the sign of gamma,
+            // so the window's first maximum of relu(BN(y)) -- torch max_pool2d's rule, bn_relu_pool_kernel's --
+            // is the first maximum of y (gamma > 0), the first minimum (gamma < 0), or the first element (gamma
+            // 0: all equal), wherever that maximum is positive; where it is not, the pooled value and every
+            // gradient through it are 0 whichever element is recorded.  Writes y at the selected element and
+            // its index at the pooled resolution (ysel / parg: the backward's EPI_BWD_POOLSEL inputs); the
+            // pooled activation is then one light pass over ysel (pool_act_kernel) instead of bn_relu_pool's
+            // full-resolution read of y.  sgn: the LDS table of sign(gamma) per output channel.
+            const float* sgn = reinterpret_cast<const float*>(cfl);
+            const int HWp = (a.H >> 1) * (a.W >> 1);
+            const __amdgpu_buffer_rsrc_t rsy = wrs(a.pool_ysel, HWp, 4), rsa = wrs(a.pool_arg, HWp, 1);
+            const unsigned pe = (unsigned)(lpl * HWp + tr * (a.W >> 1) + tc);
+            const unsigned oy = tvalid ? 4u * pe : WOOB, oa = tvalid ? pe : WOOB;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float sg = sgn[n0 + 16 * (j >> 2) + 4 * kq + (j & 3)];
+                float best = y[j][0] * sg, ys = y[j][0];
+                unsigned arg = 0;
+#pragma unroll
+                for (int e = 1; e < 4; ++e) {
+                    const float z = y[j][e] * sg;
+                    const bool gt = z > best;
+                    best = gt ? z : best;
+                    ys = gt ? y[j][e] : ys;
+                    arg = gt ? (unsigned)e : arg;
+                }
+                bst1(rsy, oy, chs(j, 4 * HWp), ys);
+                __builtin_amdgcn_raw_buffer_store_b8((unsigned char)arg, rsa, oa, chs(j, HWp), 0);
+            }
+        }
         // the last of the block's 4 waves to get here merges the 4 waves' statistics (round 6: no block barrier;
         // a __syncthreads here cost 3-6 % of the forward convs, profiles/r6_wino_epilogue_barrier.txt).  The
         // scratch is safe to reuse: every wave passes the next unit's first chunk barrier only after this merge.
@@ -576,8 +608,9 @@ __device__ __forceinline__ void wino_epilogue(const ConvArgs& a, const float (&y
 // sources of the granules straddle the image's left / right edges, and the out-of-image columns they
 // bring in (the neighbouring rows' values) are zeroed by selects in the border waves, for every prologue.
 // Needs 4 readable bytes before a.src (ConvArgs::src_guard: the plans carve a guard at the workspace start).
-template <int PRO, int EPI, int CK, bool V4, bool X4, bool SP = false>
+template <int PRO, int EPI, int CK, bool V4, bool X4, bool SP = false, bool POOL = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv_wino_kernel(ConvArgs a, WinoGeo g) {
+    static_assert(!POOL || (EPI == EPI_FWD && !SP), "pooled selection: forward epilogue, per-sample units");
     static_assert(!X4 || CK == 8, "16-byte staging covers whole 8-channel chunks");
     static_assert(!SP || X4, "spanning units stage by 16-byte copies");
     constexpr int WROW = X4 ? 40 : WSW;       // slot row width (floats)
@@ -598,6 +631,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     float4* cfl = reinterpret_cast<float4*>(red + 516);
     if (CFL)
         for (int c = tid; c < a.cout; c += 256) cfl[c] = a.cf_out[c];
+    if (POOL)  // the pooled selection's sign(gamma) per output channel, in the same LDS slot
+        for (int c = tid; c < a.cout; c += 256) {
+            const float gm = a.pool_gamma[c];
+            reinterpret_cast<float*>(cfl)[c] = gm > 0.f ? 1.f : gm < 0.f ? -1.f : 0.f;
+        }
     const unsigned lds0 = (unsigned)(uintptr_t)(lds_void*)smem;
     if (PRO != PRO_RAW)
         for (int c = tid; c < a.cin; c += 256) {
@@ -998,7 +1036,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
             if (t == 1234.5f) a.out[tid] = t;
         }
 #else
-        wino_epilogue<EPI, V4>(a, y, red, cfl, lb, cur.tb, cur.cg * 32, tr, tc, tvalid, wave, tid);
+        wino_epilogue<EPI, V4, POOL>(a, y, red, cfl, lb, cur.tb, cur.cg * 32, tr, tc, tvalid, wave, tid);
 #endif
         u = un;
         cur = nxt;
@@ -1139,8 +1177,10 @@ int launch_conv3x3_wino(int pro, int epi, ConvArgs a, hipStream_t s) {
     PCX_CHECK_ARG(epi != EPI_BWD_POOLSELP || a.dpool, "conv3x3_wino: EPI_BWD_POOLSELP needs dpool");
     const int ck = wino_ck(a.cin);
     const size_t buff = (size_t)4 * (ck * WSP + 32) + (size_t)ck * 512;
-    const bool cfl = epi != EPI_FWD && epi != EPI_BWD_STORE;  // + the epilogue's BN coefficients (float4 per channel)
-    const size_t smem = (2 * buff + 2 * (size_t)a.cin + 512 + 4 + (cfl ? 4 * (size_t)a.cout : 0)) * 4;
+    const bool pool = a.pool_ysel != nullptr;
+    // + the epilogue's BN coefficients (float4 per channel) or the pooled selection's signs (float per channel)
+    const bool cfl = epi != EPI_FWD && epi != EPI_BWD_STORE;
+    const size_t smem = (2 * buff + 2 * (size_t)a.cin + 512 + 4 + (cfl ? 4 * (size_t)a.cout : pool ? (size_t)a.cout : 0)) * 4;
     PCX_CHECK_ARG(smem <= 160 * 1024, "conv3x3_wino: %zu B of LDS", smem);
     // persistent workgroups: two per CU (a multiple of 8, one XCD-contiguous run of units each round)
     const int64_t units = (int64_t)g.nblk * g.ncg;
@@ -1164,6 +1204,16 @@ int launch_conv3x3_wino(int pro, int epi, ConvArgs a, hipStream_t s) {
         conv_wino_kernel<P_, E_, CK_, V4_, X4_><<<grid, 256, smem, s>>>(a, g);                          \
         PCX_LAUNCH_CHECK("conv_wino_kernel");                                                           \
         return PCX_OK;                                                                                  \
+    }
+    if (pool) {
+        PCX_CHECK_ARG(!sp && epi == EPI_FWD && pro == PRO_BNRELU && ck == 8 && x4 && a.pool_arg && a.pool_gamma &&
+                          !(a.H & 1) && !(a.W & 1),
+                      "conv3x3_wino: pooled selection needs the BN + ReLU forward with 16-byte staging at even H, W");
+        (void)hipFuncSetAttribute((const void*)conv_wino_kernel<PRO_BNRELU, EPI_FWD, 8, false, true, false, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        conv_wino_kernel<PRO_BNRELU, EPI_FWD, 8, false, true, false, true><<<grid, 256, smem, s>>>(a, g);
+        PCX_LAUNCH_CHECK("conv_wino_kernel (pooled selection)");
+        return PCX_OK;
     }
     if (sp) {
         if (epi == EPI_FWD) {

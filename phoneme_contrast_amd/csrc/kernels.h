@@ -54,6 +54,12 @@ struct ConvArgs {
     float* dpool;         // EPI_BWD_POOLSELP: the routed gradient at the pooled resolution [B][cout][H][W]
     int* queue;           // conv_wino: unit queue (WINO_QUEUE_INTS, zero before the first launch; each launch
                           // leaves it zero), nullptr = static unit order
+    // conv_wino EPI_FWD (optional, round 6): also the next block's 2x2 max-pool selection of relu(BN(y)) -- y at
+    // each window's selected element and its index at the pooled resolution [B][cout][H / 2][W / 2] -- from
+    // the sign of that BN's gamma (the selection bn_relu_pool_kernel records)
+    const float* pool_gamma;
+    float* pool_ysel;
+    uint8_t* pool_arg;
 };
 constexpr int WINO_QUEUE_INTS = 9 * 32;  // 8 per-XCD unit counters + a completion counter, 128 B apart
 
@@ -87,6 +93,10 @@ int launch_conv3x3_wino(int pro, int epi, ConvArgs a, hipStream_t s);
 // max_pool2d rule) and its index, for the EPI_BWD_POOLSEL data gradient
 int launch_bn_relu_pool(const float* y, const float4* cf, const float* drop, float* x, int B, int C,
                         int Hs, int Ws, hipStream_t s, float* ysel = nullptr, uint8_t* parg = nullptr);
+// the same block tail from a selection made by the producer conv (ConvArgs::pool_ysel): x = drop * relu(ysel s + t)
+// over [B][C][HWp] (HWp % 4 == 0)
+int launch_pool_act(const float* ysel, const float4* cf, const float* drop, float* x, int B, int C, int HWp,
+                    hipStream_t s);
 
 // Cin = 1 convolution (first layer), 3x3 pad 1, with BN statistics.
 struct Conv1Args {
@@ -145,6 +155,7 @@ struct WinoWgradArgs {
     float* part;          // [nslice][cout][cin][16] Winograd-domain partials
     float* dy_out;        // optional: dy written here by the cin-group-0 blocks
     int S, nseg, V, XCS, DCS, nd, nx, Ksteps;  // strip tiles, strips per row, vector width, LDS strides, items
+    int NH;               // input-channel halves per block (2: 64 input channels, 8 waves)
     size_t lds;
     int ntask, per_slice, nslice;
 };

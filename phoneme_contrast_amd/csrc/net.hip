@@ -103,6 +103,13 @@ int build_small(Plan& p) {
                 L4.W % 4 == 0 && L4.ww.V == 4 && (L4.ww.nseg == 1 || !(L4.ww.S & 1)) && L5.H == L4.H / 2 &&
                 L5.W == L4.W / 2 && !PCX_AB_NO_POOLDZ;
     }
+    // (round 6) the block tails behind layers 2 / 4: the producer's forward epilogue makes the 2x2 pool selection
+    // (its tiles are the windows), so the pooled activation is a light pass over the selected values
+    for (int l = 3; l <= 5; l += 2) {
+        Layer &L = p.L[l], &Lp = p.L[l - 1];
+        L.psel = L.pooled_in && L.ysel && Lp.wino && Lp.cin % 8 == 0 && !(Lp.H & 1) && !(Lp.W & 1) &&
+                 L.H == Lp.H / 2 && L.W == Lp.W / 2 && (L.H * L.W) % 4 == 0 && !PCX_AB_NO_PSEL;
+    }
     // first-layer weight gradient slices
     {
         p.wg1_nslice = wgrad1_nslice(B, H1, W1, 32, &p.wg1_rows);
@@ -216,8 +223,19 @@ int small_forward(const Plan& p, const float* const* P, float* const* bnstat, in
         c.nblk = L.wino ? L.nblk : (int)conv3x3_nblk(B, L.H, L.W, L.cout);
         c.src_guard = 1;  // workspace tensors (and the input never reaches a 3x3 conv)
         c.queue = p.wq ? at<int>(ws, p.wq) : nullptr;
+        if (l < 6 && p.L[l + 1].psel) {  // this conv's epilogue also makes the next block tail's pool selection
+            c.pool_gamma = P[p_bn_g(l)];
+            c.pool_ysel = at<float>(ws, p.L[l + 1].ysel);
+            c.pool_arg = at<uint8_t>(ws, p.L[l + 1].parg);
+        }
         int pro = PRO_BNRELU;
-        if (L.pooled_in) {  // block tail materialised once; the conv and its wgrad read it raw
+        if (L.pooled_in && L.psel) {  // block tail from the producer's selection: one light pass over ysel
+            Scope sc(&p.prof, s, "pool_act", l);
+            RC(launch_pool_act(at<float>(ws, L.ysel), c.cf_in, c.drop_in, at<float>(ws, L.xp), B, L.cin, L.H * L.W, s));
+            c.src = at<float>(ws, L.xp);
+            c.srcH = L.H; c.srcW = L.W;
+            pro = PRO_RAW;
+        } else if (L.pooled_in) {  // block tail materialised once; the conv and its wgrad read it raw
             Scope sc(&p.prof, s, "bn_relu_pool", l);
             RC(launch_bn_relu_pool(c.src, c.cf_in, c.drop_in, at<float>(ws, L.xp), B, L.cin, L.srcH,
                                    L.srcW, s, L.ysel ? at<float>(ws, L.ysel) : nullptr,

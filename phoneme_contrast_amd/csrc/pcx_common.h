@@ -117,3 +117,12 @@ inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 #ifndef PCX_AB_NO_EPSUMS          // 1: the BN-backward sums of the channel-last data gradient as a separate pass
 #define PCX_AB_NO_EPSUMS 0
 #endif
+#ifndef PCX_AB_WW_NH1             // 1: Winograd weight gradient blocks of 32 input channels only (no 8-wave NH = 2)
+#define PCX_AB_WW_NH1 0
+#endif
+#ifndef PCX_AB_NO_PSEL            // 1: block tails by bn_relu_pool (no pool selection in the producer's epilogue)
+#define PCX_AB_NO_PSEL 0
+#endif
+#ifndef PCX_AB_WW_ODD_ALL         // 1: odd-width Winograd weight gradients at any tile coverage (analysis builds)
+#define PCX_AB_WW_ODD_ALL 0
+#endif

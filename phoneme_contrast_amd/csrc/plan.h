@@ -140,6 +140,8 @@ struct Layer {  // one 3x3 conv of the trunk (L = 1..6)
     bool wgbd;             // weight AND data gradient in one kernel (wgbd_wino.hip: layer 2, W % 4 == 0)
     WinoBwdArgs wb;
     bool pd;               // wgbd: dz read as layer 3's pooled gradient + window selection (EPI_BWD_POOLSELP)
+    bool psel;             // pooled_in: ysel / parg written by the producer conv's epilogue (conv_wino POOL), xp
+                           // then one light pass over ysel (pool_act) instead of bn_relu_pool (round 6)
 };
 
 struct DeepPlan;  // deep.hip

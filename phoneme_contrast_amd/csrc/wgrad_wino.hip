@@ -46,7 +46,7 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BUF_FLAGS = 0x00020000;  // raw buffer, 32-bit data
 constexpr int OOB = 0x7fff0000;        // beyond every num_records: loads 0, stores dropped
-constexpr int NIR = 4;                 // staged vectors per thread and row (dy and x): 8 threads x 4 >= 32 per channel
+constexpr int NIR = 4;                 // staged x vectors per thread and row: 8 threads x 4 >= 32 per channel
 constexpr int NIT = 2 * NIR;           // per stage (two rows)
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* base, int64_t bytes) {
@@ -154,33 +154,40 @@ __device__ __forceinline__ void kloop(const float* w_, const float* u_, const fl
     if (s < n) kmul(A, k, sxx, syy, acc);
 }
 
-// one wave's work: Winograd row Q = wave (elements 4 Q .. 4 Q + 3) of the 32 x 32 channel block
-template <int PRO, int V, bool PD>
+// one wave's work: Winograd row Q = wave & 3 (elements 4 Q .. 4 Q + 3) of the 32 x 32 channel block of input
+// channel half h = wave >> 2.  NH = 2 (round 6): a block of 8 waves covers 32 output x 64 input channels, so every
+// staged dy value (two loads, the BN backward, an LDS and an HBM store) feeds twice the MFMAs; x staging per MFMA
+// is unchanged.  One block per CU instead of two (the same 8 waves).
+template <int PRO, int V, bool PD, int NH>
 __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int co0, int ci0, int slice) {
     const int tid = threadIdx.x, lane = tid & 63, c32 = lane & 31, g = lane >> 5;
-    const int Q = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int Q = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
+    const int hx = __builtin_amdgcn_readfirstlane(tid >> 8);  // the wave's input channel half (NH = 2)
     constexpr int NPT = V == 4 ? 2 : 4;  // parts of the next tile row's loads (V = 4: 4 parts spill)
+    constexpr int CX = 32 * NH;          // staged x channels
+    constexpr int TPD = 8 * NH;          // threads per dy channel
+    constexpr int NIRD = NIR / NH, NITD = 2 * NIRD;  // dy vectors per thread and row / stage
     const int XCS = a.XCS, DCS = a.DCS;
-    float* const xl = smem + 4;                   // [4 ring slots][32][XCS]
-    float* const dyl = xl + 4 * 32 * XCS;         // [2 rows][32][DCS]
+    float* const xl = smem + 4;                   // [4 ring slots][CX][XCS]
+    float* const dyl = xl + 4 * CX * XCS;         // [2 rows][32][DCS]
     const int H = a.H, W = a.W, HW = H * W;
     const int nd = a.nd, nx = a.nx;
 
-    // staging items: thread -> channel ch = tid >> 3 of the block (dy: cout co0 + ch, x: cin ci0 + ch)
-    // and, in each of the stage's two rows r, the vectors k = (tid & 7) + 8 m (m < NIR) of that channel:
-    // item i = NIR r + m.  Offsets are one per-thread base plus compile-time / uniform terms.
+    // staging items: x: thread -> channel ch = tid >> 3 (cin ci0 + ch) and, in each of the stage's two rows r,
+    // the vectors k = (tid & 7) + 8 m (m < NIR): item i = NIR r + m; dy: channel chd = tid / TPD (cout co0 + chd),
+    // vectors k = jd + TPD m (m < NIRD), jd = tid % TPD.  Offsets are one per-thread base plus compile-time /
+    // uniform terms.
     const int ch = tid >> 3, j0 = tid & 7;
-    const int dgb = ch * HW + V * j0, dlb = ch * DCS + V * j0;
+    const int chd = tid / TPD, jd = tid % TPD;
+    const int dgb = chd * HW + V * jd, dlb = chd * DCS + V * jd;
     const int xgb = ch * HW + V * j0 - V, xlb = ch * XCS + V * j0 - (V - 1);
     unsigned dex = 0, xex = 0;  // existing items (bit masks)
 #pragma unroll
-    for (int i = 0; i < 2 * NIR; ++i) {
-        const int k = j0 + 8 * (i % NIR);
-        dex |= (unsigned)(k < nd) << i;
-        xex |= (unsigned)(k < nx) << i;
-    }
+    for (int i = 0; i < NITD; ++i) dex |= (unsigned)(jd + TPD * (i % NIRD) < nd) << i;
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) xex |= (unsigned)(j0 + 8 * (i % NIR) < nx) << i;
     // BN backward coefficients of this thread's dy channel, BN + ReLU of its x channel
-    const float4 kd = a.cf_dy[co0 + ch];  // {a, mb, mgi, mean}: dy = a (dz - mb - (y - mean) mgi)
+    const float4 kd = a.cf_dy[co0 + chd];  // {a, mb, mgi, mean}: dy = a (dz - mb - (y - mean) mgi)
     const float A1 = kd.x, A2 = -kd.x * kd.z, A3 = kd.x * (kd.w * kd.z - kd.y);
     float xs = 1.f, xt = 0.f;
     if (PRO == PRO_BNRELU) {
@@ -196,9 +203,9 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
     const bool write_dy = a.dy_out != nullptr && ci0 == 0;
     const int TR = (H + 1) >> 1;
     const int t0s = slice * a.per_slice, t1s = min(a.ntask, t0s + a.per_slice);
-    vecf<V> dzv[NIT], yv[NIT], xv[NIT];
+    vecf<V> dzv[NITD], yv[NITD], xv[NIT];
     static_assert(!PD || V == 4, "pooled dz: 4-column items");
-    unsigned pav[NIT];  // PD: the items' two selection bytes (their two pooled gradients wait in dzv[m][0..1])
+    unsigned pav[NITD];  // PD: the items' two selection bytes (their two pooled gradients wait in dzv[m][0..1])
     const int Wp = W >> 1, HWp = (H >> 1) * Wp;
 
     // per-task state: the sample's buffer resources and the items' column validity (whole vectors: V
@@ -219,12 +226,13 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
                      PD ? (int64_t)32 * HWp : 0);
         t.ry = rsrc(a.y + ((int64_t)b * a.cout + co0) * HW, (int64_t)32 * HW * 4);
         t.rdo = rsrc(write_dy ? a.dy_out + ((int64_t)b * a.cout + co0) * HW : a.dz, write_dy ? (int64_t)32 * HW * 4 : 0);
-        t.rx = rsrc(a.src + ((int64_t)b * a.cin + ci0) * HW, (int64_t)32 * HW * 4);
+        t.rx = rsrc(a.src + ((int64_t)b * a.cin + ci0) * HW, (int64_t)CX * HW * 4);
         unsigned dcol = 0, xcol = 0;
+#pragma unroll
+        for (int i = 0; i < NITD; ++i) dcol |= (unsigned)(t.c0 + V * (jd + TPD * (i % NIRD)) < W) << i;
 #pragma unroll
         for (int i = 0; i < NIT; ++i) {
             const int kc = V * (j0 + 8 * (i % NIR));
-            dcol |= (unsigned)(t.c0 + kc < W) << i;
             xcol |= (unsigned)((unsigned)(t.c0 + kc - V) < (unsigned)W) << i;
         }
         t.dcol = dcol & dex;
@@ -233,14 +241,15 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
     };
 
     // stage st (= -1 .. TR - 1): dy rows 2 st, 2 st + 1 and x rows 2 st + 1, 2 st + 2
-    constexpr unsigned R1 = ((1u << NIR) - 1) << NIR;  // items of the stage's second row
+    constexpr unsigned R1 = ((1u << NIR) - 1) << NIR;     // x items of the stage's second row
+    constexpr unsigned R1D = ((1u << NIRD) - 1) << NIRD;  // dy items of the stage's second row
     auto masks = [&](const Task& t, int st, unsigned& dm, unsigned& xm) {
         const bool d0 = 2 * st >= 0, d1 = 2 * st + 1 >= 0 && 2 * st + 1 < H;
         const bool x0 = 2 * st + 1 >= 0 && 2 * st + 1 < H, x1 = 2 * st + 2 < H;
-        dm = t.dcol & ((d0 ? ~R1 : 0u) | (d1 ? R1 : 0u));
+        dm = t.dcol & ((d0 ? ~R1D : 0u) | (d1 ? R1D : 0u));
         xm = t.xcol & ((x0 ? ~R1 : 0u) | (x1 ? R1 : 0u));
     };
-    auto dgo = [&](int i) { return dgb + (i / NIR) * W + 8 * V * (i % NIR); };
+    auto dgo = [&](int i) { return dgb + (i / NIRD) * W + TPD * V * (i % NIRD); };
     auto xgo = [&](int i) { return xgb + (i / NIR) * W + 8 * V * (i % NIR); };
     // part: only the items m with m NPT / NIT == part (-1: all items)
     auto load_dy = [&](const Task& t, int st, int part) {
@@ -248,14 +257,14 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
         masks(t, st, dm, xm);
         int db = 2 * st * W + t.c0 + dgb;
         asm volatile("" : "+v"(db));  // opaque: per-item offsets formed at the load, not kept live
-        int pb = ch * HWp + st * Wp + ((t.c0 + V * j0) >> 1);  // PD: pooled row st (dy rows 2 st, 2 st + 1)
+        int pb = chd * HWp + st * Wp + ((t.c0 + V * jd) >> 1);  // PD: pooled row st (dy rows 2 st, 2 st + 1)
         if constexpr (PD) asm volatile("" : "+v"(pb));
 #pragma unroll
-        for (int m = 0; m < NIT; ++m) {
-            if (part >= 0 && m * NPT / NIT != part) continue;
+        for (int m = 0; m < NITD; ++m) {
+            if (part >= 0 && m * NPT / NITD != part) continue;
             const int o = (dm >> m) & 1 ? 4 * (dgo(m) - dgb + db) : OOB;
             if constexpr (PD) {
-                const int op = (dm >> m) & 1 ? pb + 4 * V * (m % NIR) : OOB / 4;
+                const int op = (dm >> m) & 1 ? pb + (TPD * V / 2) * (m % NIRD) : OOB / 4;
                 const vecf<2> dp = bload<2>(t.rdz, 4 * op);
                 dzv[m][0] = dp[0];
                 dzv[m][1] = dp[1];
@@ -271,11 +280,11 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
         unsigned dm, xm;
         masks(t, st, dm, xm);
 #pragma unroll
-        for (int m = 0; m < NIT; ++m) {
+        for (int m = 0; m < NITD; ++m) {
             const float a3 = (dm >> m) & 1 ? A3 : 0.f;
-            if constexpr (PD) {  // dz: each pooled gradient at its window's selected element (row parity m / NIR)
+            if constexpr (PD) {  // dz: each pooled gradient at its window's selected element (row parity m / NIRD)
                 const float g0 = dzv[m][0], g1 = dzv[m][1];
-                const unsigned pa = pav[m], i2 = 2u * (unsigned)(m / NIR);
+                const unsigned pa = pav[m], i2 = 2u * (unsigned)(m / NIRD);
 #pragma unroll
                 for (int e = 0; e < V; ++e)
                     dzv[m][e] = ((pa >> (8 * (e >> 1))) & 3u) == i2 + (unsigned)(e & 1) ? (e >> 1 ? g1 : g0) : 0.f;
@@ -297,7 +306,7 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
         unsigned dm, xm;
         masks(t, st, dm, xm);
         // x rows 2 st + 1, 2 st + 2 -> ring slots (2 st + 2) & 3, (2 st + 3) & 3
-        const int sl0 = ((2 * st + 2) & 3) * 32 * XCS, sl1 = ((2 * st + 3) & 3) * 32 * XCS;
+        const int sl0 = ((2 * st + 2) & 3) * CX * XCS, sl1 = ((2 * st + 3) & 3) * CX * XCS;
 #pragma unroll
         for (int m = 0; m < NIT; ++m) {
             if (!((xex >> m) & 1)) continue;
@@ -325,11 +334,11 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
         masks(t, st, dm, xm);
         const int db = 2 * st * W + t.c0;
 #pragma unroll
-        for (int m = 0; m < NIT; ++m) {
+        for (int m = 0; m < NITD; ++m) {
             if (!((dex >> m) & 1)) continue;
             const bool ok = (dm >> m) & 1;
             const vecf<V> v = dzv[m];
-            float* d = dyl + dlb + (m / NIR) * 32 * DCS + 8 * V * (m % NIR);
+            float* d = dyl + dlb + (m / NIRD) * 32 * DCS + TPD * V * (m % NIRD);
             if constexpr (V == 1) {
                 d[0] = v[0];
             } else {
@@ -377,8 +386,8 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
     auto row = [&](const Task& t, int tr, auto kind) {
         constexpr int KIND = decltype(kind)::value;
         // x rows 2 tr - 1 + i of this tile row live in ring slot (2 tr + i) & 3
-        const float* xw = xl + ((2 * tr + IW) & 3) * 32 * XCS + c32 * XCS + 2 * g;
-        const float* xu = xl + ((2 * tr + IU) & 3) * 32 * XCS + c32 * XCS + 2 * g;
+        const float* xw = xl + ((2 * tr + IW) & 3) * CX * XCS + (32 * hx + c32) * XCS + 2 * g;
+        const float* xu = xl + ((2 * tr + IU) & 3) * CX * XCS + (32 * hx + c32) * XCS + 2 * g;
         // the next tile row's dz / y / x rows loaded over this row's K-steps in NPT parts (a burst of 3
         // NIT loads at the row start stalls the issuing waves on the texture unit, MFMA pipes idle); dy
         // formed after the last part
@@ -429,26 +438,26 @@ __device__ __forceinline__ void ww_body(const WinoWgradArgs& a, float* smem, int
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int co = co0 + (r & 3) + 8 * (r >> 2) + 4 * g;
-        *reinterpret_cast<float4*>(out + ((int64_t)co * a.cin + ci0 + c32) * 16 + 4 * Q) =
+        *reinterpret_cast<float4*>(out + ((int64_t)co * a.cin + ci0 + 32 * hx + c32) * 16 + 4 * Q) =
             make_float4(acc[0][r], acc[1][r], acc[2][r], acc[3][r]);
     }
 }
 
-template <int PRO, int V, bool PD>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void wgrad_wino_kernel(WinoWgradArgs a) {
+template <int PRO, int V, bool PD, int NH>
+__global__ __launch_bounds__(256 * NH) __attribute__((amdgpu_waves_per_eu(2))) void wgrad_wino_kernel(WinoWgradArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x;
-    const int ncgi = a.cin / 32, ngroups = (a.cout / 32) * ncgi;
+    const int ncgi = a.cin / (32 * NH), ngroups = (a.cout / 32) * ncgi;
     const int f = blockIdx.x, kk = f >> 3;
     const int group = kk % ngroups;
     const int slice = (kk / ngroups) * 8 + (f & 7);  // XCD-aware: a slice's groups share an XCD
     if (slice >= a.nslice) return;
-    const int co0 = (group / ncgi) * 32, ci0 = (group % ncgi) * 32;
+    const int co0 = (group / ncgi) * 32, ci0 = (group % ncgi) * 32 * NH;
     // zero the staging image (padding positions and padded tiles read zeros)
-    const int nz = 4 + 4 * 32 * a.XCS + 2 * 32 * a.DCS;
-    for (int i = tid; i < nz; i += 256) smem[i] = 0.f;
+    const int nz = 4 + 4 * 32 * NH * a.XCS + 2 * 32 * a.DCS;
+    for (int i = tid; i < nz; i += 256 * NH) smem[i] = 0.f;
     __syncthreads();
-    ww_body<PRO, V, PD>(a, smem, co0, ci0, slice);
+    ww_body<PRO, V, PD, NH>(a, smem, co0, ci0, slice);
 }
 
 // dW[n][c] = G^T dU G per (n, c) from the slices' sum (float64, fixed order); the partials carry
@@ -529,7 +538,7 @@ bool wgrad_wino_geometry(int B, int H, int W, int cin, int cout, WinoWgradArgs* 
     const int TC = (W + 1) / 2;
     // odd widths only where the 2 x 2 tiles cover the image well: 5 x 25 (0.80 of the tiles' outputs real)
     // 5.77 vs 6.05 ms on the row-window kernel; 3 x 13 (0.70) 10.8 vs 8.7 ms (profiles/r5_wgrad_wino_odd.txt)
-    if (V == 1 && (double)H * W < 0.75 * 4.0 * ((H + 1) / 2) * TC) return false;
+    if (V == 1 && !PCX_AB_WW_ODD_ALL && (double)H * W < 0.75 * 4.0 * ((H + 1) / 2) * TC) return false;
     int nseg = ceil_div(TC, 50);
     int S = ceil_div(TC, nseg);
     if (nseg > 1) S = (S + 1) & ~1;  // strip starts 2 t0 on a 16-byte boundary (V = 4)
@@ -540,9 +549,12 @@ bool wgrad_wino_geometry(int B, int H, int W, int cin, int cout, WinoWgradArgs* 
     if (2 * nd > 8 * NIT || 2 * nx > 8 * NIT) return false;  // 8 threads x NIT items per channel
     const int XCS = smallest_2odd(std::max(std::max(V * kmax + 1, 4 * Ksteps + 2), 2 * S + 5));
     const int DCS = smallest_2odd(4 * Ksteps);
-    const size_t lds = ((size_t)4 + 128 * XCS + 64 * DCS) * 4;
-    if (lds > 80 * 1024) return false;
-    if ((int64_t)32 * H * W * 4 >= OOB) return false;  // valid offsets stay below the out-of-range marker
+    // NH = 2 (64 input channels per block of 8 waves, one block per CU) where the input channels and LDS allow
+    const int NH = (cin % 64 == 0 && !PCX_AB_WW_NH1 &&
+                    ((size_t)4 + 256 * XCS + 64 * DCS) * 4 <= 160 * 1024) ? 2 : 1;
+    const size_t lds = ((size_t)4 + 128 * NH * XCS + 64 * DCS) * 4;
+    if (lds > 80 * 1024 * NH) return false;
+    if ((int64_t)64 * H * W * 4 >= OOB) return false;  // valid offsets (NH = 2: 64 x planes) stay below the marker
     if (a) {
         a->S = S;
         a->nseg = nseg;
@@ -553,9 +565,10 @@ bool wgrad_wino_geometry(int B, int H, int W, int cin, int cout, WinoWgradArgs* 
         a->nx = nx;
         a->Ksteps = Ksteps;
         a->lds = lds;
+        a->NH = NH;
         a->ntask = B * nseg;
-        const int ngroups = (cout / 32) * (cin / 32);
-        int want = std::max(8, 2 * num_cus() / ngroups);  // ~2 resident blocks per CU
+        const int ngroups = (cout / 32) * (cin / (32 * NH));
+        int want = std::max(8, (2 / NH) * num_cus() / ngroups);  // ~2 (NH = 2: 1) resident blocks per CU
         want = std::min(want, a->ntask);
         a->per_slice = ceil_div(a->ntask, want);
         a->nslice = ceil_div(a->ntask, a->per_slice);
@@ -568,24 +581,25 @@ int launch_wgrad_wino(int pro, WinoWgradArgs a, hipStream_t s) {
     PCX_CHECK_ARG(wgrad_wino_geometry(a.B, a.H, a.W, a.cin, a.cout, &g), "wgrad_wino: unsupported shape %dx%d (%d, %d)",
                   a.H, a.W, a.cin, a.cout);
     PCX_CHECK_ARG(g.S == a.S && g.V == a.V && g.XCS == a.XCS && g.DCS == a.DCS && g.nslice == a.nslice &&
-                      g.per_slice == a.per_slice && g.ntask == a.ntask,
+                      g.per_slice == a.per_slice && g.ntask == a.ntask && g.NH == a.NH,
                   "wgrad_wino: geometry mismatch");
     PCX_CHECK_ARG(pro == PRO_RAW || pro == PRO_BNRELU, "wgrad_wino: prologue %d", pro);
-    const int ngroups = (a.cout / 32) * (a.cin / 32);
+    const int ngroups = (a.cout / 32) * (a.cin / (32 * a.NH));
     dim3 grid((unsigned)(((a.nslice + 7) / 8) * 8 * ngroups));
     PCX_CHECK_ARG((a.dz != nullptr) != (a.dzpool != nullptr), "wgrad_wino: exactly one of dz / dzpool");
     const bool pd = a.dzpool != nullptr;
     // pooled dz: 4-column items over whole windows, 2-byte aligned selection pairs (even strip starts)
     PCX_CHECK_ARG(!pd || (a.parg && pro == PRO_BNRELU && a.V == 4 && !(a.H & 1) && (a.nseg == 1 || !(a.S & 1))),
                   "wgrad_wino: pooled dz needs parg, PRO_BNRELU, V = 4, even H and even strip starts");
-#define PCX_WW(P_, V_, PD_)                                                                              \
-    if (pro == P_ && a.V == V_ && pd == PD_) {                                                           \
-        (void)hipFuncSetAttribute((const void*)wgrad_wino_kernel<P_, V_, PD_>,                           \
+#define PCX_WW1(P_, V_, PD_, NH_)                                                                        \
+    if (pro == P_ && a.V == V_ && pd == PD_ && a.NH == NH_) {                                            \
+        (void)hipFuncSetAttribute((const void*)wgrad_wino_kernel<P_, V_, PD_, NH_>,                      \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)a.lds);               \
-        wgrad_wino_kernel<P_, V_, PD_><<<grid, 256, a.lds, s>>>(a);                                      \
+        wgrad_wino_kernel<P_, V_, PD_, NH_><<<grid, 256 * NH_, a.lds, s>>>(a);                           \
         PCX_LAUNCH_CHECK("wgrad_wino_kernel");                                                           \
         return PCX_OK;                                                                                   \
     }
+#define PCX_WW(P_, V_, PD_) PCX_WW1(P_, V_, PD_, 1) PCX_WW1(P_, V_, PD_, 2)
     PCX_WW(PRO_RAW, 4, false)
     PCX_WW(PRO_RAW, 2, false)
     PCX_WW(PRO_BNRELU, 4, false)
@@ -594,6 +608,7 @@ int launch_wgrad_wino(int pro, WinoWgradArgs a, hipStream_t s) {
     PCX_WW(PRO_RAW, 1, false)
     PCX_WW(PRO_BNRELU, 1, false)
 #undef PCX_WW
+#undef PCX_WW1
     set_error("wgrad_wino: unsupported combination (pro %d, vec %d)", pro, a.V);
     return PCX_EINVAL;
 }
