@@ -4,9 +4,9 @@
 #           B = 4096 leg), both cnn_deep lines, rocprofv3 kernel stats of the cnn_small step;
 #   part b: PMC traffic per plan label (FETCH_SIZE / WRITE_SIZE passes mapped by ROCTx labels) for
 #           cnn_small and both cnn_deep lines, MFMA-busy + MOPS pass at B = 4096 for cnn_small.
-# Output under gpurun_out/ev6/.
+# Output under gpurun_out/ev6b/ (EVOUT).
 set -o pipefail
-OUT=gpurun_out/ev6
+OUT=gpurun_out/${EVOUT:-ev6b}
 mkdir -p $OUT
 export TMPDIR=/tmp
 PART=${1:-a}
