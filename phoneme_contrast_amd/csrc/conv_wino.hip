@@ -1196,7 +1196,8 @@ int launch_conv3x3_wino(int pro, int epi, ConvArgs a, hipStream_t s) {
     // copy offsets of X4 made that 31-34)
     // measured at B = 4096 (profiles/r4_x4_time.txt): BN + ReLU forward and the data gradients gain
     // 3-6 %, the raw-input forward (L3 / L5: 32 -> 64, 64 -> 128) nothing or -2.5 %: dword copies there
-    const bool x4 = ck == 8 && a.src_guard && x4_env && epi != EPI_BWD_POOL && !(pro == PRO_RAW && epi == EPI_FWD);
+    const bool x4 = ck == 8 && a.src_guard && x4_env && epi != EPI_BWD_POOL &&
+                    (PCX_AB_WINO_X4_RAWFWD || !(pro == PRO_RAW && epi == EPI_FWD));
 #define PCX_WINO_CASE(P_, E_, CK_, V4_, X4_)                                                            \
     if (pro == P_ && epi == E_ && ck == CK_ && v4 == V4_ && x4 == X4_) {                                \
         (void)hipFuncSetAttribute((const void*)conv_wino_kernel<P_, E_, CK_, V4_, X4_>,                 \

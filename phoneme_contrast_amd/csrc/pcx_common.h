@@ -126,3 +126,6 @@ inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 #ifndef PCX_AB_WW_ODD_ALL         // 1: odd-width Winograd weight gradients at any tile coverage (analysis builds)
 #define PCX_AB_WW_ODD_ALL 0
 #endif
+#ifndef PCX_AB_WINO_X4_RAWFWD     // 1: 16-byte operand copies for the raw-input Winograd forward too (layers 3 / 5)
+#define PCX_AB_WINO_X4_RAWFWD 0
+#endif
