@@ -15,27 +15,33 @@ __device__ __forceinline__ float conv_sum32(float v) {  // reduce within each 32
 // (instead of 16 x 5).  Lane l of a half returns the total of r = (l >> 1) & 15.  `sel` gets the
 // same lane-bit selection applied to a half-uniform array (no shuffles): sel = u[(l >> 1) & 15].
 __device__ __forceinline__ float xsum16(const float (&v)[16], int l32) {
+    // (named scalars at every level: selects between elements of a local array became one dynamically indexed
+    // load, which kept the array in scratch -- 16 stores and an indexed scratch load per call: round 6)
     const bool b4 = l32 & 16, b3 = l32 & 8, b2 = l32 & 4, b1 = l32 & 2;
-    float w8[8], w4[4], w2[2];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) w8[j] = (b4 ? v[j + 8] : v[j]) + __shfl_xor(b4 ? v[j] : v[j + 8], 16, 64);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) w4[j] = (b3 ? w8[j + 4] : w8[j]) + __shfl_xor(b3 ? w8[j] : w8[j + 4], 8, 64);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) w2[j] = (b2 ? w4[j + 2] : w4[j]) + __shfl_xor(b2 ? w4[j] : w4[j + 2], 4, 64);
-    float w1 = (b1 ? w2[1] : w2[0]) + __shfl_xor(b1 ? w2[0] : w2[1], 2, 64);
+#define PCX_X8(j) const float w8_##j = (b4 ? v[j + 8] : v[j]) + __shfl_xor(b4 ? v[j] : v[j + 8], 16, 64);
+    PCX_X8(0) PCX_X8(1) PCX_X8(2) PCX_X8(3) PCX_X8(4) PCX_X8(5) PCX_X8(6) PCX_X8(7)
+#undef PCX_X8
+    const float w4_0 = (b3 ? w8_4 : w8_0) + __shfl_xor(b3 ? w8_0 : w8_4, 8, 64);
+    const float w4_1 = (b3 ? w8_5 : w8_1) + __shfl_xor(b3 ? w8_1 : w8_5, 8, 64);
+    const float w4_2 = (b3 ? w8_6 : w8_2) + __shfl_xor(b3 ? w8_2 : w8_6, 8, 64);
+    const float w4_3 = (b3 ? w8_7 : w8_3) + __shfl_xor(b3 ? w8_3 : w8_7, 8, 64);
+    const float w2_0 = (b2 ? w4_2 : w4_0) + __shfl_xor(b2 ? w4_0 : w4_2, 4, 64);
+    const float w2_1 = (b2 ? w4_3 : w4_1) + __shfl_xor(b2 ? w4_1 : w4_3, 4, 64);
+    const float w1 = (b1 ? w2_1 : w2_0) + __shfl_xor(b1 ? w2_0 : w2_1, 2, 64);
     return w1 + __shfl_xor(w1, 1, 64);
 }
+// select u[(l32 >> 1) & 15] with the butterfly's lane bits (named scalars, elements made opaque: as xsum16)
 __device__ __forceinline__ float xsel16(const float (&u)[16], int l32) {
     const bool b4 = l32 & 16, b3 = l32 & 8, b2 = l32 & 4, b1 = l32 & 2;
-    float w8[8], w4[4], w2[2];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) w8[j] = b4 ? u[j + 8] : u[j];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) w4[j] = b3 ? w8[j + 4] : w8[j];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) w2[j] = b2 ? w4[j + 2] : w4[j];
-    return b1 ? w2[1] : w2[0];
+#define PCX_S8(j)                                  \
+    float lo_##j = u[j], hi_##j = u[j + 8];        \
+    asm("" : "+v"(lo_##j), "+v"(hi_##j));          \
+    const float w8_##j = b4 ? hi_##j : lo_##j;
+    PCX_S8(0) PCX_S8(1) PCX_S8(2) PCX_S8(3) PCX_S8(4) PCX_S8(5) PCX_S8(6) PCX_S8(7)
+#undef PCX_S8
+    const float w4_0 = b3 ? w8_4 : w8_0, w4_1 = b3 ? w8_5 : w8_1, w4_2 = b3 ? w8_6 : w8_2, w4_3 = b3 ? w8_7 : w8_3;
+    const float w2_0 = b2 ? w4_2 : w4_0, w2_1 = b2 ? w4_3 : w4_1;
+    return b1 ? w2_1 : w2_0;
 }
 __device__ __forceinline__ float readlane_f(float v, int l) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));

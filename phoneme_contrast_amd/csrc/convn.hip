@@ -227,10 +227,12 @@ __device__ __forceinline__ int64_t xcd_logical(int64_t nblocks) {
 // 128-byte rows per MFMA output row), optionally the producer BN's backward sums (EP, mode 1) or the BN
 // forward partials (mode 0).  col[ni]: the flattened pixel of the lane's column (a valid pixel even where
 // valid[ni] is false), cnt_w: valid pixels among the wave's 32 WN columns, tn of ntile: the partials' tile.
+// bs >= 0 (the halo kernel, modes 0 / 1): every column of the tile is a pixel of sample bs, and col[] holds the
+// pixel's index inside that sample -- no per-lane 64-bit division (round 6: ~100 VALU per column).
 template <int MODE, int WM, int WN, bool EP, int NWC = 2>
 __device__ __forceinline__ void convn_epilogue(const ConvGArgs& a, const f32x16 (&acc)[WM][WN], char* smem, int64_t m0,
                                                int64_t M, const int64_t (&col)[WN], const bool (&valid)[WN], int cnt_w,
-                                               int64_t ntile, int64_t tn, int64_t tm) {
+                                               int64_t ntile, int64_t tn, int64_t tm, int bs = -1) {
     // (NWC wave columns of 32 WN pixels, two wave rows of 32 WM output rows)
     constexpr int BM = 64 * WM;
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
@@ -246,12 +248,12 @@ __device__ __forceinline__ void convn_epilogue(const ConvGArgs& a, const f32x16 
         int64_t obase, ostride;
         float* dst = a.out;
         if (MODE == 0) {
-            const int64_t b = cl / OHW;
-            obase = b * a.cout * OHW + (cl - b * OHW);
+            const int64_t b = bs >= 0 ? bs : cl / OHW;
+            obase = b * a.cout * OHW + (bs >= 0 ? cl : cl - b * OHW);
             ostride = OHW;
         } else if (MODE == 1) {
-            const int64_t b = cl / IHW;
-            obase = b * a.cin * IHW + (cl - b * IHW);
+            const int64_t b = bs >= 0 ? bs : cl / IHW;
+            obase = b * a.cin * IHW + (bs >= 0 ? cl : cl - b * IHW);
             ostride = IHW;
         } else {
             const int64_t b = cl / CHW, p = cl - b * CHW;
@@ -290,8 +292,8 @@ __device__ __forceinline__ void convn_epilogue(const ConvGArgs& a, const f32x16 
         int64_t yb[WN], db[WN];
 #pragma unroll
         for (int ni = 0; ni < WN; ++ni) {
-            const int64_t cc = col[ni], b = cc / IHWe;
-            yb[ni] = b * a.cin * IHWe + (cc - b * IHWe);
+            const int64_t cc = col[ni], b = bs >= 0 ? bs : cc / IHWe;
+            yb[ni] = b * a.cin * IHWe + (bs >= 0 ? cc : cc - b * IHWe);
             db[ni] = b * a.cin;
         }
 #pragma unroll
@@ -549,13 +551,15 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     else { CK = a.cout; H = a.IH; W = a.IW; M = a.cin; }
     Hp = H + 2; Wp = W + 2;
     const int64_t HW = (int64_t)H * W;
+    // (32-bit tile decode, host-checked mt * ntile < 2^31: the int64 divisions were ~100 scalar instructions each)
     const int tps = g.nsr * g.nsc;
-    const int64_t mt = (M + BM - 1) / BM, ntile = (int64_t)a.B * tps;
-    const int64_t lid = xcd_logical(mt * ntile);
-    if (lid >= mt * ntile) return;  // (grid padded to a multiple of 8)
-    const int64_t tm = lid % mt, tn = lid / mt;
-    const int64_t m0 = tm * BM;
-    const int b = (int)(tn / tps), tl = (int)(tn - (int64_t)b * tps);
+    const int mt = (int)((M + BM - 1) / BM), ntile = a.B * tps;
+    const unsigned nb = (unsigned)(mt * ntile), bid = blockIdx.x;
+    const unsigned lid = (bid & 7) * ((nb + 7) >> 3) + (bid >> 3);  // xcd_logical in 32 bits
+    if (lid >= nb) return;  // (grid padded to a multiple of 8)
+    const int tm = (int)(lid % (unsigned)mt), tn = (int)(lid / (unsigned)mt);
+    const int64_t m0 = (int64_t)tm * BM;
+    const int b = tn / tps, tl = tn - b * tps;
     const int sr = tl / g.nsc, sc = tl - sr * g.nsc;
     const int oh0 = sr * g.TR, ow0 = sc * g.TW;
     const int HW2 = g.TW + 2;
@@ -619,7 +623,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
         valid[ni] = n < g.TR * g.TW && oh0 + r < H && ow0 + c < W;
         const int rr = valid[ni] ? r : 0, cq = valid[ni] ? c : 0;
         hpb[ni] = MODE == 0 ? rr * HW2 + cq : (rr + 2) * HW2 + cq + 2;
-        col[ni] = (int64_t)b * HW + (int64_t)(oh0 + rr) * W + ow0 + cq;
+        col[ni] = (int64_t)(oh0 + rr) * W + ow0 + cq;  // (pixel inside sample b: the epilogue's bs)
         cnt_w += __popcll(__ballot(valid[ni]) & 0xffffffffull);
     }
 
@@ -674,7 +678,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
         }
         if (++th == 3) { th = 0; ++cc; }
     }
-    convn_epilogue<MODE, WM, WN, EP, NWC>(a, acc, smem, m0, M, col, valid, cnt_w, ntile, tn, tm);
+    convn_epilogue<MODE, WM, WN, EP, NWC>(a, acc, smem, m0, M, col, valid, cnt_w, ntile, tn, tm, b);
 }
 
 // ------------------------------------------------------------------ weight gradient
