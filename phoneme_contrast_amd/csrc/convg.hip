@@ -62,10 +62,10 @@ __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
     const int64_t nlog = mt * nt * (MODE == 2 ? a.nslice : 1), per = (nlog + 7) / 8;
     int64_t bid = (int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
     if (bid >= nlog) return;
-    const int64_t tm = bid % mt;
-    bid /= mt;
-    const int64_t tn = bid % nt;
-    const int slice = (int)(bid / nt);
+    const int64_t tq = udiv32(bid, mt), tm = bid - tq * mt;
+    bid = tq;
+    const int64_t tr_ = udiv32(bid, nt), tn = bid - tr_ * nt;
+    const int slice = (int)tr_;
     const int64_t m0 = tm * BM, n0 = tn * BN;
     int64_t k_begin = 0, k_end = K;
     if (MODE == 2) {
@@ -89,20 +89,20 @@ __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
         bvalid = m < N;
         const int64_t mm = bvalid ? m : 0;
         if (MODE == 3) {
-            const int64_t b = mm / CHW, p = mm - b * CHW;
-            const int ihc = (int)(p / IWc), iwc = (int)(p - (int64_t)(p / IWc) * IWc);
+            const int64_t b = udiv32(mm, CHW), p = mm - b * CHW;
+            const int ihc = (int)udiv32(p, IWc), iwc = (int)(p - (int64_t)ihc * IWc);
             xbase = b * a.cout * OHW;
             ih0 = 2 * ihc + ph + pad;
             iw0 = 2 * iwc + pw + pad;
         } else if (MODE == 0) {
-            const int64_t b = mm / OHW, p = mm - b * OHW;
-            const int oh = (int)(p / a.OW), ow = (int)(p - (int64_t)(p / a.OW) * a.OW);
+            const int64_t b = udiv32(mm, OHW), p = mm - b * OHW;
+            const int oh = (int)udiv32(p, a.OW), ow = (int)(p - (int64_t)oh * a.OW);
             xbase = b * a.cin * IHW;
             ih0 = oh * s - pad;
             iw0 = ow * s - pad;
         } else {
-            const int64_t b = mm / IHW, p = mm - b * IHW;
-            const int ih = (int)(p / a.IW), iw = (int)(p - (int64_t)(p / a.IW) * a.IW);
+            const int64_t b = udiv32(mm, IHW), p = mm - b * IHW;
+            const int ih = (int)udiv32(p, a.IW), iw = (int)(p - (int64_t)ih * a.IW);
             xbase = b * a.cout * OHW;
             ih0 = ih + pad;
             iw0 = iw + pad;
@@ -116,14 +116,14 @@ __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
     int64_t wco[MODE == 2 ? NBv : 1];
     if (MODE == 2) {
         const int64_t q = k_begin + kq;
-        pb = q / OHW;
+        pb = udiv32(q, OHW);
         const int64_t p = q - pb * OHW;
-        poh = (int)(p / a.OW);
+        poh = (int)udiv32(p, a.OW);
         pow_ = (int)(p - (int64_t)poh * a.OW);
 #pragma unroll
         for (int i = 0; i < NBv; ++i) {
             const int64_t jj = n0 + colq + 16 * i;
-            const int tap = (int)(jj / a.cin), c = (int)(jj - (int64_t)tap * a.cin);
+            const int tap = (int)udiv32(jj, a.cin), c = (int)(jj - (int64_t)tap * a.cin);
             const bool jv = jj < N;
             wkh[i] = jv ? tap / KW - pad : -(1 << 28);  // out of range: never loads
             wkw[i] = tap % KW - pad;
@@ -137,7 +137,7 @@ __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
         if (MODE == 0 || MODE == 1 || MODE == 3) {
             // A: weights, k = kbase + kq -> (tap, channel)
             const int64_t k = kbase + kq;
-            const int tap = (int)(k / CK), ch = (int)(k - (int64_t)tap * CK);
+            const int tap = (int)udiv32(k, CK), ch = (int)(k - (int64_t)tap * CK);
             const bool kv = k < K;
             if (a.wpack) {  // packed [M][K16] rows: 16 lanes read 64 contiguous bytes
                 const float* wp = static_cast<const float*>(a.wpack) + k;
@@ -162,7 +162,7 @@ __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
         }
         if (MODE == 0) {
             if (FK) {  // one tap per chunk
-                const int tap = (int)(kbase / CK), c0 = (int)(kbase - (int64_t)tap * CK);
+                const int tap = (int)udiv32(kbase, CK), c0 = (int)(kbase - (int64_t)tap * CK);
                 const int ih = ih0 + tap / KW, iw = iw0 + tap % KW;
                 const bool ok = bvalid && ih >= 0 && ih < a.IH && iw >= 0 && iw < a.IW;
                 const float* p = a.x + xbase + (int64_t)(c0 + brow) * IHW + (int64_t)ih * a.IW + iw;
@@ -174,7 +174,7 @@ __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
                     const int64_t kb = kbase + brow + BROWS * i;
                     float v = 0.f;
                     if (bvalid && kb < K) {
-                        const int tap = (int)(kb / CK), c = (int)(kb - (int64_t)tap * CK);
+                        const int tap = (int)udiv32(kb, CK), c = (int)(kb - (int64_t)tap * CK);
                         const int ih = ih0 + tap / KW, iw = iw0 + tap % KW;
                         if (ih >= 0 && ih < a.IH && iw >= 0 && iw < a.IW)
                             v = a.x[xbase + ((int64_t)c * a.IH + ih) * a.IW + iw];
@@ -196,7 +196,7 @@ __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
                 return ok && oh < a.OH && ow < a.OW;
             };
             if (FK) {
-                const int tap = (int)(kbase / CK), c0 = (int)(kbase - (int64_t)tap * CK);
+                const int tap = (int)udiv32(kbase, CK), c0 = (int)(kbase - (int64_t)tap * CK);
                 int oh = 0, ow = 0;
                 const bool ok = bvalid && src(tap, oh, ow);
                 const float* p = a.dy + xbase + (int64_t)(c0 + brow) * OHW + (int64_t)oh * a.OW + ow;
@@ -208,7 +208,7 @@ __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
                     const int64_t kb = kbase + brow + BROWS * i;
                     float v = 0.f;
                     if (bvalid && kb < K) {
-                        const int tap = (int)(kb / CK), nn = (int)(kb - (int64_t)tap * CK);
+                        const int tap = (int)udiv32(kb, CK), nn = (int)(kb - (int64_t)tap * CK);
                         int oh = 0, ow = 0;
                         if (src(tap, oh, ow)) v = a.dy[xbase + ((int64_t)nn * a.OH + oh) * a.OW + ow];
                     }
@@ -217,7 +217,7 @@ __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
             }
         } else if (MODE == 3) {
             if (FK) {
-                const int tap = (int)(kbase / CK), c0 = (int)(kbase - (int64_t)tap * CK);
+                const int tap = (int)udiv32(kbase, CK), c0 = (int)(kbase - (int64_t)tap * CK);
                 const int oh = (ih0 - (kh0 + 2 * (tap / ntw))) >> 1, ow = (iw0 - (kw0 + 2 * (tap % ntw))) >> 1;
                 const bool ok = bvalid && oh >= 0 && ow >= 0 && oh < a.OH && ow < a.OW;
                 const float* p = a.dy + xbase + (int64_t)(c0 + brow) * OHW + (int64_t)oh * a.OW + ow;
@@ -229,7 +229,7 @@ __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
                     const int64_t kb = kbase + brow + BROWS * i;
                     float v = 0.f;
                     if (bvalid && kb < K) {
-                        const int tap = (int)(kb / CK), nn = (int)(kb - (int64_t)tap * CK);
+                        const int tap = (int)udiv32(kb, CK), nn = (int)(kb - (int64_t)tap * CK);
                         const int oh = (ih0 - (kh0 + 2 * (tap / ntw))) >> 1, ow = (iw0 - (kw0 + 2 * (tap % ntw))) >> 1;
                         if (oh >= 0 && ow >= 0 && oh < a.OH && ow < a.OW)
                             v = a.dy[xbase + ((int64_t)nn * a.OH + oh) * a.OW + ow];
@@ -322,26 +322,26 @@ __global__ __launch_bounds__(256) void convg_kernel(ConvGArgs a) {
         int64_t ostride;  // distance between consecutive rows (M index)
         float* dst = a.out;
         if (MODE == 0) {
-            const int64_t b = col / OHW;
+            const int64_t b = udiv32(col, OHW);
             obase = b * a.cout * OHW + (col - b * OHW);
             ostride = OHW;
         } else if (MODE == 1) {
-            const int64_t b = col / IHW;
+            const int64_t b = udiv32(col, IHW);
             obase = b * a.cin * IHW + (col - b * IHW);
             ostride = IHW;
         } else if (MODE == 3) {
-            const int64_t b = col / CHW, p = col - b * CHW;
+            const int64_t b = udiv32(col, CHW), p = col - b * CHW;
             if (a.par_out) {  // dense class planes
                 dst = a.par_out;
                 obase = b * a.cin * CHW + p;
                 ostride = CHW;
             } else {
-                const int ihc = (int)(p / IWc), iwc = (int)(p - (int64_t)(p / IWc) * IWc);
+                const int ihc = (int)udiv32(p, IWc), iwc = (int)(p - (int64_t)ihc * IWc);
                 obase = b * a.cin * IHW + (int64_t)(2 * ihc + ph) * a.IW + 2 * iwc + pw;
                 ostride = IHW;
             }
         } else {  // column (tap, c) -> the reference weight layout [cout][cin][KH][KW]
-            const int tap = (int)(col / a.cin), c = (int)(col - (int64_t)tap * a.cin);
+            const int tap = (int)udiv32(col, a.cin), c = (int)(col - (int64_t)tap * a.cin);
             obase = (int64_t)slice * M * N + (int64_t)c * KK + tap;
             ostride = N;
         }
@@ -993,6 +993,10 @@ int launch_convg(ConvGArgs a, hipStream_t s) {
         M = a.cin;
         N = a.B * (int64_t)((a.IH - (a.par >> 1) + 1) / 2) * ((a.IW - (a.par & 1) + 1) / 2);
     } else { M = a.cout; N = (int64_t)a.cin * a.KH * a.KW; }
+    // the kernel's index arithmetic divides in 32 bits (udiv32): pixels, columns, K indices and block ids < 2^31
+    PCX_CHECK_ARG((int64_t)a.B * std::max(IHW, OHW) < ((int64_t)1 << 31) && N < ((int64_t)1 << 31) &&
+                      (int64_t)std::max(a.cin, a.cout) * a.KH * a.KW < ((int64_t)1 << 31),
+                  "convg: %lld x %lld problem exceeds 32-bit indexing", (long long)M, (long long)N);
     // narrow weight-gradient GEMMs (stem 7x7 of one channel: N = 49; 1x1 shortcuts of <= 64
     // channels) take 64-column tiles: a 128-column tile would multiply mostly padding
     const int wm = M >= 128 ? 2 : 1, wn = (a.mode == 2 && N <= 64 && (a.KH == 7 || a.KH == 1)) ? 1 : 2;

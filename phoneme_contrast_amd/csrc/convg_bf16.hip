@@ -104,10 +104,10 @@ __global__ __launch_bounds__(256) void convg_bf16_kernel(ConvGArgs a) {
     else { M = a.cout; N = (int64_t)a.cin * KK; K = a.B * OHW; }
     const int64_t mt = (M + BM - 1) / BM, nt = (N + BN - 1) / BN;
     int64_t bid = blockIdx.x;
-    const int64_t tm = bid % mt;
-    bid /= mt;
-    const int64_t tn = bid % nt;
-    const int slice = (int)(bid / nt);
+    const int64_t tq_ = udiv32(bid, mt), tm = bid - tq_ * mt;  // (32-bit index division: pcx_common.h)
+    bid = tq_;
+    const int64_t tr_ = udiv32(bid, nt), tn = bid - tr_ * nt;
+    const int slice = (int)tr_;
     const int64_t m0 = tm * BM, n0 = tn * BN;
     int64_t k_begin = 0, k_end = K;
     if (MODE == 2) {
@@ -128,20 +128,20 @@ __global__ __launch_bounds__(256) void convg_bf16_kernel(ConvGArgs a) {
     if (MODE == 0 || MODE == 1 || MODE == 3) {
         const int64_t mm = bvalid ? brow : 0;
         if (MODE == 3) {
-            const int64_t b = mm / CHW, p = mm - b * CHW;
-            const int ihc = (int)(p / IWc), iwc = (int)(p - (int64_t)(p / IWc) * IWc);
+            const int64_t b = udiv32(mm, CHW), p = mm - b * CHW;
+            const int ihc = (int)udiv32(p, IWc), iwc = (int)(p - (int64_t)ihc * IWc);
             xbase = b * a.cout * OHW;
             ih0 = 2 * ihc + ph + pad;
             iw0 = 2 * iwc + pw + pad;
         } else if (MODE == 0) {
-            const int64_t b = mm / OHW, p = mm - b * OHW;
-            const int oh = (int)(p / a.OW), ow = (int)(p - (int64_t)(p / a.OW) * a.OW);
+            const int64_t b = udiv32(mm, OHW), p = mm - b * OHW;
+            const int oh = (int)udiv32(p, a.OW), ow = (int)(p - (int64_t)oh * a.OW);
             xbase = b * a.cin * IHW;
             ih0 = oh * s - pad;
             iw0 = ow * s - pad;
         } else {
-            const int64_t b = mm / IHW, p = mm - b * IHW;
-            const int ih = (int)(p / a.IW), iw = (int)(p - (int64_t)(p / a.IW) * a.IW);
+            const int64_t b = udiv32(mm, IHW), p = mm - b * IHW;
+            const int ih = (int)udiv32(p, a.IW), iw = (int)(p - (int64_t)ih * a.IW);
             xbase = b * a.cout * OHW;
             ih0 = ih + pad;
             iw0 = iw + pad;
@@ -155,14 +155,14 @@ __global__ __launch_bounds__(256) void convg_bf16_kernel(ConvGArgs a) {
     int boff[MODE == 2 ? MB2 : 1], bkhw[MODE == 2 ? MB2 : 1];
     if (MODE == 2) {
         const int64_t q = k_begin + 2 * kq2;
-        p2.b = q / OHW;
+        p2.b = udiv32(q, OHW);
         const int64_t r = q - p2.b * OHW;
-        p2.oh = (int)(r / a.OW);
+        p2.oh = (int)udiv32(r, a.OW);
         p2.ow = (int)(r - (int64_t)p2.oh * a.OW);
 #pragma unroll
         for (int i = 0; i < MB2; ++i) {
             const int64_t jj = n0 + rq + 16 * i;
-            const int tap = (int)(jj / a.cin), c = (int)(jj - (int64_t)tap * a.cin);
+            const int tap = (int)udiv32(jj, a.cin), c = (int)(jj - (int64_t)tap * a.cin);
             const int kh = tap / KW - pad, kw = tap % KW - pad;
             boff[i] = (int)(c * IHW) + kh * a.IW + kw;
             // (kh, kw) for the bounds test; columns past N get kh far out of range (never load)
@@ -183,7 +183,7 @@ __global__ __launch_bounds__(256) void convg_bf16_kernel(ConvGArgs a) {
 #pragma unroll
                 for (int q = 0; q < NA / 8; ++q) rap[q] = avalid ? src[q] : bf16x8{};
             } else if (FK) {
-                const int tap = (int)(kbase / CK), ch0 = (int)(k0 - (int64_t)tap * CK);
+                const int tap = (int)udiv32(kbase, CK), ch0 = (int)(k0 - (int64_t)tap * CK);
                 const float* wp;
                 int64_t wst;
                 if (MODE == 0) { wp = a.w + (arow * a.cin + ch0) * KK + tap; wst = KK; }
@@ -200,7 +200,7 @@ __global__ __launch_bounds__(256) void convg_bf16_kernel(ConvGArgs a) {
                     const int64_t k = k0 + j;
                     float v = 0.f;
                     if (avalid && k < K) {
-                        const int tap = (int)(k / CK), ch = (int)(k - (int64_t)tap * CK);
+                        const int tap = (int)udiv32(k, CK), ch = (int)(k - (int64_t)tap * CK);
                         if (MODE == 0) v = a.w[(arow * a.cin + ch) * KK + tap];
                         else if (MODE == 1) v = a.w[((int64_t)ch * a.cin + arow) * KK + tap];
                         else
@@ -213,7 +213,7 @@ __global__ __launch_bounds__(256) void convg_bf16_kernel(ConvGArgs a) {
             // ---- B: activations (mode 0) / output gradients (modes 1, 3) of pixel brow
             const int64_t kb0 = kbase + bkg * NB;
             if (FK) {
-                const int tap = (int)(kbase / CK), c0 = (int)(kb0 - (int64_t)tap * CK);
+                const int tap = (int)udiv32(kbase, CK), c0 = (int)(kb0 - (int64_t)tap * CK);
                 int ih, iw;
                 bool ok;
                 const float* src;
@@ -253,7 +253,7 @@ __global__ __launch_bounds__(256) void convg_bf16_kernel(ConvGArgs a) {
                     const int64_t k = kb0 + i;
                     float v = 0.f;
                     if (bvalid && k < K) {
-                        const int tap = (int)(k / CK), ch = (int)(k - (int64_t)tap * CK);
+                        const int tap = (int)udiv32(k, CK), ch = (int)(k - (int64_t)tap * CK);
                         if (MODE == 0) {
                             const int ih = ih0 + tap / KW, iw = iw0 + tap % KW;
                             if (ih >= 0 && ih < a.IH && iw >= 0 && iw < a.IW)
@@ -380,20 +380,20 @@ __global__ __launch_bounds__(256) void convg_bf16_kernel(ConvGArgs a) {
         if (col >= N) continue;
         int64_t obase, ostride;
         if (MODE == 0) {
-            const int64_t b = col / OHW;
+            const int64_t b = udiv32(col, OHW);
             obase = b * a.cout * OHW + (col - b * OHW);
             ostride = OHW;
         } else if (MODE == 1) {
-            const int64_t b = col / IHW;
+            const int64_t b = udiv32(col, IHW);
             obase = b * a.cin * IHW + (col - b * IHW);
             ostride = IHW;
         } else if (MODE == 3) {
-            const int64_t b = col / CHW, p = col - b * CHW;
-            const int ihc = (int)(p / IWc), iwc = (int)(p - (int64_t)(p / IWc) * IWc);
+            const int64_t b = udiv32(col, CHW), p = col - b * CHW;
+            const int ihc = (int)udiv32(p, IWc), iwc = (int)(p - (int64_t)ihc * IWc);
             obase = b * a.cin * IHW + (int64_t)(2 * ihc + ph) * a.IW + 2 * iwc + pw;
             ostride = IHW;
         } else {
-            const int tap = (int)(col / a.cin), c = (int)(col - (int64_t)tap * a.cin);
+            const int tap = (int)udiv32(col, a.cin), c = (int)(col - (int64_t)tap * a.cin);
             obase = (int64_t)slice * M * N + (int64_t)c * KK + tap;
             ostride = N;
         }
@@ -426,6 +426,10 @@ int launch_convg_bf16(ConvGArgs a, hipStream_t s) {
     const int64_t mt = ceil_div(M, 64 * wm), nt = ceil_div(N, 128);
     const int64_t nblocks = mt * nt * (a.mode == 2 ? a.nslice : 1);
     PCX_CHECK_ARG(nblocks < ((int64_t)1 << 31), "convg_bf16: grid too large");
+    // (32-bit index divisions in the kernel: udiv32)
+    PCX_CHECK_ARG((int64_t)a.B * std::max(IHW, OHW) < ((int64_t)1 << 31) && N < ((int64_t)1 << 31) &&
+                      (int64_t)std::max(a.cin, a.cout) * a.KH * a.KW < ((int64_t)1 << 31),
+                  "convg_bf16: %lld x %lld problem exceeds 32-bit indexing", (long long)M, (long long)N);
     if (a.mode == 2) PCX_CHECK_ARG(a.kslice % KB == 0 && a.nslice >= 1, "convg_bf16: bad weight-gradient split");
     // (mode 2 reuses the flag: false = dy computed as the BN backward of (bn_g, bn_y) while staging)
     const bool fk = a.mode == 2 ? a.bn_g == nullptr : (a.mode == 0 ? a.cin : a.cout) % KB == 0;

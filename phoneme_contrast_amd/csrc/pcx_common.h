@@ -67,6 +67,13 @@ inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
 }  // namespace pcx
 
+// nonnegative n / d in 32 bits, for index arithmetic whose operands the launcher has checked to be < 2^31 (round 6:
+// an int64 division compiles to ~100 scalar or ~60 vector instructions; convg / convg_bf16 did several per block and
+// per K-chunk and lane)
+namespace pcx {
+__host__ __device__ __forceinline__ int64_t udiv32(int64_t n, int64_t d) { return (int64_t)((unsigned)n / (unsigned)d); }
+}  // namespace pcx
+
 // ---------------------------------------------------------------- A/B alternates (analysis builds only)
 // The measured-and-superseded alternates of the product kernels (the round-4/5 A/B comparisons in DESIGN.md)
 // are compile-time switches: `make AB="-DPCX_AB_NO_WGBD=1"` builds a library that takes the old path.  The
