@@ -146,19 +146,21 @@ __device__ __forceinline__ float row16_xsel8(const float (&v)[8], int n) {
 // output plane: lanes keep byte offsets, an element outside the image gets an offset past num_records (the
 // hardware drops the store), the channel's plane offset rides in soffset.
 constexpr unsigned WOOB = 0x80000000u;  // masked element offset (> every num_records used)
+// epilogue stores stream (cache policy nt on gfx950; round 6): every output tensor is GBs, read by the next kernel
+constexpr int WST = PCX_AB_NO_NT_STORES ? 0 : 2;
 typedef unsigned u32x2w __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4w __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void bst1(__amdgpu_buffer_rsrc_t r, unsigned vo, int so, float x) {
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), r, vo, so, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), r, vo, so, WST);
 }
 __device__ __forceinline__ void bst2(__amdgpu_buffer_rsrc_t r, unsigned vo, int so, float x, float y) {
     __builtin_amdgcn_raw_buffer_store_b64(u32x2w{__builtin_bit_cast(unsigned, x), __builtin_bit_cast(unsigned, y)}, r,
-                                          vo, so, 0);
+                                          vo, so, WST);
 }
 __device__ __forceinline__ void bst4(__amdgpu_buffer_rsrc_t r, unsigned vo, int so, float x, float y, float z, float w) {
     __builtin_amdgcn_raw_buffer_store_b128(u32x4w{__builtin_bit_cast(unsigned, x), __builtin_bit_cast(unsigned, y),
                                                   __builtin_bit_cast(unsigned, z), __builtin_bit_cast(unsigned, w)},
-                                           r, vo, so, 0);
+                                           r, vo, so, WST);
 }
 __device__ __forceinline__ float2 bld2(__amdgpu_buffer_rsrc_t r, unsigned vo, int so) {
     const u32x2w t = __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0);

@@ -488,8 +488,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void w
                             rz[k2] += dz[e];
                             rx_[k2] = fmaf(dz[e], xh[e], rx_[k2]);
                         }
-                        *reinterpret_cast<float2*>(a.dzp + o) = make_float2(dz[0], dz[1]);
-                        if (r1ok) *reinterpret_cast<float2*>(a.dzp + o + W) = make_float2(dz[2], dz[3]);
+                        if constexpr (PCX_AB_NO_NT_STORES) {
+                            *reinterpret_cast<float2*>(a.dzp + o) = make_float2(dz[0], dz[1]);
+                            if (r1ok) *reinterpret_cast<float2*>(a.dzp + o + W) = make_float2(dz[2], dz[3]);
+                        } else {  // (streaming stores: dz_prev is read once, by the layer-1 weight gradient)
+                            __builtin_nontemporal_store(f2{dz[0], dz[1]}, reinterpret_cast<f2*>(a.dzp + o));
+                            if (r1ok) __builtin_nontemporal_store(f2{dz[2], dz[3]}, reinterpret_cast<f2*>(a.dzp + o + W));
+                        }
                     }
                 }
             }

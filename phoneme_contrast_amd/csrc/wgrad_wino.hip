@@ -66,12 +66,12 @@ __device__ __forceinline__ vecf<V> bload(__amdgpu_buffer_rsrc_t r, int voff) {
 template <int V>
 __device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int voff, vecf<V> v) {
     if constexpr (V == 4)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, voff, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, voff, 0, PCX_AB_NO_NT_STORES ? 0 : 2);
     else if constexpr (V == 2)
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, voff, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, voff, 0, PCX_AB_NO_NT_STORES ? 0 : 2);
     else {
         const float f = v.x;  // (a named copy: no bit_cast of a vector-lane lvalue)
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, f), r, voff, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, f), r, voff, 0, PCX_AB_NO_NT_STORES ? 0 : 2);
     }
 }
 
