@@ -550,7 +550,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     if (MODE == 0) { CK = a.cin; H = a.OH; W = a.OW; M = a.cout; }
     else { CK = a.cout; H = a.IH; W = a.IW; M = a.cin; }
     Hp = H + 2; Wp = W + 2;
-    const int64_t HW = (int64_t)H * W;
     // (32-bit tile decode, host-checked mt * ntile < 2^31: the int64 divisions were ~100 scalar instructions each)
     const int tps = g.nsr * g.nsc;
     const int mt = (int)((M + BM - 1) / BM), ntile = a.B * tps;

@@ -136,7 +136,8 @@ int build_deep(Plan& p) {
     auto plan_routed = [&](int ci, int co, int h, int w, bool* fwd, bool* w32, WgradArgs* wga, int* nblk,
                            bool* ww, WinoWgradArgs* wwa) {
         *fwd = route && (co == 32 || co % 64 == 0) && (ci == 32 || ci % 64 == 0) && ci % 2 == 0;
-        // the Winograd weight gradient at even widths; else the pixel-stream kernel from 50 columns
+        // the Winograd weight gradient wherever its geometry takes the shape (even widths; odd widths past its
+        // tile-coverage gate: 5 x 25, not 3 x 13); else the pixel-stream kernel from 50 columns
         // up (narrower rows waste its 8-column stream granule: the 32x32 row-window kernel takes them)
         *ww = route && wgrad_wino_geometry(B, h, w, ci, co, wwa);
         if (*ww) wg = std::max(wg, (size_t)wwa->nslice * co * ci * 16);
