@@ -139,6 +139,9 @@ __host__ __device__ __forceinline__ int64_t udiv32(int64_t n, int64_t d) { retur
 #ifndef PCX_AB_NO_NT_STORES       // 1: plain (not streaming) output stores in conv_wino / wgrad_wino / wgbd_wino (nt measured 2 % slower)
 #define PCX_AB_NO_NT_STORES 1
 #endif
+#ifndef PCX_AB_SUPCON_DWORD       // 1: SupCon gradient B operands by dword loads (feature 32 q + n)
+#define PCX_AB_SUPCON_DWORD 0
+#endif
 #ifndef PCX_AB_BN_NO_SPLIT        // 1: one block per channel in the BN finalisers (no split + merge)
 #define PCX_AB_BN_NO_SPLIT 0
 #endif

@@ -129,14 +129,17 @@ __global__ __launch_bounds__(256) void supcon_rows_partial(
 // rowstats[i] = {m_i, den_i, msum_i, loss_i} for the nrows anchors of the range; loss_out reduced
 // per `reduction` over the range, the mean taken over all B anchors of the batch (a range's value
 // is its share of the batch mean; the shares of a partition sum to the mean).
-__global__ __launch_bounds__(256) void supcon_rows_finalize(const RowPart* __restrict__ part,
+// (one block of FIN_T threads: the loss is one fixed-order tree sum; 1024 threads instead of 256 cut the
+// per-thread chain of row merges 4x, 44 -> ~15 us at B = 4096)
+constexpr int FIN_T = 1024;
+__global__ __launch_bounds__(FIN_T) void supcon_rows_finalize(const RowPart* __restrict__ part,
                                                              int nsplit, int64_t B, int64_t nrows,
                                                              float t_over_bt, int reduction,
                                                              float4* __restrict__ rowstats,
                                                              float* __restrict__ loss_out) {
-    __shared__ float red[256];
+    __shared__ float red[FIN_T];
     float acc = 0.f;
-    for (int64_t i = threadIdx.x; i < nrows; i += blockDim.x) {
+    for (int64_t i = threadIdx.x; i < nrows; i += FIN_T) {
         RowPart q = part[i];
         for (int sp = 1; sp < nsplit; ++sp) q = merge(q, part[(int64_t)sp * nrows + i]);
         float den = q.s + 1e-6f;
@@ -149,7 +152,7 @@ __global__ __launch_bounds__(256) void supcon_rows_finalize(const RowPart* __res
     }
     red[threadIdx.x] = acc;
     __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
+    for (int o = FIN_T / 2; o > 0; o >>= 1) {
         if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
         __syncthreads();
     }
@@ -211,15 +214,39 @@ __global__ __launch_bounds__(256) void supcon_grad_partial(
             hv[r] = v;
         }
         // dF_i += sum_j H_ij F_j : A = H (lane = anchor i, k = j of register r), B = F_j rows
+        // (accumulator column n of sub-tile q is feature NQ n + q: the lane's NQ B values of a row are
+        // consecutive floats, one 8- / 16-byte load per row instead of NQ dword loads; PCX_AB_SUPCON_DWORD:
+        // feature 32 q + n, dword loads)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             int64_t j = jb * TILE + acc_row(r, h);
-            const float* fj = F + j * D + (lane & 31);
             bool jv = j < B;
+            if constexpr (PCX_AB_SUPCON_DWORD) {
+                const float* fj = F + j * D + (lane & 31);
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                float b = jv ? fj[32 * q] : 0.f;
-                acc[q] = mfma32(hv[r], b, acc[q]);
+                for (int q = 0; q < NQ; ++q) {
+                    float b = jv ? fj[32 * q] : 0.f;
+                    acc[q] = mfma32(hv[r], b, acc[q]);
+                }
+            } else {
+                const float* fj = F + j * D + NQ * (lane & 31);
+                float b[NQ];
+#pragma unroll
+                for (int q4 = 0; q4 < NQ; q4 += 4) {
+                    if constexpr (NQ == 2) {
+                        const float2 v = jv ? *reinterpret_cast<const float2*>(fj) : make_float2(0.f, 0.f);
+                        b[0] = v.x;
+                        b[1] = v.y;
+                    } else {
+                        const float4 v = jv ? ld4(fj + q4) : make_float4(0.f, 0.f, 0.f, 0.f);
+                        b[q4] = v.x;
+                        b[q4 + 1] = v.y;
+                        b[q4 + 2] = v.z;
+                        b[q4 + 3] = v.w;
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) acc[q] = mfma32(hv[r], b[q], acc[q]);
             }
         }
     }
@@ -231,7 +258,7 @@ __global__ __launch_bounds__(256) void supcon_grad_partial(
             for (int q = 0; q < NQ; ++q)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    float* dst = &red[acc_row(r, h)][32 * q + (lane & 31)];
+                    float* dst = &red[acc_row(r, h)][PCX_AB_SUPCON_DWORD ? 32 * q + (lane & 31) : NQ * (lane & 31) + q];
                     *dst = (w == 0) ? acc[q][r] : *dst + acc[q][r];
                 }
         }
@@ -355,7 +382,7 @@ extern "C" int pcx_supcon_forward_rows(const float* F, const int64_t* labels, co
     RowPart* part = static_cast<RowPart*>(ws);
     launch_rows_partial(F, labels, mask, B, D, row0, nrows, temperature, part, g, stream);
     PCX_LAUNCH_CHECK("supcon_rows_partial");
-    supcon_rows_finalize<<<1, 256, 0, stream>>>(part, g.nsplit, B, nrows, temperature / base_temperature,
+    supcon_rows_finalize<<<1, FIN_T, 0, stream>>>(part, g.nsplit, B, nrows, temperature / base_temperature,
                                                  reduction, reinterpret_cast<float4*>(rowstats), loss_out);
     PCX_LAUNCH_CHECK("supcon_rows_finalize");
     return PCX_OK;
