@@ -142,6 +142,9 @@ __host__ __device__ __forceinline__ int64_t udiv32(int64_t n, int64_t d) { retur
 #ifndef PCX_AB_SUPCON_DWORD       // 1: SupCon gradient B operands by dword loads (feature 32 q + n)
 #define PCX_AB_SUPCON_DWORD 0
 #endif
+#ifndef PCX_AB_SUPCON_NOFRAG      // 1: SupCon kernels reload the anchor rows' B fragments per tile
+#define PCX_AB_SUPCON_NOFRAG 0
+#endif
 #ifndef PCX_AB_BN_NO_SPLIT        // 1: one block per channel in the BN finalisers (no split + merge)
 #define PCX_AB_BN_NO_SPLIT 0
 #endif

@@ -58,6 +58,39 @@ __device__ __forceinline__ f32x16 tile_s(const float* __restrict__ F, int64_t rj
     return acc;
 }
 
+// the same tile with the anchor row's B fragments held in registers (loaded once per kernel instead of once per
+// tile: D <= 128, 16 float4 per lane)
+template <int D>
+struct AnchorFrag {
+    float4 b[D / 8];
+    __device__ __forceinline__ void load(const float* __restrict__ F, int64_t ri, int64_t B, int h) {
+        const float* pb = F + ri * D + 4 * h;
+#pragma unroll
+        for (int s = 0; s < D / 8; ++s) b[s] = ri < B ? ld4(pb + 8 * s) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+};
+template <int D>
+__device__ __forceinline__ f32x16 tile_s_frag(const float* __restrict__ F, int64_t rj, const AnchorFrag<D>& fi,
+                                              int64_t B, int h) {
+    f32x16 acc = {0.f};
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* pa = F + rj * D + 4 * h;
+    const bool va = rj < B;
+#pragma unroll
+    for (int s = 0; s < D / 8; ++s) {
+        const float4 a = va ? ld4(pa + 8 * s) : z;
+        acc = mfma32(a.x, fi.b[s].x, acc);
+        acc = mfma32(a.y, fi.b[s].y, acc);
+        acc = mfma32(a.z, fi.b[s].z, acc);
+        acc = mfma32(a.w, fi.b[s].w, acc);
+    }
+    return acc;
+}
+// anchor fragments in registers where they fit, in the gradient kernel (PCX_AB_SUPCON_NOFRAG: reload per tile;
+// 143 -> 136 us at B = 4096, profiles/r6s2_supcon.txt)
+template <int D>
+constexpr bool kFrag = D <= 128 && !PCX_AB_SUPCON_NOFRAG;
+
 __device__ __forceinline__ float pos_weight(const int64_t* __restrict__ labels,
                                             const float* __restrict__ mask, int64_t B, int64_t i,
                                             int64_t j, int64_t li) {
@@ -80,6 +113,7 @@ __global__ __launch_bounds__(256) void supcon_rows_partial(
     RowPart p = {-INFINITY, 0.f, 0.f, 0.f};
     const int64_t jb0 = (int64_t)blockIdx.y * jblk_per_split;
     const int64_t jb1 = min(nj, jb0 + jblk_per_split);
+    // (anchor fragments reloaded per tile here: held in registers this kernel measured 74 -> 78 us at B = 4096)
     for (int64_t jb = jb0 + wave; jb < jb1; jb += WAVES) {
         f32x16 acc = tile_s<D>(F, jb * TILE + (lane & 31), i, B, h);
         if (ivalid) {
@@ -197,8 +231,12 @@ __global__ __launch_bounds__(256) void supcon_grad_partial(
 
     const int64_t jb0 = (int64_t)blockIdx.y * jblk_per_split;
     const int64_t jb1 = min(nj, jb0 + jblk_per_split);
+    AnchorFrag<kFrag<D> ? D : 8> fi;
+    if constexpr (kFrag<D>) fi.load(F, i, B, h);
     for (int64_t jb = jb0 + wave; jb < jb1; jb += WAVES) {
-        f32x16 s = tile_s<D>(F, jb * TILE + (lane & 31), i, B, h);
+        f32x16 s;
+        if constexpr (kFrag<D>) s = tile_s_frag<D>(F, jb * TILE + (lane & 31), fi, B, h);
+        else s = tile_s<D>(F, jb * TILE + (lane & 31), i, B, h);
         float hv[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
