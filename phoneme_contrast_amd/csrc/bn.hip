@@ -115,6 +115,7 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(BnBwdArgs a) {
         const float g = a.gamma ? a.gamma[c] : 1.f;
         if (a.dbeta) a.dbeta[c] = (float)d0;
         if (a.dgamma) a.dgamma[c] = (float)d1;
+        if (a.zero) a.zero[c] = 0.f;
         // dy = g*invstd*(dz - dbeta/N - xhat*dgamma/N),  xhat = (y - mean)*invstd
         float ac = g * f.w;
         a.cf[c] = make_float4(ac, (float)(d0 / a.count), (float)(d1 / a.count) * f.w, f.z);
@@ -266,6 +267,7 @@ __global__ __launch_bounds__(64) void bn_bwd_merge_kernel(BnBwdArgs a, int R, in
     const float g = a.gamma ? a.gamma[c] : 1.f;
     if (a.dbeta) a.dbeta[c] = (float)d0;
     if (a.dgamma) a.dgamma[c] = (float)d1;
+    if (a.zero) a.zero[c] = 0.f;
     a.cf[c] = make_float4(g * f.w, (float)(d0 / a.count), (float)(d1 / a.count) * f.w, f.z);
 }
 

@@ -284,6 +284,8 @@ struct BnBwdArgs {
     float* dgamma;
     float* dbeta;
     float4* cf;           // out {a, mb, mgi, mean}
+    float* zero;          // or NULL: C floats set to 0 (the producing conv's bias gradient: exactly 0 before a
+                          // train-mode BN), instead of a memset launch
 };
 int launch_bn_bwd_finalize(BnBwdArgs a, hipStream_t s);
 

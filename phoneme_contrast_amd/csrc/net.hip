@@ -361,6 +361,9 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
         f.dgamma = G[p_bn_g(l)];
         f.dbeta = G[p_bn_b(l)];
         f.cf = at<float4>(ws, L.cfb);
+        // conv l's bias feeds this train-mode BN: its exact gradient is zero (sum over b, h, w of the BN
+        // backward), written here before layer l's weight gradient marks its bucket (no memset launch)
+        f.zero = G[p_conv_b(l)];
         Scope sc(&p.prof, s, "bn_bwd_finalize");
         return launch_bn_bwd_finalize(f, s);
     };
@@ -369,8 +372,6 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
     for (int l = 6; l >= 2; --l) {
         const Layer& L = p.L[l];
         const Layer& Lp = p.L[l - 1];
-        // conv bias feeding a train-mode BN: exact gradient is zero (sum_b,h,w of BN-backward)
-        RC(hip_status_ok(hipMemsetAsync(G[p_conv_b(l)], 0, L.cout * 4, s), "memset bias grad"));
         if (L.wgbd) {  // ---- weight and data gradient in one pass (dy never materialised)
             RC(launch_wino_pack(P[p_conv_w(l)], at<float>(ws, L.wud), L.cin, L.cout, 1, s));
             WinoBwdArgs w = L.wb;
@@ -499,7 +500,6 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
     // layer 1 weight gradient (input has one channel)
     {
         const Layer& L = p.L[1];
-        RC(hip_status_ok(hipMemsetAsync(G[p_conv_b(1)], 0, L.cout * 4, s), "memset bias grad"));
         Wgrad1Args w{};
         w.B = B; w.H = L.H; w.W = L.W; w.cout = L.cout;
         w.dz = at<float>(ws, L.dz);
