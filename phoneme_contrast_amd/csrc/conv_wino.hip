@@ -1056,9 +1056,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
 
 // U = G g G^T per (GEMM output channel m, GEMM input channel k), evaluated in float64.
 // flip: data-gradient GEMM of forward weights w[K][M][3][3] (g[m][k] = w[k][m] rotated 180 deg).
+__device__ __forceinline__ void wino_pack_one(const float* __restrict__ w, float* __restrict__ u, int M, int K, int flip,
+                                              int e);
 __global__ void wino_pack_kernel(const float* __restrict__ w, float* __restrict__ u, int M, int K, int flip) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= M * K) return;
+    wino_pack_one(w, u, M, K, flip, e);
+}
+// several packs in one launch (a network's layers: one launch per pass instead of one per layer)
+__global__ void wino_pack_multi_kernel(WinoPackJobs j) {
+    int e = blockIdx.x * blockDim.x + threadIdx.x;
+    for (int i = 0; i < j.n; ++i) {
+        const int n = j.M[i] * j.K[i];
+        if (e < n) {
+            wino_pack_one(j.w[i], j.u[i], j.M[i], j.K[i], j.flip[i], e);
+            return;
+        }
+        e -= n;
+    }
+}
+__device__ __forceinline__ void wino_pack_one(const float* __restrict__ w, float* __restrict__ u, int M, int K, int flip,
+                                              int e) {
     const int m = e / K, k = e - m * K;
     double gg[3][3];
     for (int r = 0; r < 3; ++r)
@@ -1152,6 +1170,20 @@ int launch_wino_pack(const float* w, float* u, int M, int K, int flip, hipStream
     const int n = M * K;
     wino_pack_kernel<<<ceil_div(n, 256), 256, 0, s>>>(w, u, M, K, flip);
     PCX_LAUNCH_CHECK("wino_pack_kernel");
+    return PCX_OK;
+}
+
+int launch_wino_pack_multi(const WinoPackJobs& j, hipStream_t s) {
+    PCX_CHECK_ARG(j.n >= 0 && j.n <= WinoPackJobs::MAXJ, "wino_pack_multi: %d packs", j.n);
+    int64_t n = 0;
+    for (int i = 0; i < j.n; ++i) {
+        PCX_CHECK_ARG(j.M[i] % 32 == 0, "wino_pack: %d output channels (multiple of 32 required)", j.M[i]);
+        n += (int64_t)j.M[i] * j.K[i];
+    }
+    PCX_CHECK_ARG(n < ((int64_t)1 << 30), "wino_pack_multi: %lld weights", (long long)n);
+    if (n == 0) return PCX_OK;
+    wino_pack_multi_kernel<<<ceil_div(n, 256), 256, 0, s>>>(j);
+    PCX_LAUNCH_CHECK("wino_pack_multi_kernel");
     return PCX_OK;
 }
 

@@ -87,6 +87,17 @@ bool wino_span_geometry(int B, int H, int W, int cin, int cout, WinoGeo* g);
 size_t wino_nblk(int B, int H, int W, int cin, int cout);
 // flip = 0: forward weights w[M][K][3][3]; flip = 1: data gradient of forward weights w[K][M][3][3]
 int launch_wino_pack(const float* w, float* u, int M, int K, int flip, hipStream_t s);
+struct WinoPackJobs {  // up to MAXJ launch_wino_pack calls in one launch
+    static constexpr int MAXJ = 8;
+    int n;
+    const float* w[MAXJ];
+    float* u[MAXJ];
+    int M[MAXJ], K[MAXJ], flip[MAXJ];
+    void add(const float* w_, float* u_, int M_, int K_, int flip_) {
+        w[n] = w_; u[n] = u_; M[n] = M_; K[n] = K_; flip[n] = flip_; ++n;
+    }
+};
+int launch_wino_pack_multi(const WinoPackJobs& j, hipStream_t s);
 int launch_conv3x3_wino(int pro, int epi, ConvArgs a, hipStream_t s);
 // materialised block tail x = drop * maxpool2(relu(y*s + t)) (feeds PRO_RAW convs)
 // ysel / parg (optional, both or neither): y at each window's first maximum of relu(y s + t) (torch's

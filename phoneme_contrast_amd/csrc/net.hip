@@ -204,11 +204,16 @@ int small_forward(const Plan& p, const float* const* P, float* const* bnstat, in
         { Scope sc(&p.prof, s, "conv1_fwd", 1); RC(launch_conv1_fwd(c, s)); }
         RC(finalize(1, L.nblk));
     }
+    {  // the Winograd layers' transformed weights, all in one launch
+        WinoPackJobs j{};
+        for (int l = 2; l <= 6; ++l)
+            if (p.L[l].wino) j.add(P[p_conv_w(l)], at<float>(ws, p.L[l].wu), p.L[l].cout, p.L[l].cin, 0);
+        RC(launch_wino_pack_multi(j, s));
+    }
     for (int l = 2; l <= 6; ++l) {
         const Layer& L = p.L[l];
         const Layer& Lp = p.L[l - 1];
-        if (L.wino) RC(launch_wino_pack(P[p_conv_w(l)], at<float>(ws, L.wu), L.cout, L.cin, 0, s));
-        else RC(launch_pack_fwd(P[p_conv_w(l)], at<float>(ws, L.wu), L.cout, L.cin, s));
+        if (!L.wino) RC(launch_pack_fwd(P[p_conv_w(l)], at<float>(ws, L.wu), L.cout, L.cin, s));
         ConvArgs c{};
         c.B = B; c.H = L.H; c.W = L.W; c.cin = L.cin; c.cout = L.cout;
         c.src = at<float>(ws, Lp.y);
@@ -368,12 +373,17 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
         return launch_bn_bwd_finalize(f, s);
     };
     RC(bwd_finalize(6, B, (double)B * p.P6));
+    {  // the flipped Winograd weights of every Winograd data gradient (fused or not), in one launch
+        WinoPackJobs j{};
+        for (int l = 6; l >= 2; --l)
+            if (p.L[l].wgbd || p.L[l].wino) j.add(P[p_conv_w(l)], at<float>(ws, p.L[l].wud), p.L[l].cin, p.L[l].cout, 1);
+        RC(launch_wino_pack_multi(j, s));
+    }
 
     for (int l = 6; l >= 2; --l) {
         const Layer& L = p.L[l];
         const Layer& Lp = p.L[l - 1];
         if (L.wgbd) {  // ---- weight and data gradient in one pass (dy never materialised)
-            RC(launch_wino_pack(P[p_conv_w(l)], at<float>(ws, L.wud), L.cin, L.cout, 1, s));
             WinoBwdArgs w = L.wb;
             w.B = B; w.H = L.H; w.W = L.W;
             w.dz = at<float>(ws, L.dz);
@@ -455,8 +465,7 @@ int small_backward(const Plan& p, const float* const* P, const float* x, const f
         }
         // ---- data gradient -> dz of the previous BN (through ReLU / MaxPool / Dropout2d)
         {
-            if (L.wino) RC(launch_wino_pack(P[p_conv_w(l)], at<float>(ws, L.wud), L.cin, L.cout, 1, s));
-            else RC(launch_pack_dgrad(P[p_conv_w(l)], at<float>(ws, L.wud), L.cout, L.cin, s));
+            if (!L.wino) RC(launch_pack_dgrad(P[p_conv_w(l)], at<float>(ws, L.wud), L.cout, L.cin, s));
             float* dzp = at<float>(ws, Lp.dz);
             if (L.pooled_in && ((L.srcH & 1) || (L.srcW & 1)))
                 RC(hip_status_ok(hipMemsetAsync(dzp, 0, (size_t)B * Lp.cout * L.srcH * L.srcW * 4, s),
