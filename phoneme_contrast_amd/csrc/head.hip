@@ -524,7 +524,18 @@ __global__ __launch_bounds__(256) void proj_bwd_data_kernel(ProjArgs a) {
         float acc[PR];
 #pragma unroll
         for (int r = 0; r < PR; ++r) acc[r] = 0.f;
-        for (int d = 0; d < a.D; ++d) {
+        int d = 0;
+        if ((a.D & 3) == 0)  // (16-byte LDS reads of the rows' dh, as proj_fwd_kernel)
+            for (; d < a.D; d += 4) {
+                const float w0 = a.w[(int64_t)d * a.K + k], w1 = a.w[(int64_t)(d + 1) * a.K + k];
+                const float w2 = a.w[(int64_t)(d + 2) * a.K + k], w3 = a.w[(int64_t)(d + 3) * a.K + k];
+#pragma unroll
+                for (int r = 0; r < PR; ++r) {
+                    const float4 x = *reinterpret_cast<const float4*>(&sd[r * a.D + d]);
+                    acc[r] = fmaf(x.w, w3, fmaf(x.z, w2, fmaf(x.y, w1, fmaf(x.x, w0, acc[r]))));
+                }
+            }
+        for (; d < a.D; ++d) {
             const float w = a.w[(int64_t)d * a.K + k];
 #pragma unroll
             for (int r = 0; r < PR; ++r) acc[r] = fmaf(sd[r * a.D + d], w, acc[r]);
